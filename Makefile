@@ -1,0 +1,46 @@
+# Top-level build. `make` builds everything in-tree (the .so files travel to the
+# GPU box with the gpurun snapshot). gfx950 only.
+HIPCC   ?= /opt/rocm/bin/hipcc
+CLANGXX ?= /opt/rocm/llvm/bin/clang++
+ARCH    ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
+CSRC := bdls_amd/csrc
+LIB  := bdls_amd/lib
+
+HDRS := $(wildcard $(CSRC)/*.h) include/bdls_hip.h
+
+all: $(LIB)/libbdlship.so $(LIB)/libbdlsgen.so oracle tests/native/build/libhostsim.so
+
+$(LIB)/verify_kernels.o: $(CSRC)/verify_kernels.hip $(HDRS)
+	@mkdir -p $(LIB)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB)/bdls_hip.o: $(CSRC)/bdls_hip.cpp $(HDRS)
+	@mkdir -p $(LIB)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB)/libbdlship.so: $(LIB)/verify_kernels.o $(LIB)/bdls_hip.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
+
+$(LIB)/libbdlsgen.so: bdls_amd/workload/gen.c
+	@mkdir -p $(LIB)
+	gcc -O2 -fPIC -shared -Wall -o $@ $< -lcrypto -lpthread
+
+oracle:
+	$(MAKE) -C oracle
+
+# test-only host build of the device arithmetic (never linked into the product)
+tests/native/build/libhostsim.so: tests/native/hostsim.cpp $(HDRS)
+	@mkdir -p tests/native/build
+	$(CLANGXX) -O2 -std=c++17 -shared -fPIC -o $@ $<
+
+clean:
+	rm -rf $(LIB) tests/native/build
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean
+
+$(LIB)/ubench: $(CSRC)/ubench.hip $(HDRS)
+	@mkdir -p $(LIB)
+	$(HIPCC) $(HIPFLAGS) -o $@ $<
+all: $(LIB)/ubench

@@ -1,0 +1,100 @@
+"""ctypes binding of libbdlship.so (include/bdls_hip.h).
+
+The product path is the HIP library: if it is missing, or no gfx950 device is
+visible, every entry point raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libbdlship.so")
+
+BH_OK = 0
+BH_F_HASH_SHA256 = 1
+BH_F_NO_LOW_S = 2
+BH_CURVE_P256 = 0
+BH_CURVE_SECP256K1 = 1
+
+# Every symbol include/bdls_hip.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "bh_init", "bh_shutdown", "bh_device_count", "bh_last_error", "bh_version",
+    "bh_workspace_bytes", "bh_verify", "bh_verify_dev", "bh_csp_verify_p256",
+    "bh_parse_der_sig",
+)
+
+
+class BhBatch(ctypes.Structure):
+    _fields_ = [
+        ("pub", ctypes.c_void_p),
+        ("sig", ctypes.c_void_p),
+        ("sig_off", ctypes.c_void_p),
+        ("sig_len", ctypes.c_void_p),
+        ("msg", ctypes.c_void_p),
+        ("msg_off", ctypes.c_void_p),
+        ("msg_len", ctypes.c_void_p),
+    ]
+
+
+class BhTiming(ctypes.Structure):
+    _fields_ = [("prep_ms", ctypes.c_float), ("inv_ms", ctypes.c_float),
+                ("ladder_ms", ctypes.c_float)]
+
+
+class EngineError(RuntimeError):
+    """The HIP engine itself failed (no device, HIP error, bad arguments)."""
+
+
+_lib = None
+_init_lock = threading.Lock()
+_initialised = False
+
+
+def lib() -> ctypes.CDLL:
+    """Load libbdlship.so (no device access)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EngineError(f"{LIB_PATH} is not built (run `make` or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int
+        L.bh_init.argtypes = [u32, u32]
+        L.bh_init.restype = i32
+        L.bh_shutdown.restype = i32
+        L.bh_device_count.restype = i32
+        L.bh_last_error.restype = ctypes.c_char_p
+        L.bh_version.restype = ctypes.c_char_p
+        L.bh_workspace_bytes.argtypes = [sz]
+        L.bh_workspace_bytes.restype = sz
+        L.bh_verify.argtypes = [i32, ctypes.POINTER(BhBatch), sz, u32, vp, vp]
+        L.bh_verify.restype = i32
+        L.bh_verify_dev.argtypes = [i32, i32, ctypes.POINTER(BhBatch), sz, u32, vp, vp, vp, i32,
+                                    ctypes.POINTER(BhTiming)]
+        L.bh_verify_dev.restype = i32
+        L.bh_csp_verify_p256.argtypes = [vp, vp, sz, vp, sz, ctypes.POINTER(i32),
+                                         ctypes.POINTER(i32)]
+        L.bh_csp_verify_p256.restype = i32
+        L.bh_parse_der_sig.argtypes = [vp, sz, vp, vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+        L.bh_parse_der_sig.restype = i32
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != BH_OK:
+        raise EngineError(f"libbdlship error {rc}: {lib().bh_last_error().decode(errors='replace')}")
+
+
+def ensure_init(device_mask: int = 0) -> None:
+    """bh_init on first use; raises EngineError without a gfx950 device."""
+    global _initialised
+    with _init_lock:
+        if not _initialised:
+            check(lib().bh_init(device_mask, 0))
+            _initialised = True
+
+
+def last_error() -> str:
+    return lib().bh_last_error().decode(errors="replace")

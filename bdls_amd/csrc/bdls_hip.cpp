@@ -1,0 +1,405 @@
+// libbdlship.so host runtime: device contexts, workspaces, C ABI (include/bdls_hip.h).
+//
+// One context per initialised GPU: a HIP stream, the fixed-base G tables (one
+// per curve) and a growable workspace. The host-buffer API shards a batch
+// into contiguous record ranges (multiples of 64 so bitmap words concatenate)
+// and drives each device from its own host thread -- no collective, since
+// records are independent.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/bdls_hip.h"
+#include "verify.h"
+
+namespace bh {
+hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s);
+hipError_t launch_verify(int curve, const BatchIn& in, const Work& w, const uint32_t* gtab,
+                         uint32_t n, uint32_t chunk, uint64_t* bitmap, uint8_t* reason,
+                         hipStream_t s);
+}  // namespace bh
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(BH_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));        \
+  } while (0)
+
+constexpr size_t kMaxChunk = size_t(1) << 22;  // records per kernel pass (workspace bound)
+constexpr size_t kGtabWords = size_t(bh::kCombWindows) * bh::kCombEntries * 16;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return BH_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 4096);
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) return fail(BH_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    cap = want;
+    return BH_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct Dev {
+  int id = -1;
+  hipStream_t stream = nullptr;
+  uint32_t* gtab[2] = {nullptr, nullptr};
+  DevBuf ws;        // Work arrays
+  DevBuf in_fix;    // host-API staging: pub, offsets, lengths
+  DevBuf in_sig, in_msg, out;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::mutex mu;
+};
+
+std::mutex g_mu;
+std::vector<Dev*> g_devs;
+
+size_t round64(size_t n) { return (n + 63) & ~size_t(63); }
+
+size_t work_bytes(size_t ns) {
+  // 9 SoA 8-limb arrays + status + per-wave Q tables
+  return 9 * 32 * ns + ns + (ns / 64) * bh::kQTab * 24 * 64 * 4 + 256 * 16;
+}
+
+int carve_work(Dev& d, size_t n, bh::Work* w) {
+  const size_t ns = round64(n);
+  int rc = d.ws.ensure(work_bytes(ns));
+  if (rc) return rc;
+  char* p = (char*)d.ws.p;
+  auto take = [&](size_t bytes) {
+    char* q = p;
+    p += (bytes + 255) & ~size_t(255);
+    return q;
+  };
+  w->ns = (uint32_t)ns;
+  w->e = (uint32_t*)take(32 * ns);
+  w->r = (uint32_t*)take(32 * ns);
+  w->sm = (uint32_t*)take(32 * ns);
+  w->pre = (uint32_t*)take(32 * ns);
+  w->qx = (uint32_t*)take(32 * ns);
+  w->qy = (uint32_t*)take(32 * ns);
+  w->rm = (uint32_t*)take(32 * ns);
+  w->r2m = (uint32_t*)take(32 * ns);
+  w->st = (uint8_t*)take(ns);
+  w->qtab = (uint32_t*)take((ns / 64) * bh::kQTab * 24 * 64 * 4);
+  return BH_OK;
+}
+
+int dev_init(Dev& d, int id) {
+  d.id = id;
+  HIPCHK(hipSetDevice(id));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, id));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(BH_E_NODEV, std::string("device ") + std::to_string(id) + " is " +
+                                prop.gcnArchName + ", this build targets gfx950 only");
+  HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  for (int c = 0; c < 2; c++) {
+    HIPCHK(hipMalloc(&d.gtab[c], kGtabWords * 4));
+    HIPCHK(bh::launch_gtab_build(c, d.gtab[c], d.stream));
+  }
+  for (auto& e : d.ev) HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipStreamSynchronize(d.stream));
+  return BH_OK;
+}
+
+void dev_free(Dev& d) {
+  (void)hipSetDevice(d.id);
+  if (d.stream) (void)hipStreamSynchronize(d.stream);
+  for (auto& g : d.gtab)
+    if (g) (void)hipFree(g);
+  d.ws.release();
+  d.in_fix.release();
+  d.in_sig.release();
+  d.in_msg.release();
+  d.out.release();
+  for (auto& e : d.ev)
+    if (e) (void)hipEventDestroy(e);
+  if (d.stream) (void)hipStreamDestroy(d.stream);
+}
+
+Dev* get_dev(int device) {
+  std::lock_guard<std::mutex> g(g_mu);
+  for (Dev* d : g_devs)
+    if (d->id == device) return d;
+  return nullptr;
+}
+
+uint32_t inv_chunk(size_t n) {
+  size_t c = n / 65536;
+  return (uint32_t)std::max<size_t>(1, std::min<size_t>(16, c));
+}
+
+// Core device-resident pass (caller holds d.mu and has set the device).
+int run_dev(Dev& d, int curve, const bh_batch* b, size_t n, uint32_t flags, uint64_t* bitmap,
+            uint8_t* reason, hipStream_t s) {
+  for (size_t base = 0; base < n; base += kMaxChunk) {
+    const size_t m = std::min(kMaxChunk, n - base);
+    bh::Work w;
+    int rc = carve_work(d, m, &w);
+    if (rc) return rc;
+    bh::BatchIn in;
+    in.pub = b->pub + base * 64;
+    in.sig = b->sig;
+    in.sig_off = b->sig_off + base;
+    in.sig_len = b->sig_len + base;
+    in.msg = b->msg;
+    in.msg_off = b->msg_off + base;
+    in.msg_len = b->msg_len + base;
+    in.flags = flags;
+    HIPCHK(bh::launch_verify(curve, in, w, d.gtab[curve], (uint32_t)m, inv_chunk(m),
+                             bitmap + base / 64, reason + base, s));
+  }
+  return BH_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// timed variant of the launch sequence: events between the three kernels
+namespace bh {
+hipError_t launch_verify_timed(int curve, const BatchIn& in, const Work& w, const uint32_t* gtab,
+                               uint32_t n, uint32_t chunk, uint64_t* bitmap, uint8_t* reason,
+                               hipStream_t s, hipEvent_t ev[4]);
+}
+
+extern "C" {
+
+const char* bh_last_error(void) { return g_err.c_str(); }
+const char* bh_version(void) { return "bdls-hip 0.1.0 (gfx950)"; }
+
+int bh_init(uint32_t device_mask, uint32_t flags) {
+  (void)flags;
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count <= 0) return fail(BH_E_NODEV, "no HIP device visible");
+  std::lock_guard<std::mutex> g(g_mu);
+  for (int id = 0; id < count && id < 32; id++) {
+    if (device_mask && !(device_mask & (1u << id))) continue;
+    bool have = false;
+    for (Dev* d : g_devs) have |= (d->id == id);
+    if (have) continue;
+    Dev* d = new Dev();
+    int rc = dev_init(*d, id);
+    if (rc) {
+      dev_free(*d);
+      delete d;
+      return rc;
+    }
+    g_devs.push_back(d);
+  }
+  if (g_devs.empty()) return fail(BH_E_NODEV, "device_mask selects no visible device");
+  return BH_OK;
+}
+
+int bh_shutdown(void) {
+  std::lock_guard<std::mutex> g(g_mu);
+  for (Dev* d : g_devs) {
+    dev_free(*d);
+    delete d;
+  }
+  g_devs.clear();
+  return BH_OK;
+}
+
+int bh_device_count(void) {
+  std::lock_guard<std::mutex> g(g_mu);
+  return (int)g_devs.size();
+}
+
+size_t bh_workspace_bytes(size_t n) { return work_bytes(round64(std::min(n, kMaxChunk))); }
+
+int bh_verify_dev(int device, int curve, const bh_batch* b, size_t n, uint32_t flags,
+                  uint64_t* bitmap_words, uint8_t* reason, void* stream, int sync,
+                  bh_timing* timing) {
+  if (!b || (n && (!b->pub || !b->sig || !b->sig_off || !b->sig_len || !b->msg ||
+                   !b->msg_off || !b->msg_len || !bitmap_words || !reason)))
+    return fail(BH_E_INVALID, "null pointer in batch");
+  if (curve != BH_CURVE_P256) return fail(BH_E_INVALID, "curve not supported by bh_verify_dev");
+  if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
+  Dev* d = get_dev(device);
+  if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
+  std::lock_guard<std::mutex> g(d->mu);
+  HIPCHK(hipSetDevice(d->id));
+  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  if (n == 0) return BH_OK;
+  if (timing) {
+    *timing = bh_timing{0.f, 0.f, 0.f};
+    for (size_t base = 0; base < n; base += kMaxChunk) {
+      const size_t m = std::min(kMaxChunk, n - base);
+      bh::Work w;
+      int rc = carve_work(*d, m, &w);
+      if (rc) return rc;
+      bh::BatchIn in{b->pub + base * 64, b->sig, b->sig_off + base, b->sig_len + base,
+                     b->msg, b->msg_off + base, b->msg_len + base, flags};
+      HIPCHK(bh::launch_verify_timed(curve, in, w, d->gtab[curve], (uint32_t)m, inv_chunk(m),
+                                     bitmap_words + base / 64, reason + base, s, d->ev));
+      HIPCHK(hipEventSynchronize(d->ev[3]));
+      float a = 0, bb = 0, c = 0;
+      HIPCHK(hipEventElapsedTime(&a, d->ev[0], d->ev[1]));
+      HIPCHK(hipEventElapsedTime(&bb, d->ev[1], d->ev[2]));
+      HIPCHK(hipEventElapsedTime(&c, d->ev[2], d->ev[3]));
+      timing->prep_ms += a;
+      timing->inv_ms += bb;
+      timing->ladder_ms += c;
+    }
+    return BH_OK;
+  }
+  int rc = run_dev(*d, curve, b, n, flags, bitmap_words, reason, s);
+  if (rc) return rc;
+  if (sync) HIPCHK(hipStreamSynchronize(s));
+  return BH_OK;
+}
+
+int bh_verify(int curve, const bh_batch* b, size_t n, uint32_t flags, uint8_t* bitmap,
+              uint8_t* reason) {
+  if (!b || (n && (!b->pub || !b->sig_off || !b->sig_len || !b->msg_off || !b->msg_len ||
+                   !bitmap || !reason)))
+    return fail(BH_E_INVALID, "null pointer in batch");
+  if (curve != BH_CURVE_P256) return fail(BH_E_INVALID, "curve not supported by bh_verify");
+  std::vector<Dev*> devs;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    devs = g_devs;
+  }
+  if (devs.empty()) return fail(BH_E_NOT_INIT, "bh_init not called");
+  std::memset(bitmap, 0, (n + 7) / 8);
+  if (n == 0) return BH_OK;
+  // contiguous shards, 64-record aligned
+  const size_t nd = std::min(devs.size(), (n + 63) / 64);
+  const size_t per = round64((n + nd - 1) / nd);
+  std::vector<int> rcs(nd, BH_OK);
+  std::vector<std::string> errs(nd);
+  auto work = [&](size_t k) {
+    const size_t lo = k * per, hi = std::min(n, lo + per);
+    if (lo >= hi) return;
+    const size_t m = hi - lo;
+    Dev& d = *devs[k];
+    std::lock_guard<std::mutex> g(d.mu);
+    auto body = [&]() -> int {
+      HIPCHK(hipSetDevice(d.id));
+      // byte ranges of sig / msg used by this shard; offsets rebased
+      uint64_t smin = UINT64_MAX, smax = 0, mmin = UINT64_MAX, mmax = 0;
+      for (size_t i = lo; i < hi; i++) {
+        smin = std::min<uint64_t>(smin, b->sig_off[i]);
+        smax = std::max<uint64_t>(smax, b->sig_off[i] + b->sig_len[i]);
+        mmin = std::min<uint64_t>(mmin, b->msg_off[i]);
+        mmax = std::max<uint64_t>(mmax, b->msg_off[i] + b->msg_len[i]);
+      }
+      std::vector<uint64_t> so(m), mo(m);
+      for (size_t i = 0; i < m; i++) {
+        so[i] = b->sig_off[lo + i] - smin;
+        mo[i] = b->msg_off[lo + i] - mmin;
+      }
+      const size_t fix = m * 64 + m * 8 * 2 + m * 4 * 2;
+      int rc;
+      if ((rc = d.in_fix.ensure(fix + 1024))) return rc;
+      if ((rc = d.in_sig.ensure(smax - smin + 16))) return rc;
+      if ((rc = d.in_msg.ensure(mmax - mmin + 16))) return rc;
+      if ((rc = d.out.ensure(round64(m) / 8 + m + 1024))) return rc;
+      char* f = (char*)d.in_fix.p;
+      uint8_t* dpub = (uint8_t*)f;
+      uint64_t* dso = (uint64_t*)(f + ((m * 64 + 255) & ~size_t(255)));
+      uint64_t* dmo = dso + m;
+      uint32_t* dsl = (uint32_t*)(dmo + m);
+      uint32_t* dml = dsl + m;
+      uint64_t* dbm = (uint64_t*)d.out.p;
+      uint8_t* drs = (uint8_t*)(dbm + round64(m) / 64);
+      hipStream_t s = d.stream;
+      HIPCHK(hipMemcpyAsync(dpub, b->pub + lo * 64, m * 64, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(dso, so.data(), m * 8, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(dmo, mo.data(), m * 8, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(dsl, b->sig_len + lo, m * 4, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(dml, b->msg_len + lo, m * 4, hipMemcpyHostToDevice, s));
+      if (smax > smin)
+        HIPCHK(hipMemcpyAsync(d.in_sig.p, b->sig + smin, smax - smin, hipMemcpyHostToDevice, s));
+      if (mmax > mmin)
+        HIPCHK(hipMemcpyAsync(d.in_msg.p, b->msg + mmin, mmax - mmin, hipMemcpyHostToDevice, s));
+      bh_batch db{dpub, (const uint8_t*)d.in_sig.p, dso, dsl, (const uint8_t*)d.in_msg.p, dmo, dml};
+      rc = run_dev(d, curve, &db, m, flags, dbm, drs, s);
+      if (rc) return rc;
+      std::vector<uint64_t> words(round64(m) / 64);
+      HIPCHK(hipMemcpyAsync(words.data(), dbm, words.size() * 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(reason + lo, drs, m, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      // lo is a multiple of 64 -> byte-aligned splice
+      uint8_t* dst = bitmap + lo / 8;
+      const size_t nbytes = (m + 7) / 8;
+      std::memcpy(dst, words.data(), nbytes);
+      return BH_OK;
+    };
+    rcs[k] = body();
+    if (rcs[k]) errs[k] = g_err;
+  };
+  if (nd == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < nd; k++) th.emplace_back(work, k);
+    for (auto& t : th) t.join();
+  }
+  for (size_t k = 0; k < nd; k++)
+    if (rcs[k]) return fail(rcs[k], errs[k]);
+  return BH_OK;
+}
+
+int bh_csp_verify_p256(const uint8_t pub[64], const uint8_t* sig, size_t sig_len,
+                       const uint8_t* digest, size_t digest_len, int* valid, int* reason) {
+  if (!pub || !valid || !reason) return fail(BH_E_INVALID, "null argument");
+  static const uint8_t empty = 0;
+  uint64_t so = 0, mo = 0;
+  uint32_t sl = (uint32_t)sig_len, ml = (uint32_t)digest_len;
+  bh_batch b{pub, sig ? sig : &empty, &so, &sl, digest ? digest : &empty, &mo, &ml};
+  uint8_t bm = 0, rs = 0;
+  int rc = bh_verify(BH_CURVE_P256, &b, 1, 0, &bm, &rs);
+  if (rc) return rc;
+  *valid = bm & 1;
+  *reason = rs;
+  return BH_OK;
+}
+
+int bh_parse_der_sig(const uint8_t* der, size_t len, uint8_t r[32], uint8_t s[32], int* r_big,
+                     int* s_big) {
+  if ((!der && len) || !r || !s || !r_big || !s_big) return fail(BH_E_INVALID, "null argument");
+  if (len > 0xffffffffull) return BH_R_DER;
+  bh::DerSig ds;
+  std::memset(&ds, 0, sizeof(ds));
+  uint8_t rc = bh::der_parse_sig(der, (uint32_t)len, &ds);
+  std::memset(r, 0, 32);
+  std::memset(s, 0, 32);
+  *r_big = *s_big = 0;
+  if (rc == BH_R_OK) {
+    bh::limbs_to_be32(r, ds.r);
+    bh::limbs_to_be32(s, ds.s);
+    *r_big = (int)ds.r_big;
+    *s_big = (int)ds.s_big;
+  }
+  return rc;
+}
+
+}  // extern "C"

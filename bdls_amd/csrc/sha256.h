@@ -1,0 +1,109 @@
+// SHA-256 (FIPS 180-4), one message per lane, message bytes read straight
+// from HBM. Replaces bccsp/sw/hash.go:29-33 (Go crypto/sha256, SHA-NI asm) as
+// reached from msp/identities.go:179 (identity.Verify hashes the message with
+// the SHA2 family before CSP.Verify).
+#pragma once
+#include "bh_common.h"
+
+namespace bh {
+
+#if defined(__HIPCC__)
+__device__ __constant__ static const uint32_t kSha256K[64] = {
+#else
+static const uint32_t kSha256K[64] = {
+#endif
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
+    0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
+    0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
+    0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
+    0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
+    0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
+    0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
+    0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
+    0xc67178f2u};
+
+BH_HD uint32_t rotr32(uint32_t x, uint32_t n) { return (x >> n) | (x << (32 - n)); }
+
+BH_HD void sha256_block(uint32_t h[8], uint32_t w[16]) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+  for (int i = 0; i < 64; i++) {
+    uint32_t wi;
+    if (i < 16) {
+      wi = w[i];
+    } else {
+      uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+      uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
+      uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+      w[i & 15] = wi;
+    }
+    uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t t1 = hh + S1 + ch + kSha256K[i] + wi;
+    uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint32_t t2 = S0 + mj;
+    hh = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d;
+  h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// Big-endian 32-bit word at message byte position pos of a padded stream:
+// bytes [0, len) are the message, then 0x80, zeros, 64-bit bit length.
+BH_HD uint32_t sha256_word(const uint8_t* m, uint64_t len, uint64_t total, uint64_t pos) {
+  // fast path: the word lies fully inside the message
+  if (pos + 4 <= len) {
+    return ((uint32_t)m[pos] << 24) | ((uint32_t)m[pos + 1] << 16) | ((uint32_t)m[pos + 2] << 8) |
+           (uint32_t)m[pos + 3];
+  }
+  uint32_t w = 0;
+  const uint64_t bits = len * 8;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint64_t p = pos + k;
+    uint32_t byte;
+    if (p < len) byte = m[p];
+    else if (p == len) byte = 0x80u;
+    else if (p >= total - 8) byte = (uint32_t)(bits >> (8 * (total - 1 - p))) & 0xffu;
+    else byte = 0;
+    w = (w << 8) | byte;
+  }
+  return w;
+}
+
+// out = SHA-256(m[0..len)) as 8 big-endian words (out[0] = most significant).
+BH_HD void sha256_msg(uint32_t out[8], const uint8_t* m, uint64_t len) {
+  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  const uint64_t total = ((len + 9 + 63) / 64) * 64;
+  const bool aligned = (((uintptr_t)m) & 3u) == 0;
+  for (uint64_t blk = 0; blk < total; blk += 64) {
+    uint32_t w[16];
+    if (aligned && blk + 64 <= len) {
+      const uint32_t* m32 = (const uint32_t*)(m + blk);
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        uint32_t x = m32[i];
+        w[i] = (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; i++) w[i] = sha256_word(m, len, total, blk + 4 * i);
+    }
+    sha256_block(h, w);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = h[i];
+}
+
+}  // namespace bh

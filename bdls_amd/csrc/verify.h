@@ -1,0 +1,393 @@
+// Per-record stages of the batched ECDSA verify pipeline (P-256 / secp256k1).
+//
+//   stage_prep   : CSP.Verify arg checks, Go-exact DER parse, low-S, key and r
+//                  range / on-curve checks, digest (fused SHA-256 or given),
+//                  e = hashToNat, Montgomery conversions.        (1 lane/record)
+//   stage_inv    : w = s^-1 mod n by Montgomery's batch trick over a chunk of
+//                  records, u1 = e w, u2 = r w.               (1 lane/chunk)
+//   stage_ladder : Q table, signed-window (Booth w=5) ladder for u2 Q, fixed-base
+//                  comb (8-bit signed windows) for u1 G, final add, projective
+//                  x == r (or r + n) check.                   (1 lane/record)
+//
+// Reference semantics restated (see DESIGN.md for the full contract):
+//   bccsp/sw/impl.go:247-270, bccsp/sw/ecdsa.go:41-57, bccsp/utils/ecdsa.go:41-89,
+//   Go 1.21.4 crypto/ecdsa verifyNISTEC/hashToNat/pointFromAffine.
+// All intermediate records live in HBM as structure-of-arrays (8 u32 limbs per
+// value, limb-major with stride `ns`), so every per-limb access by a wave is one
+// coalesced 256-byte transaction.
+#pragma once
+#include "der.h"
+#include "ec.h"
+#include "sha256.h"
+
+namespace bh {
+
+enum : uint32_t {
+  BHF_HASH_SHA256 = 1u,  // msg is a message: digest = SHA-256(msg) (identity.Verify)
+  BHF_NO_LOW_S = 2u,     // skip Fabric's low-S rule (plain Go ecdsa.Verify semantics)
+};
+
+// Status byte kept per record between stages: low 7 bits = reason, bit 7 = r+n < p.
+enum : uint8_t { ST_R2OK = 0x80u };
+
+struct BatchIn {  // device pointers (see include/bdls_hip.h bh_batch)
+  const uint8_t* pub;
+  const uint8_t* sig;
+  const uint64_t* sig_off;
+  const uint32_t* sig_len;
+  const uint8_t* msg;
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+  uint32_t flags;
+};
+
+struct Work {
+  uint32_t ns;      // SoA stride in records (multiple of 64)
+  uint32_t* e;      // [8][ns]  e, then u1
+  uint32_t* r;      // [8][ns]  r, then u2
+  uint32_t* sm;     // [8][ns]  s * R mod n
+  uint32_t* pre;    // [8][ns]  batch-inversion prefix products
+  uint32_t* qx;     // [8][ns]  Q.x * R mod p
+  uint32_t* qy;     // [8][ns]
+  uint32_t* rm;     // [8][ns]  r * R mod p
+  uint32_t* r2m;    // [8][ns]  (r + n) * R mod p   (valid iff ST_R2OK)
+  uint8_t* st;      // [ns]
+  uint32_t* qtab;   // [ns/64][16][24][64]  per-wave Q multiples 1..16 (Jacobian)
+};
+
+// G comb table: window w in [0, 33), entry j in [0, 128): (j+1) * 2^(8w) * G,
+// affine Montgomery x (limbs 0..7) and y (limbs 8..15).
+constexpr int kCombWindows = 33;
+constexpr int kCombEntries = 128;
+constexpr int kQTab = 16;
+
+BH_HD void ld8(uint32_t v[8], const uint32_t* base, uint32_t i, uint32_t ns) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) v[k] = base[(size_t)k * ns + i];
+}
+BH_HD void st8(uint32_t* base, uint32_t i, uint32_t ns, const uint32_t v[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) base[(size_t)k * ns + i] = v[k];
+}
+
+// ------------------------------------------------------------------ prep
+template <class F, class N, class C>
+BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
+  uint8_t reason = R_OK;
+  uint32_t r[8], s[8], e[8], qx[8], qy[8];
+  const uint32_t slen = in.sig_len[i];
+  const uint32_t mlen = in.msg_len[i];
+  const bool fused = (in.flags & BHF_HASH_SHA256) != 0;
+  // impl.go:249-257: empty signature, then empty digest (a fused message always
+  // has a 32-byte digest).
+  if (slen == 0) reason = R_EMPTY_SIG;
+  else if (!fused && mlen == 0) reason = R_EMPTY_DIGEST;
+  DerSig ds;
+  if (reason == R_OK) reason = der_parse_sig(in.sig + in.sig_off[i], slen, &ds);
+  uint32_t half[8], nn[8], pp[8];
+  load_const8(half, C::half_n);
+  load_const8(nn, C::n);
+  load_const8(pp, C::p);
+  if (reason == R_OK) {
+    copy8(r, ds.r);
+    copy8(s, ds.s);
+    // sw/ecdsa.go:48-54 IsLowS: S <= floor(n/2)
+    if (!(in.flags & BHF_NO_LOW_S) && (ds.s_big || !geq8(half, s))) reason = R_HIGH_S;
+  }
+  // ---- inside crypto/ecdsa.Verify (verifyNISTEC): Q first, then r, s ranges
+  const uint8_t* q = in.pub + (size_t)i * 64;
+  be32_to_limbs(qx, q);
+  be32_to_limbs(qy, q + 32);
+  if (reason == R_OK) {
+    if (geq8(qx, pp) || geq8(qy, pp)) {
+      reason = R_BAD_KEY;
+    } else {
+      to_mont<F>(qx, qx);
+      to_mont<F>(qy, qy);
+      if (!on_curve<F, C>(qx, qy)) reason = R_BAD_KEY;
+    }
+  }
+  if (reason == R_OK && (ds.r_big || geq8(r, nn))) reason = R_R_RANGE;
+  if (reason == R_OK && (ds.s_big || geq8(s, nn))) reason = R_S_RANGE;
+  // ---- digest -> e (hashToNat: left-most 32 bytes, reduced mod n)
+  if (reason == R_OK) {
+    const uint8_t* m = in.msg + in.msg_off[i];
+    if (fused) {
+      uint32_t h[8];
+      sha256_msg(h, m, mlen);
+#pragma unroll
+      for (int k = 0; k < 8; k++) e[k] = h[7 - k];
+    } else {
+      const uint32_t L = mlen < 32 ? mlen : 32;
+#pragma unroll
+      for (int k = 0; k < 8; k++) e[k] = 0;
+#pragma unroll
+      for (int j = 0; j < 32; j++) {  // j = byte index from the least significant end
+        uint32_t v = 0;
+        if ((uint32_t)j < L) v = m[L - 1 - j];
+        e[j >> 2] |= v << (8 * (j & 3));
+      }
+    }
+    uint32_t t[8];
+    uint32_t bo = sub8(t, e, nn);
+    if (!bo) copy8(e, t);  // e < 2^256 < 2n: one conditional subtraction
+  }
+  uint8_t st = reason;
+  if (reason == R_OK) {
+    // r*R mod p and, when r + n < p, (r + n)*R mod p for the x-mod-n check
+    uint32_t pmn[8], rn[8], rm[8], r2m[8];
+    load_const8(pmn, C::p_minus_n);
+    to_mont<F>(rm, r);
+    if (!geq8(r, pmn)) {
+      st |= ST_R2OK;
+      add8(rn, r, nn);
+      to_mont<F>(r2m, rn);
+    } else {
+      copy8(r2m, rm);
+    }
+    st8(w.rm, i, w.ns, rm);
+    st8(w.r2m, i, w.ns, r2m);
+    to_mont<N>(s, s);
+  } else {
+    // keep the arithmetic of failed lanes well defined: e = r = 1, s = 1 (Mont),
+    // Q = G
+    for (int k = 0; k < 8; k++) { e[k] = r[k] = 0; }
+    e[0] = r[0] = 1;
+    load_const8(s, N::r1);
+    load_const8(qx, C::gx_m);
+    load_const8(qy, C::gy_m);
+  }
+  st8(w.e, i, w.ns, e);
+  st8(w.r, i, w.ns, r);
+  st8(w.sm, i, w.ns, s);
+  st8(w.qx, i, w.ns, qx);
+  st8(w.qy, i, w.ns, qy);
+  w.st[i] = st;
+}
+
+// ------------------------------------------------------------ batch inverse
+// Records [lo, hi) of one lane. Montgomery's trick: one Fermat inversion per
+// chunk, 3 multiplications per record.
+template <class N>
+BH_HD void stage_inv(const Work& w, uint32_t lo, uint32_t hi) {
+  uint32_t acc[8], x[8];
+  load_const8(acc, N::r1);
+  for (uint32_t i = lo; i < hi; i++) {
+    st8(w.pre, i, w.ns, acc);  // prefix of records < i
+    ld8(x, w.sm, i, w.ns);
+    mont_mul<N>(acc, acc, x);
+  }
+  uint32_t inv[8];
+  mont_inv<N>(inv, acc);  // (prod s_i)^-1 * R
+  for (uint32_t i = hi; i-- > lo;) {
+    uint32_t pre[8], wi[8], t[8];
+    ld8(pre, w.pre, i, w.ns);
+    mont_mul<N>(wi, inv, pre);  // s_i^-1 * R
+    ld8(x, w.sm, i, w.ns);
+    mont_mul<N>(inv, inv, x);
+    ld8(t, w.e, i, w.ns);
+    mont_mul<N>(t, t, wi);      // u1 = e * w (plain)
+    st8(w.e, i, w.ns, t);
+    ld8(t, w.r, i, w.ns);
+    mont_mul<N>(t, t, wi);      // u2 = r * w (plain)
+    st8(w.r, i, w.ns, t);
+  }
+}
+
+// ------------------------------------------------------------------ ladder
+BH_HD void booth5(uint32_t in6, uint32_t* mag, bool* neg) {
+  uint32_t sgn = 0u - (in6 >> 5);  // all ones if the top bit is set
+  uint32_t d = (63u - in6) & sgn;
+  d |= in6 & ~sgn;
+  *mag = (d >> 1) + (d & 1u);
+  *neg = sgn != 0;
+}
+
+// Q-table slot address for (wave, entry, limb-of-24, lane)
+BH_HD size_t qtab_idx(uint32_t wave, uint32_t entry, uint32_t limb, uint32_t lane) {
+  return (((size_t)wave * kQTab + entry) * 24 + limb) * 64 + lane;
+}
+
+BH_HD void qtab_store(uint32_t* tab, uint32_t wave, uint32_t entry, uint32_t lane, const Jac& P) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    tab[qtab_idx(wave, entry, k, lane)] = P.X[k];
+    tab[qtab_idx(wave, entry, 8 + k, lane)] = P.Y[k];
+    tab[qtab_idx(wave, entry, 16 + k, lane)] = P.Z[k];
+  }
+}
+
+BH_HD void qtab_load(Jac& P, const uint32_t* tab, uint32_t wave, uint32_t entry, uint32_t lane) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    P.X[k] = tab[qtab_idx(wave, entry, k, lane)];
+    P.Y[k] = tab[qtab_idx(wave, entry, 8 + k, lane)];
+    P.Z[k] = tab[qtab_idx(wave, entry, 16 + k, lane)];
+  }
+}
+
+// Returns true iff the signature equation holds (valid). `pre_ok` lanes only.
+template <class F, class N, class C>
+BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_t wave,
+                        uint32_t lane) {
+  uint32_t u1[8], u2[8], qx[8], qy[8];
+  ld8(u1, w.e, i, w.ns);
+  ld8(u2, w.r, i, w.ns);
+  ld8(qx, w.qx, i, w.ns);
+  ld8(qy, w.qy, i, w.ns);
+  uint32_t one[8];
+  load_const8(one, F::r1);
+
+  // ---- Q multiples 1..16 (Jacobian) into this wave's scratch slab
+  Jac T;
+  copy8(T.X, qx);
+  copy8(T.Y, qy);
+  copy8(T.Z, one);
+  qtab_store(w.qtab, wave, 0, lane, T);
+  pt_dbl<F, C>(T, T);
+  qtab_store(w.qtab, wave, 1, lane, T);
+  for (uint32_t k = 2; k < kQTab; k++) {
+    bool same;
+    pt_madd<F>(T, T, qx, qy, &same);  // (k+1) Q = k Q + Q, never degenerate for k < n-1
+    qtab_store(w.qtab, wave, k, lane, T);
+  }
+
+  // ---- u2 Q: Booth w=5 windows, most significant first. K = u2 << 28 (288 bits)
+  uint32_t K[9];
+  K[0] = u2[0] << 28;
+#pragma unroll
+  for (int k = 1; k < 8; k++) K[k] = (u2[k] << 28) | (u2[k - 1] >> 4);
+  K[8] = u2[7] >> 4;
+
+  Jac A;
+  bool a_inf;
+  {
+    uint32_t mag;
+    bool neg;
+    booth5(K[8] >> 26, &mag, &neg);
+#pragma unroll
+    for (int k = 8; k > 0; k--) K[k] = (K[k] << 5) | (K[k - 1] >> 27);
+    K[0] <<= 5;
+    qtab_load(A, w.qtab, wave, mag ? mag - 1 : 0, lane);
+    if (neg) mod_neg<F>(A.Y, A.Y);
+    a_inf = (mag == 0);
+  }
+  for (int win = 50; win >= 0; win--) {
+    uint32_t mag;
+    bool neg;
+    booth5(K[8] >> 26, &mag, &neg);
+#pragma unroll
+    for (int k = 8; k > 0; k--) K[k] = (K[k] << 5) | (K[k - 1] >> 27);
+    K[0] <<= 5;
+    Jac T2;
+    qtab_load(T2, w.qtab, wave, mag ? mag - 1 : 0, lane);  // issued before the doublings
+    for (int d = 0; d < 5; d++) pt_dbl<F, C>(A, A);
+    if (neg) mod_neg<F>(T2.Y, T2.Y);
+    Jac R;
+    bool same;
+    bool deg = pt_add<F>(R, A, T2, &same);
+    const bool take = mag != 0;
+    const bool use_t = take && a_inf;
+    const bool use_r = take && !a_inf && !deg;
+    const bool rare = take && !a_inf && deg;
+    jac_sel(A, use_r, R, A);
+    jac_sel(A, use_t, T2, A);
+    if (rare) {  // A == +-T: only reachable at the last window for crafted u2
+      if (same) pt_dbl<F, C>(A, T2);
+      else a_inf = true;
+    }
+    if (use_t) a_inf = false;
+  }
+
+  // ---- u1 G: fixed-base comb, 8-bit signed windows, affine table in HBM/L2
+  Jac B;
+  bool b_inf = true;
+  copy8(B.X, one);
+  copy8(B.Y, one);
+  copy8(B.Z, one);
+  uint32_t k1[8];
+  copy8(k1, u1);
+  uint32_t carry = 0;
+  for (int win = 0; win < kCombWindows; win++) {
+    uint32_t v = (k1[0] & 0xffu) + carry;
+#pragma unroll
+    for (int k = 0; k < 7; k++) k1[k] = (k1[k] >> 8) | (k1[k + 1] << 24);
+    k1[7] >>= 8;
+    uint32_t mag;
+    bool neg;
+    if (v > 128u) {
+      mag = 256u - v;
+      neg = true;
+      carry = 1;
+    } else {
+      mag = v;
+      neg = false;
+      carry = 0;
+    }
+    const uint32_t* te = gtab + ((size_t)win * kCombEntries + (mag ? mag - 1 : 0)) * 16;
+    uint32_t tx[8], ty[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      tx[k] = te[k];
+      ty[k] = te[8 + k];
+    }
+    if (neg) mod_neg<F>(ty, ty);
+    Jac R;
+    bool same;
+    bool deg = pt_madd<F>(R, B, tx, ty, &same);
+    const bool take = mag != 0;
+    const bool use_t = take && b_inf;
+    const bool use_r = take && !b_inf && !deg;
+    const bool rare = take && !b_inf && deg;
+    jac_sel(B, use_r, R, B);
+    if (use_t) {
+      copy8(B.X, tx);
+      copy8(B.Y, ty);
+      copy8(B.Z, one);
+    }
+    if (rare) {
+      if (same) {
+        Jac Tj;
+        copy8(Tj.X, tx);
+        copy8(Tj.Y, ty);
+        copy8(Tj.Z, one);
+        pt_dbl<F, C>(B, Tj);
+      } else {
+        b_inf = true;
+      }
+    }
+    if (use_t) b_inf = false;
+  }
+
+  // ---- P = A + B, then x(P) mod n == r  <=>  X == r Z^2  or  X == (r+n) Z^2
+  Jac P;
+  bool p_inf;
+  if (b_inf) {
+    jac_copy(P, A);
+    p_inf = a_inf;
+  } else if (a_inf) {
+    jac_copy(P, B);
+    p_inf = false;
+  } else {
+    bool same;
+    bool deg = pt_add<F>(P, A, B, &same);
+    p_inf = false;
+    if (deg) {
+      if (same) pt_dbl<F, C>(P, A);
+      else p_inf = true;
+    }
+  }
+  uint32_t z2[8], t[8], rm[8];
+  mont_sqr<F>(z2, P.Z);
+  ld8(rm, w.rm, i, w.ns);
+  mont_mul<F>(t, rm, z2);
+  bool ok = eq8(t, P.X);
+  if (w.st[i] & ST_R2OK) {
+    ld8(rm, w.r2m, i, w.ns);
+    mont_mul<F>(t, rm, z2);
+    ok = ok || eq8(t, P.X);
+  }
+  return ok && !p_inf && !is_zero8(P.Z);
+}
+
+}  // namespace bh

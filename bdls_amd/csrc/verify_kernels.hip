@@ -1,0 +1,144 @@
+// HIP kernels for gfx950 (MI355X): batched ECDSA verification.
+//
+// Launch structure per batch (one stream, see bdls_hip.cpp):
+//   k_prep   <<<ceil(n/256), 256>>>   parse / checks / SHA-256 / Montgomery inputs
+//   k_inv    <<<ceil(chunks/256),256>>> batched s^-1 mod n, u1, u2
+//   k_ladder <<<ceil(n/256), 256>>>   u1 G + u2 Q, x check, bitmap word per wave
+// plus k_gtab_build once per device at bh_init (fixed-base comb table for G).
+#include "verify.h"
+
+using namespace bh;
+
+namespace {
+
+template <class F, class N, class C>
+__global__ __launch_bounds__(256) void k_prep(BatchIn in, Work w, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  stage_prep<F, N, C>(in, w, i);
+}
+
+template <class N>
+__global__ __launch_bounds__(256) void k_inv(Work w, uint32_t n, uint32_t chunk) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t lo = (uint64_t)c * chunk;
+  if (lo >= n) return;
+  const uint64_t hi = lo + chunk < n ? lo + chunk : n;
+  stage_inv<N>(w, (uint32_t)lo, (uint32_t)hi);
+}
+
+template <class F, class N, class C>
+__global__ __launch_bounds__(256) void k_ladder(Work w, const uint32_t* __restrict__ gtab,
+                                                uint32_t n, uint64_t* __restrict__ bitmap,
+                                                uint8_t* __restrict__ reason) {
+  const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = i0 >> 6;
+  // every lane of a wave runs (out-of-range lanes on record n-1's slot data is
+  // avoided by clamping) so that the ballot below sees the whole wave
+  const bool active = i0 < n;
+  const uint32_t i = active ? i0 : (n - 1);
+  const uint8_t st = w.st[i];
+  const bool pre_ok = (st & 0x7fu) == R_OK;
+  bool ok = stage_ladder<F, N, C>(w, gtab, i, wave, lane);
+  ok = ok && pre_ok && active;
+  const uint64_t m = __ballot(ok);
+  if (lane == 0) bitmap[wave] = m;
+  if (active) reason[i] = pre_ok ? (ok ? R_OK : R_MATH) : (uint8_t)(st & 0x7fu);
+}
+
+// Entry (w, j) = (j+1) * 2^(8w) * G as affine Montgomery (x, y).
+template <class F, class C>
+__global__ __launch_bounds__(64) void k_gtab_build(uint32_t* gtab) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (uint32_t)(kCombWindows * kCombEntries)) return;
+  const uint32_t win = t / kCombEntries, j = t % kCombEntries;
+  Jac B;
+  load_const8(B.X, C::gx_m);
+  load_const8(B.Y, C::gy_m);
+  load_const8(B.Z, F::r1);
+  for (uint32_t d = 0; d < 8 * win; d++) pt_dbl<F, C>(B, B);
+  // (j+1) * B by left-to-right double-and-add over the bits of j+1 (<= 128)
+  const uint32_t k = j + 1;
+  int top = 31 - __builtin_clz(k);
+  Jac A;
+  jac_copy(A, B);
+  for (int b = top - 1; b >= 0; b--) {
+    pt_dbl<F, C>(A, A);
+    if ((k >> b) & 1u) {
+      bool same;
+      Jac R;
+      pt_add<F>(R, A, B, &same);  // A = m B, m >= 2: never degenerate
+      jac_copy(A, R);
+    }
+  }
+  uint32_t zi[8], zi2[8], x[8], y[8];
+  mont_inv<F>(zi, A.Z);
+  mont_sqr<F>(zi2, zi);
+  mont_mul<F>(x, A.X, zi2);
+  mont_mul<F>(zi2, zi2, zi);
+  mont_mul<F>(y, A.Y, zi2);
+  uint32_t* o = gtab + (size_t)t * 16;
+  for (int q = 0; q < 8; q++) {
+    o[q] = x[q];
+    o[8 + q] = y[q];
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Launchers (C++ linkage, used by bdls_hip.cpp)
+namespace bh {
+
+hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s) {
+  const int nt = kCombWindows * kCombEntries;
+  if (curve == 0)
+    hipLaunchKernelGGL((k_gtab_build<Fp_p256, Cv_p256>), dim3((nt + 63) / 64), dim3(64), 0, s,
+                       gtab);
+  else
+    hipLaunchKernelGGL((k_gtab_build<Fp_k1, Cv_k1>), dim3((nt + 63) / 64), dim3(64), 0, s, gtab);
+  return hipGetLastError();
+}
+
+hipError_t launch_verify(int curve, const BatchIn& in, const Work& w, const uint32_t* gtab,
+                         uint32_t n, uint32_t chunk, uint64_t* bitmap, uint8_t* reason,
+                         hipStream_t s) {
+  const dim3 blk(256);
+  const dim3 grd((n + 255) / 256);
+  const uint32_t nchunks = (n + chunk - 1) / chunk;
+  const dim3 grc((nchunks + 255) / 256);
+  if (curve == 0) {
+    hipLaunchKernelGGL((k_prep<Fp_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, in, w, n);
+    hipLaunchKernelGGL((k_inv<Fn_p256>), grc, blk, 0, s, w, n, chunk);
+    hipLaunchKernelGGL((k_ladder<Fp_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, w, gtab, n, bitmap,
+                       reason);
+  } else {
+    hipLaunchKernelGGL((k_prep<Fp_k1, Fn_k1, Cv_k1>), grd, blk, 0, s, in, w, n);
+    hipLaunchKernelGGL((k_inv<Fn_k1>), grc, blk, 0, s, w, n, chunk);
+    hipLaunchKernelGGL((k_ladder<Fp_k1, Fn_k1, Cv_k1>), grd, blk, 0, s, w, gtab, n, bitmap,
+                       reason);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_verify_timed(int curve, const BatchIn& in, const Work& w, const uint32_t* gtab,
+                               uint32_t n, uint32_t chunk, uint64_t* bitmap, uint8_t* reason,
+                               hipStream_t s, hipEvent_t ev[4]) {
+  if (curve != 0) return hipErrorInvalidValue;
+  const dim3 blk(256);
+  const dim3 grd((n + 255) / 256);
+  const uint32_t nchunks = (n + chunk - 1) / chunk;
+  const dim3 grc((nchunks + 255) / 256);
+  if (hipError_t e = hipEventRecord(ev[0], s)) return e;
+  hipLaunchKernelGGL((k_prep<Fp_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, in, w, n);
+  if (hipError_t e = hipEventRecord(ev[1], s)) return e;
+  hipLaunchKernelGGL((k_inv<Fn_p256>), grc, blk, 0, s, w, n, chunk);
+  if (hipError_t e = hipEventRecord(ev[2], s)) return e;
+  hipLaunchKernelGGL((k_ladder<Fp_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, w, gtab, n, bitmap,
+                     reason);
+  if (hipError_t e = hipEventRecord(ev[3], s)) return e;
+  return hipGetLastError();
+}
+
+}  // namespace bh

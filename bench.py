@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""bench.py -- P-256 ECDSA batch-verify throughput on MI355X (BASELINE.json).
+
+Workload (BASELINE.json configs[1] = SURVEY.md 8(d) config 2): per GPU, a batch
+of 1,048,576 P-256 records -- 256-byte messages hashed on device (fused
+SHA-256, identity.Verify semantics), 65,536 distinct keys, 1/16 of the records
+corrupted over eleven reject/accept classes, seed 2 (+ rank). One "step" = one
+full verify pass over the batch resident in HBM (DER parse, checks, SHA-256,
+batched inversion, u1 G + u2 Q, bitmap). `--config 5` gives one distinct key
+per record (the 64M-over-8-GPUs scaling shape, per-GPU share).
+
+Multi-GPU: one process per GPU (torch.distributed.run); records shard with no
+data-path collective (weak scaling); a gloo barrier brackets the timed region
+and the max time over ranks is reported.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Algorithmic work per verify (SURVEY.md 8(d) schedule S0):
+# 3.2e3 F_p mul/sqr x 128 u32 MACs (64 product + 64 reduction) = 4.1e5 MACs.
+MACS_PER_VERIFY = 4.1e5
+# Algorithmic HBM bytes per verify record (config 2): pub 64 + sig ~71 + msg 256
+# + offsets/lengths 24 + reason 1 + bitmap 1/8.
+def alg_bytes_per_record(msg_len: int) -> float:
+    return 64 + 72 + msg_len + 24 + 1 + 0.125
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=1 << 20, help="records per GPU")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 5])
+    ap.add_argument("--nkeys", type=int, default=65536)
+    ap.add_argument("--msg-len", type=int, default=256)
+    ap.add_argument("--corrupt-den", type=int, default=16)
+    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 20)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--mac-peak", type=float, default=float(os.environ.get("BH_MAC_PEAK", 0) or 0),
+                    help="measured v_mad_u64_u32 peak (MAC/s); default: profiles/ubench.json")
+    return ap.parse_args()
+
+
+def mac_peak_default() -> tuple[float, str]:
+    path = os.path.join(ROOT, "profiles", "ubench.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            u = json.load(f)
+        return float(u["mad_u64_u32_per_s"]), "profiles/ubench.json (measured v_mad_u64_u32)"
+    # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz / 4 (quarter-rate assumption)
+    return 256 * 4 * 32 * 2.4e9 / 4, "assumed quarter-rate v_mad_u64_u32"
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    from bdls_amd import _lib, workload
+
+    nkeys = a.n if a.config == 5 else a.nkeys
+    corrupt = 64 if a.config == 5 else a.corrupt_den
+    t_gen = time.time()
+    w = workload.generate(a.n, nkeys, a.msg_len, corrupt, seed=a.seed + 1000 * rank,
+                          nthreads=max(1, min(16, (os.cpu_count() or 1)) // max(1, min(world, 8)) or 1))
+    t_gen = time.time() - t_gen
+
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    _lib.check(_lib.lib().bh_init(1 << local, 0))
+
+    def up(x):
+        if x.dtype == np.uint64:
+            x = x.view(np.int64)
+        elif x.dtype == np.uint32:
+            x = x.view(np.int32)
+        return torch.from_numpy(x).to(dev)
+
+    d = dict(pub=up(w.pub), sig=up(w.sig), so=up(w.sig_off), sl=up(w.sig_len), msg=up(w.msg),
+             mo=up(w.msg_off), ml=up(w.msg_len))
+    n = w.n
+    words = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    reason = torch.zeros(n, dtype=torch.uint8, device=dev)
+    b = _lib.BhBatch(d["pub"].data_ptr(), d["sig"].data_ptr(), d["so"].data_ptr(),
+                     d["sl"].data_ptr(), d["msg"].data_ptr(), d["mo"].data_ptr(),
+                     d["ml"].data_ptr())
+    stream = torch.cuda.Stream(dev)  # the launch stream: kernels and timing events share it
+    L = _lib.lib()
+    flags = _lib.BH_F_HASH_SHA256
+    tm = _lib.BhTiming()
+
+    def step(timing):
+        _lib.check(L.bh_verify_dev(local, 0, ctypes.byref(b), n, flags, words.data_ptr(),
+                                   reason.data_ptr(), stream.cuda_stream, 0,
+                                   ctypes.byref(timing) if timing is not None else None))
+
+    for _ in range(a.warmup):
+        step(None)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    kern = {"prep_ms": 0.0, "inv_ms": 0.0, "ladder_ms": 0.0}
+    for _ in range(a.steps):
+        step(tm)  # HIP events around each kernel on `stream` (synchronises per step)
+        for k in kern:
+            kern[k] += getattr(tm, k)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    ev_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt[0])
+
+    # parity of the last pass: bit-exact vs the expected results of the batch
+    got_reason = reason.cpu().numpy()
+    bits = np.unpackbits(words.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+    parity_ok = bool((got_reason == w.reason).all() and (bits == w.expected_valid).all())
+    if world > 1:
+        pt = torch.tensor([1 if parity_ok else 0], dtype=torch.int32)
+        dist.all_reduce(pt, op=dist.ReduceOp.MIN)
+        parity_ok = bool(pt[0])
+
+    total = n * world * a.steps
+    value = total / elapsed
+    ms_per_step = elapsed * 1e3 / a.steps
+    ladder_avg_s = kern["ladder_ms"] * 1e-3 / a.steps
+    peak, peak_src = (a.mac_peak, "--mac-peak") if a.mac_peak else mac_peak_default()
+    achieved = n * MACS_PER_VERIFY / ladder_avg_s if ladder_avg_s > 0 else 0.0
+
+    out = {
+        "metric": "P-256 ECDSA verifies/sec (fused SHA-256, bit-exact vs Go crypto/ecdsa + Fabric low-S)",
+        "value": round(value, 1),
+        "unit": "verifies/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded P-256 keys/signatures, workload/gen.c)",
+        "config": {
+            "workload": f"BASELINE config {a.config}: {n} records/GPU, {a.msg_len}B messages, "
+                        f"{nkeys} distinct keys, 1/{corrupt} corrupted, fused SHA-256",
+            "records_per_gpu": n, "msg_len": a.msg_len, "nkeys": nkeys,
+            "corrupt_den": corrupt, "parallelism": f"shard{world} (no collective)",
+        },
+        "parity": parity_ok,
+        "kernel_ms_per_step": {k: round(v / a.steps, 3) for k, v in kern.items()},
+        "event_ms_timed_region": round(ev_ms, 3),
+        "roofline": {
+            "bound": "valu",
+            "kernel": "k_ladder",
+            "achieved": achieved / 1e12,
+            "peak": peak / 1e12,
+            "unit": "TMAC/s (u32 x u32 -> u64)",
+            "frac": achieved / peak if peak else None,
+            "work_per_unit": f"{MACS_PER_VERIFY:.2e} MAC/verify (SURVEY 8(d) S0)",
+            "peak_source": peak_src,
+            "traffic": None,
+            "alg_bytes_per_record": alg_bytes_per_record(a.msg_len),
+        },
+        "gen_s": round(t_gen, 2),
+    }
+    prof = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(prof):
+        with open(prof) as f:
+            out["roofline"]["traffic"] = json.load(f).get("ladder_bytes_per_launch")
+
+    if rank == 0 and world == 1 and a.cpu_baseline:
+        from oracle import orc
+        m = min(a.cpu_sample, n)
+        t = time.perf_counter()
+        orc.batch_verify(w.pub[:64 * m].reshape(-1, 64), w.msg, w.msg_off[:m], w.msg_len[:m],
+                         w.sig, w.sig_off[:m], w.sig_len[:m], fused=True, nthreads=a.cpu_threads)
+        dt = time.perf_counter() - t
+        out["cpu_baseline"] = {
+            "value": round(m / dt, 1), "unit": "verifies/s", "cores": a.cpu_threads,
+            "kind": "port",
+            "sample": f"first {m} records of the same batch, identity.Verify semantics "
+                      f"(SHA-256 + DER + low-S + ECDSA via OpenSSL ECDSA_do_verify), "
+                      f"{a.cpu_threads} threads, {dt:.2f}s",
+        }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if parity_ok else 3
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,123 @@
+/*
+ * bdls_hip.h -- C ABI of libbdlship.so, the MI355X (gfx950) batched ECDSA
+ * verification engine for the BDLS / Fabric signature-verification hot path.
+ *
+ * Drop-in boundary: the reference verifies every signature through the BCCSP
+ * provider interface, one call at a time:
+ *   bccsp/bccsp.go:125             BCCSP.Verify(k Key, signature, digest []byte, opts) (bool, error)
+ *   bccsp/sw/impl.go:247-270       sw CSP.Verify (arg checks + verifier dispatch)
+ *   bccsp/sw/ecdsa.go:41-57        verifyECDSA (DER unmarshal, low-S, crypto/ecdsa.Verify)
+ *   bccsp/sw/hash.go:29-33         hasher.Hash (SHA-256)
+ *   msp/identities.go:170-199      identity.Verify = Hash(msg) + Verify(pk, sig, digest)
+ * The entry points below are what a `bccsp/hip` provider binds over cgo (see
+ * INTEGRATION.md): plain pointers and sizes, no Go or torch types.
+ *
+ * Result encoding for every verify entry point:
+ *   bitmap : ceil(n/8) bytes (host API) or ceil(n/64) uint64 words (device
+ *            API), LSB-first: bit i set <=> record i verified (Go returns true).
+ *   reason : n bytes, BH_R_* below. Codes 1..6 correspond to Go returning
+ *            (false, err) from BCCSP.Verify; 7..10 to (false, nil).
+ * Function return: BH_OK (0) or a negative BH_E_* (then bh_last_error()).
+ * Thread-safety: all entry points may be called concurrently from several
+ * host threads; calls on one device are serialized internally.
+ */
+#ifndef BDLS_HIP_H
+#define BDLS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ---- */
+#define BH_OK 0
+#define BH_E_INVALID (-1) /* bad argument */
+#define BH_E_NOT_INIT (-2) /* bh_init not called / device not initialised */
+#define BH_E_DEVICE (-3)   /* HIP runtime error */
+#define BH_E_NODEV (-4)    /* no usable gfx950 device */
+#define BH_E_NOMEM (-5)    /* device allocation failed */
+
+/* ---- per-record reason codes (bit 0 of the bitmap is 1 iff BH_R_OK) ---- */
+#define BH_R_OK 0
+#define BH_R_EMPTY_SIG 1    /* impl.go:252  "Invalid signature. Cannot be empty."      -> error */
+#define BH_R_EMPTY_DIGEST 2 /* impl.go:255  "Invalid digest. Cannot be empty."         -> error */
+#define BH_R_DER 3          /* utils/ecdsa.go:44 asn1.Unmarshal failed                  -> error */
+#define BH_R_R_NONPOS 4     /* utils/ecdsa.go:57 "R must be larger than zero"           -> error */
+#define BH_R_S_NONPOS 5     /* utils/ecdsa.go:60 "S must be larger than zero"           -> error */
+#define BH_R_HIGH_S 6       /* sw/ecdsa.go:53 "Invalid S. Must be smaller than half..." -> error */
+#define BH_R_BAD_KEY 7      /* ecdsa.Verify: Q not a valid curve point                  -> false */
+#define BH_R_R_RANGE 8      /* ecdsa.Verify: r >= n                                     -> false */
+#define BH_R_MATH 9         /* ecdsa.Verify: x(u1 G + u2 Q) mod n != r, or infinity    -> false */
+#define BH_R_S_RANGE 10     /* ecdsa.Verify: s >= n (only with BH_F_NO_LOW_S)           -> false */
+
+/* ---- flags ---- */
+#define BH_F_HASH_SHA256 1u /* msg[i] is a message; digest = SHA-256(msg[i]) (identity.Verify) */
+#define BH_F_NO_LOW_S 2u    /* do not apply Fabric's low-S rule (plain crypto/ecdsa.Verify) */
+
+#define BH_CURVE_P256 0
+#define BH_CURVE_SECP256K1 1
+
+/* One batch of verify records (structure of arrays). Host pointers for
+ * bh_verify(), device pointers for bh_verify_dev(). */
+typedef struct bh_batch {
+  const uint8_t *pub;      /* n * 64 bytes: Q.x || Q.y, 32-byte big-endian each        */
+  const uint8_t *sig;      /* concatenated ASN.1 DER signatures                          */
+  const uint64_t *sig_off; /* n byte offsets into sig                                    */
+  const uint32_t *sig_len; /* n lengths (0 -> BH_R_EMPTY_SIG)                            */
+  const uint8_t *msg;      /* concatenated messages (BH_F_HASH_SHA256) or digests        */
+  const uint64_t *msg_off; /* n byte offsets into msg                                    */
+  const uint32_t *msg_len; /* n lengths (digest mode: 0 -> BH_R_EMPTY_DIGEST)            */
+} bh_batch;
+
+/* Per-call kernel timing (milliseconds, HIP events on the launch stream). */
+typedef struct bh_timing {
+  float prep_ms;   /* parse + checks + SHA-256 + Montgomery inputs */
+  float inv_ms;    /* batched s^-1 mod n, u1, u2 */
+  float ladder_ms; /* u1 G + u2 Q + x check + bitmap */
+} bh_timing;
+
+/* Initialise the devices in device_mask (bit d = HIP device d; 0 = all
+ * visible). Builds the per-device fixed-base tables. Idempotent. */
+int bh_init(uint32_t device_mask, uint32_t flags);
+int bh_shutdown(void);
+int bh_device_count(void);          /* devices initialised by bh_init */
+const char *bh_last_error(void);    /* thread-local message for the last failure */
+const char *bh_version(void);
+
+/* Device-memory bytes of library workspace needed per device for n records. */
+size_t bh_workspace_bytes(size_t n);
+
+/* Host-memory batch: copies to the devices, shards [0,n) over all initialised
+ * devices (contiguous ranges, no collective), gathers bitmap and reasons.
+ * curve: BH_CURVE_P256 (secp256k1: see bh_verify_secp256k1_bdls). */
+int bh_verify(int curve, const bh_batch *b, size_t n, uint32_t flags, uint8_t *bitmap,
+              uint8_t *reason);
+
+/* Device-resident batch on one device: every pointer in *b and the outputs
+ * are device pointers on `device`. Enqueued on `stream` (hipStream_t; NULL =
+ * the library's stream for that device) and synchronised before return when
+ * timing != NULL (then filled) or when sync != 0. bitmap_words: ceil(n/64)
+ * uint64 words. */
+int bh_verify_dev(int device, int curve, const bh_batch *b, size_t n, uint32_t flags,
+                  uint64_t *bitmap_words, uint8_t *reason, void *stream, int sync,
+                  bh_timing *timing);
+
+/* Single signature with exact BCCSP.Verify semantics (the sw provider's
+ * Verify for an ECDSA P-256 public key; runs on device 0). *valid = 1/0,
+ * *reason = BH_R_*; return BH_OK unless the engine itself failed. */
+int bh_csp_verify_p256(const uint8_t pub[64], const uint8_t *sig, size_t sig_len,
+                       const uint8_t *digest, size_t digest_len, int *valid, int *reason);
+
+/* Host-side Go-exact DER unmarshal (bccsp/utils/ecdsa.go:41-65). Returns the
+ * reason (BH_R_OK, BH_R_DER, BH_R_R_NONPOS, BH_R_S_NONPOS); on BH_R_OK fills
+ * r, s (32-byte big-endian) or sets *r_big / *s_big when a value exceeds 256
+ * bits. Pure host code, no device needed. */
+int bh_parse_der_sig(const uint8_t *der, size_t len, uint8_t r[32], uint8_t s[32], int *r_big,
+                     int *s_big);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BDLS_HIP_H */

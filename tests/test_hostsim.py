@@ -1,0 +1,48 @@
+"""CPU: the device arithmetic (bdls_amd/csrc/verify.h -- the exact stage
+functions the HIP kernels run) compiled for the host by the TEST-ONLY harness
+tests/native/hostsim.cpp, checked against the golden vectors and a generated
+batch. This is logic validation without a GPU; it is never the product path."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT, pack
+
+LIB = os.path.join(ROOT, "tests", "native", "build", "libhostsim.so")
+
+
+@pytest.fixture(scope="module")
+def hs():
+    if not os.path.exists(LIB):
+        pytest.skip("hostsim not built (make)")
+    L = ctypes.CDLL(LIB)
+    vp = ctypes.c_void_p
+    L.hs_verify.argtypes = [vp] * 7 + [ctypes.c_uint32] * 3 + [vp]
+    return L
+
+
+def run(L, arrs, fused, chunk=4):
+    pub, sig, so, sl, msg, mo, ml = arrs
+    n = len(sl)
+    out = np.zeros(n, np.uint8)
+    L.hs_verify(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data, msg.ctypes.data,
+                mo.ctypes.data, ml.ctypes.data, n, 1 if fused else 0, chunk, out.ctypes.data)
+    return out
+
+
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("chunk", [1, 7])
+def test_hostsim_golden(hs, golden, fused, chunk):
+    recs = [r for r in golden if (not fused) or "msg" in r]
+    out = run(hs, pack(recs, fused), fused, chunk)
+    bad = [(r["tag"], int(o), r["reason"]) for r, o in zip(recs, out) if o != r["reason"]]
+    assert not bad
+
+
+def test_hostsim_workload(hs):
+    from bdls_amd import workload
+    w = workload.generate(700, 50, 256, 4, seed=11, nthreads=4)
+    out = run(hs, w.arrays(), True, 16)
+    assert (out == w.reason).all()
