@@ -22,7 +22,8 @@ BH_CURVE_SECP256K1 = 1
 EXPORTS = (
     "bh_init", "bh_shutdown", "bh_device_count", "bh_last_error", "bh_version",
     "bh_workspace_bytes", "bh_verify", "bh_verify_dev", "bh_csp_verify_p256",
-    "bh_parse_der_sig",
+    "bh_parse_der_sig", "bh_dev_alloc", "bh_dev_free", "bh_memcpy_h2d", "bh_memcpy_d2h",
+    "bh_sync",
 )
 
 
@@ -78,6 +79,16 @@ def lib() -> ctypes.CDLL:
         L.bh_csp_verify_p256.restype = i32
         L.bh_parse_der_sig.argtypes = [vp, sz, vp, vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         L.bh_parse_der_sig.restype = i32
+        L.bh_dev_alloc.argtypes = [i32, sz, ctypes.POINTER(vp)]
+        L.bh_dev_alloc.restype = i32
+        L.bh_dev_free.argtypes = [i32, vp]
+        L.bh_dev_free.restype = i32
+        L.bh_memcpy_h2d.argtypes = [i32, vp, vp, sz]
+        L.bh_memcpy_h2d.restype = i32
+        L.bh_memcpy_d2h.argtypes = [i32, vp, vp, sz]
+        L.bh_memcpy_d2h.restype = i32
+        L.bh_sync.argtypes = [i32]
+        L.bh_sync.restype = i32
         _lib = L
     return _lib
 
@@ -98,3 +109,41 @@ def ensure_init(device_mask: int = 0) -> None:
 
 def last_error() -> str:
     return lib().bh_last_error().decode(errors="replace")
+
+
+class DeviceArray:
+    """A device buffer owned by libbdlship.so (HBM-resident batch data)."""
+
+    def __init__(self, device: int, nbytes: int):
+        self.device = device
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(lib().bh_dev_alloc(device, self.nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+
+    @classmethod
+    def from_numpy(cls, device: int, a):
+        import numpy as np
+        a = np.ascontiguousarray(a)
+        d = cls(device, max(1, a.nbytes))
+        if a.nbytes:
+            check(lib().bh_memcpy_h2d(device, d.ptr, a.ctypes.data, a.nbytes))
+        return d
+
+    def to_numpy(self, dtype, count: int):
+        import numpy as np
+        out = np.empty(count, dtype=dtype)
+        if out.nbytes:
+            check(lib().bh_memcpy_d2h(self.device, out.ctypes.data, self.ptr, out.nbytes))
+        return out
+
+    def free(self):
+        if self.ptr:
+            lib().bh_dev_free(self.device, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # noqa: BLE001 (interpreter shutdown)
+            pass

@@ -402,4 +402,86 @@ int bh_parse_der_sig(const uint8_t* der, size_t len, uint8_t r[32], uint8_t s[32
   return rc;
 }
 
+int bh_dev_alloc(int device, size_t bytes, void** ptr) {
+  if (!ptr) return fail(BH_E_INVALID, "null ptr");
+  Dev* d = get_dev(device);
+  if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
+  HIPCHK(hipSetDevice(d->id));
+  hipError_t e = hipMalloc(ptr, bytes ? bytes : 1);
+  if (e != hipSuccess) return fail(BH_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  return BH_OK;
+}
+
+int bh_dev_free(int device, void* ptr) {
+  Dev* d = get_dev(device);
+  if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
+  HIPCHK(hipSetDevice(d->id));
+  HIPCHK(hipFree(ptr));
+  return BH_OK;
+}
+
+static int copy_sync(int device, void* dst, const void* src, size_t bytes, hipMemcpyKind k) {
+  Dev* d = get_dev(device);
+  if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
+  if (!bytes) return BH_OK;
+  if (!dst || !src) return fail(BH_E_INVALID, "null pointer");
+  std::lock_guard<std::mutex> g(d->mu);
+  HIPCHK(hipSetDevice(d->id));
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, k, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  return BH_OK;
+}
+
+int bh_memcpy_h2d(int device, void* dst, const void* src, size_t bytes) {
+  return copy_sync(device, dst, src, bytes, hipMemcpyHostToDevice);
+}
+
+int bh_memcpy_d2h(int device, void* dst, const void* src, size_t bytes) {
+  return copy_sync(device, dst, src, bytes, hipMemcpyDeviceToHost);
+}
+
+int bh_sync(int device) {
+  Dev* d = get_dev(device);
+  if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
+  HIPCHK(hipSetDevice(d->id));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  return BH_OK;
+}
+
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Debug-only export (not in the public header): run the three stages on a
+// device-resident batch and copy every intermediate SoA array back to `dump`
+// after each stage: layout = 3 snapshots x [e, r, sm, qx, qy, rm][8][ns] u32
+// followed by 3 x st[ns] bytes. Used by tools/ to bisect device/host
+// differences against tests/native/hostsim.cpp.
+namespace bh {
+hipError_t launch_stage(int stage, const BatchIn& in, const Work& w, const uint32_t* gtab,
+                        uint32_t n, uint32_t chunk, uint64_t* bitmap, uint8_t* reason,
+                        hipStream_t s);
+}
+extern "C" int bhx_debug_verify(int device, const bh_batch* b, size_t n, uint32_t flags,
+                                uint64_t* bitmap_words, uint8_t* reason, uint32_t* dump) {
+  Dev* d = get_dev(device);
+  if (!d) return fail(BH_E_NOT_INIT, "device not initialised");
+  std::lock_guard<std::mutex> g(d->mu);
+  HIPCHK(hipSetDevice(d->id));
+  bh::Work w;
+  int rc = carve_work(*d, n, &w);
+  if (rc) return rc;
+  bh::BatchIn in{b->pub, b->sig, b->sig_off, b->sig_len, b->msg, b->msg_off, b->msg_len, flags};
+  const size_t ns = w.ns;
+  uint32_t* arrs[6] = {w.e, w.r, w.sm, w.qx, w.qy, w.rm};
+  uint8_t* stdump = (uint8_t*)(dump + 3 * 6 * 8 * ns);
+  for (int stage = 0; stage < 3; stage++) {
+    HIPCHK(bh::launch_stage(stage, in, w, d->gtab[0], (uint32_t)n, inv_chunk(n), bitmap_words,
+                            reason, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    for (int a = 0; a < 6; a++)
+      HIPCHK(hipMemcpy(dump + ((size_t)stage * 6 + a) * 8 * ns, arrs[a], 8 * ns * 4,
+                       hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(stdump + stage * ns, w.st, ns, hipMemcpyDeviceToHost));
+  }
+  return BH_OK;
+}

@@ -27,13 +27,19 @@ using namespace bh;
 __global__ __launch_bounds__(256) void k_mad(uint64_t* out, int iters) {
   uint32_t a = threadIdx.x * 2654435761u + blockIdx.x, b = a ^ 0x9e3779b9u;
   uint64_t acc[8];
+  uint32_t x[8];
 #pragma unroll
-  for (int k = 0; k < 8; k++) acc[k] = a + k;
+  for (int k = 0; k < 8; k++) {
+    acc[k] = a + k;
+    x[k] = b + 3 * k;
+  }
+  // 8 independent chains; the multiplicand depends on the previous result so
+  // nothing folds: acc = lo(acc) * x + acc  (one v_mad_u64_u32 each)
   for (int i = 0; i < iters; i++) {
 #pragma unroll
     for (int r = 0; r < 16; r++) {
 #pragma unroll
-      for (int k = 0; k < 8; k++) acc[k] = (uint64_t)(a + k) * (b + r) + acc[k];
+      for (int k = 0; k < 8; k++) acc[k] = (uint64_t)(uint32_t)acc[k] * x[k] + acc[k];
     }
   }
   uint64_t s = 0;

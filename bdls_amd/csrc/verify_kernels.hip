@@ -34,8 +34,11 @@ __global__ __launch_bounds__(256) void k_ladder(Work w, const uint32_t* __restri
   const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = i0 >> 6;
-  // every lane of a wave runs (out-of-range lanes on record n-1's slot data is
-  // avoided by clamping) so that the ballot below sees the whole wave
+  // Waves wholly past n exit: the per-wave Q-table scratch exists only for
+  // ceil(n/64) waves (wave-uniform branch).
+  if ((i0 & ~63u) >= n) return;
+  // Inside the last wave every lane runs (lanes past n recompute record n-1
+  // into their own scratch slots) so the ballot below sees the whole wave.
   const bool active = i0 < n;
   const uint32_t i = active ? i0 : (n - 1);
   const uint8_t st = w.st[i];
@@ -138,6 +141,23 @@ hipError_t launch_verify_timed(int curve, const BatchIn& in, const Work& w, cons
   hipLaunchKernelGGL((k_ladder<Fp_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, w, gtab, n, bitmap,
                      reason);
   if (hipError_t e = hipEventRecord(ev[3], s)) return e;
+  return hipGetLastError();
+}
+
+hipError_t launch_stage(int stage, const BatchIn& in, const Work& w, const uint32_t* gtab,
+                        uint32_t n, uint32_t chunk, uint64_t* bitmap, uint8_t* reason,
+                        hipStream_t s) {
+  const dim3 blk(256);
+  const dim3 grd((n + 255) / 256);
+  const uint32_t nchunks = (n + chunk - 1) / chunk;
+  const dim3 grc((nchunks + 255) / 256);
+  if (stage == 0)
+    hipLaunchKernelGGL((k_prep<Fp_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, in, w, n);
+  else if (stage == 1)
+    hipLaunchKernelGGL((k_inv<Fn_p256>), grc, blk, 0, s, w, n, chunk);
+  else
+    hipLaunchKernelGGL((k_ladder<Fp_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, w, gtab, n, bitmap,
+                       reason);
   return hipGetLastError();
 }
 

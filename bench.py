@@ -70,9 +70,9 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    import torch
-    import torch.distributed as dist
     if world > 1:
+        import torch
+        import torch.distributed as dist
         dist.init_process_group("gloo")
     from bdls_amd import _lib, workload
 
@@ -83,65 +83,56 @@ def main():
                           nthreads=max(1, min(16, (os.cpu_count() or 1)) // max(1, min(world, 8)) or 1))
     t_gen = time.time() - t_gen
 
-    torch.cuda.set_device(local)
-    dev = torch.device(f"cuda:{local}")
+    # Device memory comes from libbdlship.so itself: torch ships its own HIP
+    # runtime, so torch is used only for torch.distributed (gloo) and never
+    # touches the GPU in this process.
     _lib.check(_lib.lib().bh_init(1 << local, 0))
-
-    def up(x):
-        if x.dtype == np.uint64:
-            x = x.view(np.int64)
-        elif x.dtype == np.uint32:
-            x = x.view(np.int32)
-        return torch.from_numpy(x).to(dev)
-
-    d = dict(pub=up(w.pub), sig=up(w.sig), so=up(w.sig_off), sl=up(w.sig_len), msg=up(w.msg),
-             mo=up(w.msg_off), ml=up(w.msg_len))
+    DA = _lib.DeviceArray
+    d = dict(pub=DA.from_numpy(local, w.pub), sig=DA.from_numpy(local, w.sig),
+             so=DA.from_numpy(local, w.sig_off), sl=DA.from_numpy(local, w.sig_len),
+             msg=DA.from_numpy(local, w.msg), mo=DA.from_numpy(local, w.msg_off),
+             ml=DA.from_numpy(local, w.msg_len))
     n = w.n
-    words = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
-    reason = torch.zeros(n, dtype=torch.uint8, device=dev)
-    b = _lib.BhBatch(d["pub"].data_ptr(), d["sig"].data_ptr(), d["so"].data_ptr(),
-                     d["sl"].data_ptr(), d["msg"].data_ptr(), d["mo"].data_ptr(),
-                     d["ml"].data_ptr())
-    stream = torch.cuda.Stream(dev)  # the launch stream: kernels and timing events share it
+    words = DA(local, ((n + 63) // 64) * 8)
+    reason = DA(local, n)
+    b = _lib.BhBatch(d["pub"].ptr, d["sig"].ptr, d["so"].ptr, d["sl"].ptr, d["msg"].ptr,
+                     d["mo"].ptr, d["ml"].ptr)
     L = _lib.lib()
     flags = _lib.BH_F_HASH_SHA256
     tm = _lib.BhTiming()
 
     def step(timing):
-        _lib.check(L.bh_verify_dev(local, 0, ctypes.byref(b), n, flags, words.data_ptr(),
-                                   reason.data_ptr(), stream.cuda_stream, 0,
-                                   ctypes.byref(timing) if timing is not None else None))
+        # launch stream = the library's stream for this device (NULL); timing
+        # records HIP events around each kernel on that same stream.
+        _lib.check(L.bh_verify_dev(local, 0, ctypes.byref(b), n, flags, words.ptr, reason.ptr,
+                                   None, 0, ctypes.byref(timing) if timing is not None else None))
 
     for _ in range(a.warmup):
         step(None)
-    torch.cuda.synchronize(dev)
+    _lib.check(L.bh_sync(local))
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    _lib.check(L.bh_sync(local))
     t0 = time.perf_counter()
-    ev0.record(stream)
     kern = {"prep_ms": 0.0, "inv_ms": 0.0, "ladder_ms": 0.0}
     for _ in range(a.steps):
-        step(tm)  # HIP events around each kernel on `stream` (synchronises per step)
+        step(tm)  # HIP events around each kernel (synchronises at the end of each step)
         for k in kern:
             kern[k] += getattr(tm, k)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
+    _lib.check(L.bh_sync(local))
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    ev_ms = ev0.elapsed_time(ev1)
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt[0])
 
     # parity of the last pass: bit-exact vs the expected results of the batch
-    got_reason = reason.cpu().numpy()
-    bits = np.unpackbits(words.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+    got_reason = reason.to_numpy(np.uint8, n)
+    bits = np.unpackbits(words.to_numpy(np.uint64, (n + 63) // 64).view(np.uint8),
+                         bitorder="little")[:n].astype(bool)
     parity_ok = bool((got_reason == w.reason).all() and (bits == w.expected_valid).all())
     if world > 1:
         pt = torch.tensor([1 if parity_ok else 0], dtype=torch.int32)
@@ -176,7 +167,6 @@ def main():
         },
         "parity": parity_ok,
         "kernel_ms_per_step": {k: round(v / a.steps, 3) for k, v in kern.items()},
-        "event_ms_timed_region": round(ev_ms, 3),
         "roofline": {
             "bound": "valu",
             "kernel": "k_ladder",

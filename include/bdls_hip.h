@@ -117,6 +117,15 @@ int bh_csp_verify_p256(const uint8_t pub[64], const uint8_t *sig, size_t sig_len
 int bh_parse_der_sig(const uint8_t *der, size_t len, uint8_t r[32], uint8_t s[32], int *r_big,
                      int *s_big);
 
+/* ---- device buffers on an initialised device (callers that keep batches
+ * resident in HBM, e.g. bench.py; the library owns the HIP runtime so callers
+ * never mix runtimes). Copies are synchronous on the device's stream. ---- */
+int bh_dev_alloc(int device, size_t bytes, void **ptr);
+int bh_dev_free(int device, void *ptr);
+int bh_memcpy_h2d(int device, void *dst, const void *src, size_t bytes);
+int bh_memcpy_d2h(int device, void *dst, const void *src, size_t bytes);
+int bh_sync(int device); /* wait for all work queued on the device's library stream */
+
 #ifdef __cplusplus
 }
 #endif

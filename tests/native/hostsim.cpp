@@ -48,10 +48,20 @@ static void build_gtab() {
   }
 }
 
+extern "C" int hs_verify_dump(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
+                              const uint32_t* slen, const uint8_t* msg, const uint64_t* moff,
+                              const uint32_t* mlen, uint32_t n, uint32_t flags, uint32_t chunk,
+                              uint8_t* reason, uint32_t* dump);
 extern "C" int hs_verify(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
                          const uint32_t* slen, const uint8_t* msg, const uint64_t* moff,
                          const uint32_t* mlen, uint32_t n, uint32_t flags, uint32_t chunk,
                          uint8_t* reason) {
+  return hs_verify_dump(pub, sig, soff, slen, msg, moff, mlen, n, flags, chunk, reason, nullptr);
+}
+extern "C" int hs_verify_dump(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
+                              const uint32_t* slen, const uint8_t* msg, const uint64_t* moff,
+                              const uint32_t* mlen, uint32_t n, uint32_t flags, uint32_t chunk,
+                              uint8_t* reason, uint32_t* dump) {
   if (g_gtab.empty()) build_gtab<Fp_p256, Cv_p256>();
   const uint32_t ns = (n + 63) & ~63u;
   std::vector<uint32_t> buf((size_t)9 * 8 * ns + (size_t)(ns / 64) * kQTab * 24 * 64);
@@ -71,13 +81,23 @@ extern "C" int hs_verify(const uint8_t* pub, const uint8_t* sig, const uint64_t*
   w.qtab = p;
   w.st = st.data();
   BatchIn in{pub, sig, soff, slen, msg, moff, mlen, flags};
+  uint32_t* arrs[6] = {w.e, w.r, w.sm, w.qx, w.qy, w.rm};
+  auto snap = [&](int stage) {
+    if (!dump) return;
+    for (int a = 0; a < 6; a++)
+      std::memcpy(dump + ((size_t)stage * 6 + a) * 8 * ns, arrs[a], 8 * (size_t)ns * 4);
+    std::memcpy((uint8_t*)(dump + 3 * 6 * 8 * (size_t)ns) + stage * ns, w.st, ns);
+  };
   for (uint32_t i = 0; i < n; i++) stage_prep<Fp_p256, Fn_p256, Cv_p256>(in, w, i);
+  snap(0);
   for (uint32_t lo = 0; lo < n; lo += chunk)
     stage_inv<Fn_p256>(w, lo, lo + chunk < n ? lo + chunk : n);
+  snap(1);
   for (uint32_t i = 0; i < n; i++) {
     const bool pre_ok = (w.st[i] & 0x7f) == R_OK;
     bool ok = stage_ladder<Fp_p256, Fn_p256, Cv_p256>(w, g_gtab.data(), i, i / 64, i % 64);
     reason[i] = pre_ok ? (ok ? R_OK : R_MATH) : (uint8_t)(w.st[i] & 0x7f);
   }
+  snap(2);
   return 0;
 }

@@ -1,0 +1,22 @@
+#!/bin/bash
+# One GPU session: microbench, GPU tests, bench, rocprof kernel trace.
+# Every GPU step has its own time limit; a crash/abort/timeout stops the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+ok_or_stop() {  # $1 = exit code, $2 = step; test failures (1) continue, faults stop
+  case "$1" in
+    0|1) return 0 ;;
+    *) echo "STOP after $2 (exit $1)"; exit "$1" ;;
+  esac
+}
+STEPS="${STEPS:-ubench tests bench prof}"
+for s in $STEPS; do
+  case "$s" in
+    ubench) timeout -k 10 120 bdls_amd/lib/ubench > gpurun_out/ubench.json 2> gpurun_out/ubench.err; rc=$?; cat gpurun_out/ubench.json; ok_or_stop $rc ubench ;;
+    tests)  timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -5 gpurun_out/pytest_gpu.log; ok_or_stop $rc tests ;;
+    bench)  timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err; ok_or_stop $rc bench ;;
+    prof)   export TMPDIR=/tmp; timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0 > gpurun_out/prof.log 2>&1; rc=$?; tail -3 gpurun_out/prof.log; ok_or_stop $rc prof ;;
+  esac
+done
+echo DONE
