@@ -42,7 +42,7 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 constexpr size_t kMaxChunk = size_t(1) << 22;  // records per kernel pass (workspace bound)
-constexpr size_t kGtabWords = size_t(bh::kCombWindows) * bh::kCombEntries * 16;
+constexpr size_t kGtabWords = size_t(bh::kCombWindows) * bh::kCombEntries * bh::kGEntry;
 
 struct DevBuf {
   void* p = nullptr;
@@ -82,8 +82,9 @@ std::vector<Dev*> g_devs;
 size_t round64(size_t n) { return (n + 63) & ~size_t(63); }
 
 size_t work_bytes(size_t ns) {
-  // 9 SoA 8-limb arrays + status + per-wave Q tables
-  return 9 * 32 * ns + ns + (ns / 64) * bh::kQTab * 24 * 64 * 4 + 256 * 16;
+  // 4 scalar SoA arrays (8 limbs) + 4 base-field SoA arrays (9 limbs) + status
+  // + per-wave Q tables, each carve rounded to 256 bytes
+  return 4 * 32 * ns + 4 * 36 * ns + ns + (ns / 64) * bh::kQTab * bh::kQPt * 64 * 4 + 256 * 16;
 }
 
 int carve_work(Dev& d, size_t n, bh::Work* w) {
@@ -101,12 +102,12 @@ int carve_work(Dev& d, size_t n, bh::Work* w) {
   w->r = (uint32_t*)take(32 * ns);
   w->sm = (uint32_t*)take(32 * ns);
   w->pre = (uint32_t*)take(32 * ns);
-  w->qx = (uint32_t*)take(32 * ns);
-  w->qy = (uint32_t*)take(32 * ns);
-  w->rm = (uint32_t*)take(32 * ns);
-  w->r2m = (uint32_t*)take(32 * ns);
+  w->qx = (uint32_t*)take(36 * ns);
+  w->qy = (uint32_t*)take(36 * ns);
+  w->rm = (uint32_t*)take(36 * ns);
+  w->r2m = (uint32_t*)take(36 * ns);
   w->st = (uint8_t*)take(ns);
-  w->qtab = (uint32_t*)take((ns / 64) * bh::kQTab * 24 * 64 * 4);
+  w->qtab = (uint32_t*)take((ns / 64) * bh::kQTab * bh::kQPt * 64 * 4);
   return BH_OK;
 }
 
@@ -472,7 +473,7 @@ extern "C" int bhx_debug_verify(int device, const bh_batch* b, size_t n, uint32_
   if (rc) return rc;
   bh::BatchIn in{b->pub, b->sig, b->sig_off, b->sig_len, b->msg, b->msg_off, b->msg_len, flags};
   const size_t ns = w.ns;
-  uint32_t* arrs[6] = {w.e, w.r, w.sm, w.qx, w.qy, w.rm};
+  uint32_t* arrs[6] = {w.e, w.r, w.sm, w.qx, w.qy, w.rm};  // first 8 limbs of each
   uint8_t* stdump = (uint8_t*)(dump + 3 * 6 * 8 * ns);
   for (int stage = 0; stage < 3; stage++) {
     HIPCHK(bh::launch_stage(stage, in, w, d->gtab[0], (uint32_t)n, inv_chunk(n), bitmap_words,

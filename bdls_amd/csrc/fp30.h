@@ -1,0 +1,243 @@
+// Base-field arithmetic for the verify ladder: 9 x 30-bit limbs in u32 lanes,
+// Montgomery form with R = 2^270, LAZY reduction.
+//
+// Why this shape (gfx950, measured): a Montgomery product is issue-bound, and
+// with 30-bit limbs a column accumulates <= 9 products + the reduction terms
+// in one u64 without ever overflowing, so each product term is exactly one
+// in-place v_mad_u64_u32 (no carry flags, no register-pair shuffling). The
+// 32-bit-limb CIOS version needed ~530 VALU instructions per product; this one
+// ~150. R/p ~ 2^14 leaves headroom for values far above p, so add / sub never
+// compare against p: they only carry-normalise limbs.
+//
+// Value contract ("beta"): every element is a non-negative integer < beta * p
+// whose limbs 0..7 are < 2^30 ("normalised"; limb 8 holds the rest).
+//   f_mul(a, b)  requires beta_a * beta_b <= 16384 and normalised limbs;
+//                returns beta 2 (t < ab/R + p < 2p).
+//   f_add        beta_a + beta_b
+//   f_sub<K>     a - b + K p, K in {32, 64}: requires beta_b <= K - 1;
+//                returns beta_a + K
+//   f_mulc<c>    c * beta_a
+// The formulas in ec30.h annotate the beta of every intermediate.
+//
+// Replaces the field layer of Go crypto/internal/nistec (P-256) reached from
+// bccsp/sw/ecdsa.go:56 and btcec's fieldVal (vendor/github.com/BDLS-bft/bdls/
+// crypto/btcec/field.go:149) for secp256k1.
+#pragma once
+#include "bh_common.h"
+#include "curve_consts.h"
+
+namespace bh {
+
+constexpr uint32_t kM30 = 0x3fffffffu;
+constexpr int kL = 9;  // limbs per base-field element
+
+BH_HD void f_copy(uint32_t r[9], const uint32_t a[9]) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) r[i] = a[i];
+}
+
+BH_HD void f_sel(uint32_t r[9], bool c, const uint32_t a[9], const uint32_t b[9]) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) r[i] = c ? a[i] : b[i];
+}
+
+template <class C>
+BH_HD void f_const(uint32_t r[9], const C& c) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) r[i] = c[i];
+}
+
+// Montgomery product t = a b / 2^270 mod p (lazy, beta 2).
+template <class F>
+BH_HD void f_mul(uint32_t r[9], const uint32_t a[9], const uint32_t b[9]) {
+  uint64_t acc = 0;
+  uint32_t m[9];
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < 9) acc += (uint64_t)a[i] * b[j];
+    }
+    if constexpr (F::sparse_p256) {
+      // p = 2^256 - 2^224 + 2^192 + 2^96 - 1; -p^-1 = 1 mod 2^30, so m_k is the
+      // low limb. m_k * p, limb-aligned at column k:
+      //   -m_k (col k: cancels the low limb exactly, hence just the shift)
+      //   + m_k 2^96  = m_k << 6   at col k+3
+      //   + m_k 2^192 = m_k << 12  at col k+6
+      //   - m_k 2^224 + m_k 2^256 = m_k p[7] at col k+7 + m_k p[8] at col k+8
+      if (k >= 3 && k - 3 < 9) acc += (uint64_t)m[k - 3] << 6;
+      if (k >= 6 && k - 6 < 9) acc += (uint64_t)m[k - 6] << 12;
+      if (k >= 7 && k - 7 < 9) acc += (uint64_t)m[k - 7] * F::p[7];
+      if (k >= 8 && k - 8 < 9) acc += (uint64_t)m[k - 8] * F::p[8];
+      if (k < 9) {
+        m[k] = (uint32_t)acc & kM30;
+      } else {
+        r[k - 9] = (uint32_t)acc & kM30;
+      }
+      acc >>= 30;
+    } else {
+      // generic product-scanning Montgomery (FIPS order)
+#pragma unroll
+      for (int i = 0; i < 9; i++) {
+        const int j = k - i;
+        if (i < k && j >= 1 && j < 9 && F::p[j]) acc += (uint64_t)m[i] * F::p[j];
+      }
+      if (k < 9) {
+        m[k] = ((uint32_t)acc * F::n0) & kM30;
+        acc += (uint64_t)m[k] * F::p[0];  // low 30 bits become zero
+      } else {
+        r[k - 9] = (uint32_t)acc & kM30;
+      }
+      acc >>= 30;
+    }
+  }
+  r[8] = (uint32_t)acc;
+}
+
+template <class F>
+BH_HD void f_sqr(uint32_t r[9], const uint32_t a[9]) {
+  f_mul<F>(r, a, a);
+}
+
+// r = a + b, limbs re-normalised.
+BH_HD void f_add(uint32_t r[9], const uint32_t a[9], const uint32_t b[9]) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t t = a[i] + b[i] + c;
+    r[i] = t & kM30;
+    c = t >> 30;
+  }
+  r[8] = a[8] + b[8] + c;
+}
+
+// r = a - b + K p (K = 32 or 64), limbs re-normalised. Every limb of the
+// borrowed K p exceeds the matching limb of b, so no intermediate goes negative.
+template <class F, int K>
+BH_HD void f_sub(uint32_t r[9], const uint32_t a[9], const uint32_t b[9]) {
+  static_assert(K == 32 || K == 64, "K");
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t kk = (K == 32) ? F::k32[i] : F::k64[i];
+    const uint32_t t = a[i] + kk - b[i] + c;
+    r[i] = t & kM30;
+    c = t >> 30;
+  }
+  const uint32_t k8 = (K == 32) ? F::k32[8] : F::k64[8];
+  r[8] = a[8] + k8 - b[8] + c;
+}
+
+// r = K p - a
+template <class F, int K>
+BH_HD void f_neg(uint32_t r[9], const uint32_t a[9]) {
+  const uint32_t z[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  f_sub<F, K>(r, z, a);
+}
+
+// r = c a for a small constant c (c * 2^30 + carry < 2^64 trivially).
+template <uint32_t C>
+BH_HD void f_mulc(uint32_t r[9], const uint32_t a[9]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t t = (uint64_t)a[i] * C + c;
+    r[i] = (uint32_t)t & kM30;
+    c = t >> 30;
+  }
+  r[8] = a[8] * C + (uint32_t)c;
+}
+
+// For beta <= 2: canonical representative in [0, p).
+template <class F>
+BH_HD void f_canon(uint32_t r[9], const uint32_t a[9]) {
+  uint32_t d[9];
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int32_t t = (int32_t)a[i] - (int32_t)F::p[i] + c;
+    d[i] = (uint32_t)t & kM30;
+    c = t >> 30;  // arithmetic: 0 or -1
+  }
+  const int32_t t8 = (int32_t)a[8] - (int32_t)F::p[8] + c;
+  d[8] = (uint32_t)t8;
+  f_sel(r, t8 >= 0, d, a);
+}
+
+// Any beta (<= 8192): a mod p in [0, p) in the same domain, via a Montgomery
+// product with R mod p (= 1 in Montgomery form) and one conditional subtract.
+template <class F>
+BH_HD void f_reduce(uint32_t r[9], const uint32_t a[9]) {
+  uint32_t one[9];
+  f_const(one, F::r1);
+  f_mul<F>(r, a, one);
+  f_canon<F>(r, r);
+}
+
+BH_HD bool f_eq(const uint32_t a[9], const uint32_t b[9]) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) x |= a[i] ^ b[i];
+  return x == 0;
+}
+
+// beta <= 2 and normalised: value == 0 mod p  <=>  a in {0, p}
+template <class F>
+BH_HD bool f_is_zero2(const uint32_t a[9]) {
+  uint32_t z = 0, q = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    z |= a[i];
+    q |= a[i] ^ F::p[i];
+  }
+  return z == 0 || q == 0;
+}
+
+// 8 x 32-bit little-endian limbs (value < 2^256) <-> 9 x 30-bit limbs
+BH_HD void f_from_u256(uint32_t r[9], const uint32_t a[8]) {
+  r[0] = a[0] & kM30;
+#pragma unroll
+  for (int i = 1; i < 8; i++) {
+    const int lo = 30 * i;  // bit offset
+    const int w = lo >> 5, s = lo & 31;
+    uint32_t v = a[w] >> s;
+    if (s > 2 && w + 1 < 8) v |= a[w + 1] << (32 - s);
+    r[i] = v & kM30;
+  }
+  r[8] = a[7] >> 16;
+}
+
+BH_HD void f_to_u256(uint32_t r[8], const uint32_t a[9]) {  // a normalised, < 2^256
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    const int bit = 32 * w;
+    const int i = bit / 30, s = bit % 30;
+    uint32_t v = a[i] >> s;
+    if (i + 1 < 9) v |= a[i + 1] << (30 - s);
+    if (s > 28 && i + 2 < 9) v |= a[i + 2] << (60 - s);
+    r[w] = v;
+  }
+}
+
+template <class F>
+BH_HD void f_to_mont(uint32_t r[9], const uint32_t a[9]) {
+  uint32_t r2[9];
+  f_const(r2, F::r2);
+  f_mul<F>(r, a, r2);
+}
+
+// a^(p-2) (Fermat inverse in the Montgomery domain; a != 0 mod p). Cold path
+// (table builds); binary method over the compile-time exponent.
+template <class F>
+BH_HDNI void f_inv(uint32_t r[9], const uint32_t a[9]) {
+  uint32_t acc[9];
+  f_const(acc, F::r1);
+  for (int i = 255; i >= 0; i--) {
+    f_sqr<F>(acc, acc);
+    if ((F::pm2[i >> 5] >> (i & 31)) & 1u) f_mul<F>(acc, acc, a);
+  }
+  f_copy(r, acc);
+}
+
+}  // namespace bh

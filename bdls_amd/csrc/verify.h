@@ -18,6 +18,7 @@
 #pragma once
 #include "der.h"
 #include "ec.h"
+#include "ec30.h"
 #include "sha256.h"
 
 namespace bh {
@@ -47,19 +48,22 @@ struct Work {
   uint32_t* r;      // [8][ns]  r, then u2
   uint32_t* sm;     // [8][ns]  s * R mod n
   uint32_t* pre;    // [8][ns]  batch-inversion prefix products
-  uint32_t* qx;     // [8][ns]  Q.x * R mod p
-  uint32_t* qy;     // [8][ns]
-  uint32_t* rm;     // [8][ns]  r * R mod p
-  uint32_t* r2m;    // [8][ns]  (r + n) * R mod p   (valid iff ST_R2OK)
+  uint32_t* qx;     // [9][ns]  Q.x * 2^270 mod p (radix 2^30, canonical)
+  uint32_t* qy;     // [9][ns]
+  uint32_t* rm;     // [9][ns]  r * 2^270 mod p (canonical)
+  uint32_t* r2m;    // [9][ns]  (r + n) * 2^270 mod p   (valid iff ST_R2OK)
   uint8_t* st;      // [ns]
-  uint32_t* qtab;   // [ns/64][16][24][64]  per-wave Q multiples 1..16 (Jacobian)
+  uint32_t* qtab;   // [ns/64][16][27][64]  per-wave Q multiples 1..16 (Jacobian, radix 2^30)
 };
 
 // G comb table: window w in [0, 33), entry j in [0, 128): (j+1) * 2^(8w) * G,
-// affine Montgomery x (limbs 0..7) and y (limbs 8..15).
+// affine, canonical radix-2^30 Montgomery x (limbs 0..8) and y (limbs 9..17),
+// padded to kGEntry words.
 constexpr int kCombWindows = 33;
 constexpr int kCombEntries = 128;
+constexpr int kGEntry = 18;
 constexpr int kQTab = 16;
+constexpr int kQPt = 27;  // words per Jacobian point in the Q table
 
 BH_HD void ld8(uint32_t v[8], const uint32_t* base, uint32_t i, uint32_t ns) {
 #pragma unroll
@@ -69,12 +73,21 @@ BH_HD void st8(uint32_t* base, uint32_t i, uint32_t ns, const uint32_t v[8]) {
 #pragma unroll
   for (int k = 0; k < 8; k++) base[(size_t)k * ns + i] = v[k];
 }
+BH_HD void ld9(uint32_t v[9], const uint32_t* base, uint32_t i, uint32_t ns) {
+#pragma unroll
+  for (int k = 0; k < 9; k++) v[k] = base[(size_t)k * ns + i];
+}
+BH_HD void st9(uint32_t* base, uint32_t i, uint32_t ns, const uint32_t v[9]) {
+#pragma unroll
+  for (int k = 0; k < 9; k++) base[(size_t)k * ns + i] = v[k];
+}
 
 // ------------------------------------------------------------------ prep
-template <class F, class N, class C>
+template <class P, class N, class C>
 BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
   uint8_t reason = R_OK;
   uint32_t r[8], s[8], e[8], qx[8], qy[8];
+  uint32_t qx30[9], qy30[9];
   const uint32_t slen = in.sig_len[i];
   const uint32_t mlen = in.msg_len[i];
   const bool fused = (in.flags & BHF_HASH_SHA256) != 0;
@@ -102,9 +115,13 @@ BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
     if (geq8(qx, pp) || geq8(qy, pp)) {
       reason = R_BAD_KEY;
     } else {
-      to_mont<F>(qx, qx);
-      to_mont<F>(qy, qy);
-      if (!on_curve<F, C>(qx, qy)) reason = R_BAD_KEY;
+      f_from_u256(qx30, qx);
+      f_from_u256(qy30, qy);
+      f_to_mont<P>(qx30, qx30);
+      f_to_mont<P>(qy30, qy30);
+      f_canon<P>(qx30, qx30);
+      f_canon<P>(qy30, qy30);
+      if (!j_on_curve<P>(qx30, qy30)) reason = R_BAD_KEY;
     }
   }
   if (reason == R_OK && (ds.r_big || geq8(r, nn))) reason = R_R_RANGE;
@@ -135,18 +152,22 @@ BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
   uint8_t st = reason;
   if (reason == R_OK) {
     // r*R mod p and, when r + n < p, (r + n)*R mod p for the x-mod-n check
-    uint32_t pmn[8], rn[8], rm[8], r2m[8];
+    uint32_t pmn[8], rn[8], rm[9], r2m[9];
     load_const8(pmn, C::p_minus_n);
-    to_mont<F>(rm, r);
+    f_from_u256(rm, r);
+    f_to_mont<P>(rm, rm);
+    f_canon<P>(rm, rm);
     if (!geq8(r, pmn)) {
       st |= ST_R2OK;
       add8(rn, r, nn);
-      to_mont<F>(r2m, rn);
+      f_from_u256(r2m, rn);
+      f_to_mont<P>(r2m, r2m);
+      f_canon<P>(r2m, r2m);
     } else {
-      copy8(r2m, rm);
+      f_copy(r2m, rm);
     }
-    st8(w.rm, i, w.ns, rm);
-    st8(w.r2m, i, w.ns, r2m);
+    st9(w.rm, i, w.ns, rm);
+    st9(w.r2m, i, w.ns, r2m);
     to_mont<N>(s, s);
   } else {
     // keep the arithmetic of failed lanes well defined: e = r = 1, s = 1 (Mont),
@@ -154,14 +175,14 @@ BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
     for (int k = 0; k < 8; k++) { e[k] = r[k] = 0; }
     e[0] = r[0] = 1;
     load_const8(s, N::r1);
-    load_const8(qx, C::gx_m);
-    load_const8(qy, C::gy_m);
+    f_const(qx30, P::gx_m);
+    f_const(qy30, P::gy_m);
   }
   st8(w.e, i, w.ns, e);
   st8(w.r, i, w.ns, r);
   st8(w.sm, i, w.ns, s);
-  st8(w.qx, i, w.ns, qx);
-  st8(w.qy, i, w.ns, qy);
+  st9(w.qx, i, w.ns, qx30);
+  st9(w.qy, i, w.ns, qy30);
   w.st[i] = st;
 }
 
@@ -203,52 +224,95 @@ BH_HD void booth5(uint32_t in6, uint32_t* mag, bool* neg) {
   *neg = sgn != 0;
 }
 
-// Q-table slot address for (wave, entry, limb-of-24, lane)
+// Q-table slot address for (wave, entry, word-of-27, lane)
 BH_HD size_t qtab_idx(uint32_t wave, uint32_t entry, uint32_t limb, uint32_t lane) {
-  return (((size_t)wave * kQTab + entry) * 24 + limb) * 64 + lane;
+  return (((size_t)wave * kQTab + entry) * kQPt + limb) * 64 + lane;
 }
 
-BH_HD void qtab_store(uint32_t* tab, uint32_t wave, uint32_t entry, uint32_t lane, const Jac& P) {
+BH_HD void qtab_store(uint32_t* tab, uint32_t wave, uint32_t entry, uint32_t lane, const J30& P) {
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
+  for (int k = 0; k < 9; k++) {
     tab[qtab_idx(wave, entry, k, lane)] = P.X[k];
-    tab[qtab_idx(wave, entry, 8 + k, lane)] = P.Y[k];
-    tab[qtab_idx(wave, entry, 16 + k, lane)] = P.Z[k];
+    tab[qtab_idx(wave, entry, 9 + k, lane)] = P.Y[k];
+    tab[qtab_idx(wave, entry, 18 + k, lane)] = P.Z[k];
   }
 }
 
-BH_HD void qtab_load(Jac& P, const uint32_t* tab, uint32_t wave, uint32_t entry, uint32_t lane) {
+BH_HD void qtab_load(J30& P, const uint32_t* tab, uint32_t wave, uint32_t entry, uint32_t lane) {
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
+  for (int k = 0; k < 9; k++) {
     P.X[k] = tab[qtab_idx(wave, entry, k, lane)];
-    P.Y[k] = tab[qtab_idx(wave, entry, 8 + k, lane)];
-    P.Z[k] = tab[qtab_idx(wave, entry, 16 + k, lane)];
+    P.Y[k] = tab[qtab_idx(wave, entry, 9 + k, lane)];
+    P.Z[k] = tab[qtab_idx(wave, entry, 18 + k, lane)];
   }
 }
 
-// Returns true iff the signature equation holds (valid). `pre_ok` lanes only.
-template <class F, class N, class C>
+// One G comb-table entry t = w * kCombEntries + j: (j+1) 2^(8w) G, affine,
+// canonical Montgomery radix 2^30 (out[0..8] = x, out[9..17] = y). Used by the
+// init kernel (and the test-only host harness).
+template <class P>
+BH_HD void gtab_entry(uint32_t t, uint32_t* out) {
+  const uint32_t win = t / kCombEntries, j = t % kCombEntries;
+  J30 B;
+  f_const(B.X, P::gx_m);
+  f_const(B.Y, P::gy_m);
+  f_const(B.Z, P::r1);
+  for (uint32_t d = 0; d < 8 * win; d++) j_dbl<P>(B, B);
+  // (j+1) B by left-to-right double-and-add over the bits of j+1 (<= 128)
+  const uint32_t k = j + 1;
+  int top = 31;
+  while (!((k >> top) & 1u)) top--;
+  J30 A;
+  j_copy(A, B);
+  for (int b = top - 1; b >= 0; b--) {
+    j_dbl<P>(A, A);
+    if ((k >> b) & 1u) {
+      bool same;
+      J30 R;
+      j_add<P>(R, A, B, &same);  // A = m B with 2 <= m < 128: never degenerate
+      j_copy(A, R);
+    }
+  }
+  uint32_t zi[9], zi2[9], x[9], y[9], z[9];
+  f_reduce<P>(z, A.Z);
+  f_inv<P>(zi, z);
+  f_sqr<P>(zi2, zi);
+  f_mul<P>(x, A.X, zi2);
+  f_mul<P>(zi2, zi2, zi);
+  f_mul<P>(y, A.Y, zi2);
+  f_reduce<P>(x, x);
+  f_reduce<P>(y, y);
+  for (int q = 0; q < 9; q++) {
+    out[q] = x[q];
+    out[9 + q] = y[q];
+  }
+}
+
+// Returns true iff the signature equation holds (valid). Lanes whose prep
+// failed run on placeholder inputs (Q = G, u1 = u2 = 1) and are masked by the
+// caller.
+template <class P>
 BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_t wave,
                         uint32_t lane) {
-  uint32_t u1[8], u2[8], qx[8], qy[8];
+  uint32_t u1[8], u2[8], qx[9], qy[9];
   ld8(u1, w.e, i, w.ns);
   ld8(u2, w.r, i, w.ns);
-  ld8(qx, w.qx, i, w.ns);
-  ld8(qy, w.qy, i, w.ns);
-  uint32_t one[8];
-  load_const8(one, F::r1);
+  ld9(qx, w.qx, i, w.ns);
+  ld9(qy, w.qy, i, w.ns);
+  uint32_t one[9];
+  f_const(one, P::r1);
 
   // ---- Q multiples 1..16 (Jacobian) into this wave's scratch slab
-  Jac T;
-  copy8(T.X, qx);
-  copy8(T.Y, qy);
-  copy8(T.Z, one);
+  J30 T;
+  f_copy(T.X, qx);
+  f_copy(T.Y, qy);
+  f_copy(T.Z, one);
   qtab_store(w.qtab, wave, 0, lane, T);
-  pt_dbl<F, C>(T, T);
+  j_dbl<P>(T, T);
   qtab_store(w.qtab, wave, 1, lane, T);
   for (uint32_t k = 2; k < kQTab; k++) {
     bool same;
-    pt_madd<F>(T, T, qx, qy, &same);  // (k+1) Q = k Q + Q, never degenerate for k < n-1
+    j_madd<P>(T, T, qx, qy, &same);  // (k+1) Q = k Q + Q, never degenerate for 2 <= k < 16
     qtab_store(w.qtab, wave, k, lane, T);
   }
 
@@ -259,7 +323,7 @@ BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_
   for (int k = 1; k < 8; k++) K[k] = (u2[k] << 28) | (u2[k - 1] >> 4);
   K[8] = u2[7] >> 4;
 
-  Jac A;
+  J30 A;
   bool a_inf;
   {
     uint32_t mag;
@@ -269,7 +333,7 @@ BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_
     for (int k = 8; k > 0; k--) K[k] = (K[k] << 5) | (K[k - 1] >> 27);
     K[0] <<= 5;
     qtab_load(A, w.qtab, wave, mag ? mag - 1 : 0, lane);
-    if (neg) mod_neg<F>(A.Y, A.Y);
+    if (neg) f_neg<P, 64>(A.Y, A.Y);
     a_inf = (mag == 0);
   }
   for (int win = 50; win >= 0; win--) {
@@ -279,32 +343,32 @@ BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_
 #pragma unroll
     for (int k = 8; k > 0; k--) K[k] = (K[k] << 5) | (K[k - 1] >> 27);
     K[0] <<= 5;
-    Jac T2;
+    J30 T2;
     qtab_load(T2, w.qtab, wave, mag ? mag - 1 : 0, lane);  // issued before the doublings
-    for (int d = 0; d < 5; d++) pt_dbl<F, C>(A, A);
-    if (neg) mod_neg<F>(T2.Y, T2.Y);
-    Jac R;
+    for (int d = 0; d < 5; d++) j_dbl<P>(A, A);
+    if (neg) f_neg<P, 64>(T2.Y, T2.Y);
+    J30 R;
     bool same;
-    bool deg = pt_add<F>(R, A, T2, &same);
+    const bool deg = j_add<P>(R, A, T2, &same);
     const bool take = mag != 0;
     const bool use_t = take && a_inf;
     const bool use_r = take && !a_inf && !deg;
     const bool rare = take && !a_inf && deg;
-    jac_sel(A, use_r, R, A);
-    jac_sel(A, use_t, T2, A);
+    j_sel(A, use_r, R, A);
+    j_sel(A, use_t, T2, A);
     if (rare) {  // A == +-T: only reachable at the last window for crafted u2
-      if (same) pt_dbl<F, C>(A, T2);
+      if (same) j_dbl<P>(A, T2);
       else a_inf = true;
     }
     if (use_t) a_inf = false;
   }
 
   // ---- u1 G: fixed-base comb, 8-bit signed windows, affine table in HBM/L2
-  Jac B;
+  J30 B;
   bool b_inf = true;
-  copy8(B.X, one);
-  copy8(B.Y, one);
-  copy8(B.Z, one);
+  f_copy(B.X, one);
+  f_copy(B.Y, one);
+  f_copy(B.Z, one);
   uint32_t k1[8];
   copy8(k1, u1);
   uint32_t carry = 0;
@@ -324,34 +388,34 @@ BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_
       neg = false;
       carry = 0;
     }
-    const uint32_t* te = gtab + ((size_t)win * kCombEntries + (mag ? mag - 1 : 0)) * 16;
-    uint32_t tx[8], ty[8];
+    const uint32_t* te = gtab + ((size_t)win * kCombEntries + (mag ? mag - 1 : 0)) * kGEntry;
+    uint32_t tx[9], ty[9];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < 9; k++) {
       tx[k] = te[k];
-      ty[k] = te[8 + k];
+      ty[k] = te[9 + k];
     }
-    if (neg) mod_neg<F>(ty, ty);
-    Jac R;
+    if (neg) f_neg<P, 64>(ty, ty);
+    J30 R;
     bool same;
-    bool deg = pt_madd<F>(R, B, tx, ty, &same);
+    const bool deg = j_madd<P>(R, B, tx, ty, &same);
     const bool take = mag != 0;
     const bool use_t = take && b_inf;
     const bool use_r = take && !b_inf && !deg;
     const bool rare = take && !b_inf && deg;
-    jac_sel(B, use_r, R, B);
+    j_sel(B, use_r, R, B);
     if (use_t) {
-      copy8(B.X, tx);
-      copy8(B.Y, ty);
-      copy8(B.Z, one);
+      f_copy(B.X, tx);
+      f_copy(B.Y, ty);
+      f_copy(B.Z, one);
     }
     if (rare) {
       if (same) {
-        Jac Tj;
-        copy8(Tj.X, tx);
-        copy8(Tj.Y, ty);
-        copy8(Tj.Z, one);
-        pt_dbl<F, C>(B, Tj);
+        J30 Tj;
+        f_copy(Tj.X, tx);
+        f_copy(Tj.Y, ty);
+        f_copy(Tj.Z, one);
+        j_dbl<P>(B, Tj);
       } else {
         b_inf = true;
       }
@@ -359,35 +423,39 @@ BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_
     if (use_t) b_inf = false;
   }
 
-  // ---- P = A + B, then x(P) mod n == r  <=>  X == r Z^2  or  X == (r+n) Z^2
-  Jac P;
+  // ---- Pt = A + B, then x(Pt) mod n == r  <=>  X == r Z^2  or  X == (r+n) Z^2
+  J30 Pt;
   bool p_inf;
   if (b_inf) {
-    jac_copy(P, A);
+    j_copy(Pt, A);
     p_inf = a_inf;
   } else if (a_inf) {
-    jac_copy(P, B);
+    j_copy(Pt, B);
     p_inf = false;
   } else {
     bool same;
-    bool deg = pt_add<F>(P, A, B, &same);
+    const bool deg = j_add<P>(Pt, A, B, &same);
     p_inf = false;
     if (deg) {
-      if (same) pt_dbl<F, C>(P, A);
+      if (same) j_dbl<P>(Pt, A);
       else p_inf = true;
     }
   }
-  uint32_t z2[8], t[8], rm[8];
-  mont_sqr<F>(z2, P.Z);
-  ld8(rm, w.rm, i, w.ns);
-  mont_mul<F>(t, rm, z2);
-  bool ok = eq8(t, P.X);
+  uint32_t z2[9], t[9], x[9], rm[9];
+  f_sqr<P>(z2, Pt.Z);                  // [b2]
+  const bool z_zero = f_is_zero2<P>(z2);
+  f_reduce<P>(x, Pt.X);                // canonical X
+  ld9(rm, w.rm, i, w.ns);
+  f_mul<P>(t, rm, z2);
+  f_canon<P>(t, t);
+  bool ok = f_eq(t, x);
   if (w.st[i] & ST_R2OK) {
-    ld8(rm, w.r2m, i, w.ns);
-    mont_mul<F>(t, rm, z2);
-    ok = ok || eq8(t, P.X);
+    ld9(rm, w.r2m, i, w.ns);
+    f_mul<P>(t, rm, z2);
+    f_canon<P>(t, t);
+    ok = ok || f_eq(t, x);
   }
-  return ok && !p_inf && !is_zero8(P.Z);
+  return ok && !p_inf && !z_zero;
 }
 
 }  // namespace bh

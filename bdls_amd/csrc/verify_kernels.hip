@@ -11,11 +11,11 @@ using namespace bh;
 
 namespace {
 
-template <class F, class N, class C>
+template <class P, class N, class C>
 __global__ __launch_bounds__(256) void k_prep(BatchIn in, Work w, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  stage_prep<F, N, C>(in, w, i);
+  stage_prep<P, N, C>(in, w, i);
 }
 
 template <class N>
@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void k_inv(Work w, uint32_t n, uint32_t chunk)
   stage_inv<N>(w, (uint32_t)lo, (uint32_t)hi);
 }
 
-template <class F, class N, class C>
+template <class P>
 __global__ __launch_bounds__(256) void k_ladder(Work w, const uint32_t* __restrict__ gtab,
                                                 uint32_t n, uint64_t* __restrict__ bitmap,
                                                 uint8_t* __restrict__ reason) {
@@ -43,49 +43,19 @@ __global__ __launch_bounds__(256) void k_ladder(Work w, const uint32_t* __restri
   const uint32_t i = active ? i0 : (n - 1);
   const uint8_t st = w.st[i];
   const bool pre_ok = (st & 0x7fu) == R_OK;
-  bool ok = stage_ladder<F, N, C>(w, gtab, i, wave, lane);
+  bool ok = stage_ladder<P>(w, gtab, i, wave, lane);
   ok = ok && pre_ok && active;
   const uint64_t m = __ballot(ok);
   if (lane == 0) bitmap[wave] = m;
   if (active) reason[i] = pre_ok ? (ok ? R_OK : R_MATH) : (uint8_t)(st & 0x7fu);
 }
 
-// Entry (w, j) = (j+1) * 2^(8w) * G as affine Montgomery (x, y).
-template <class F, class C>
+// G comb table (see verify.h gtab_entry): one lane per entry.
+template <class P>
 __global__ __launch_bounds__(64) void k_gtab_build(uint32_t* gtab) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (uint32_t)(kCombWindows * kCombEntries)) return;
-  const uint32_t win = t / kCombEntries, j = t % kCombEntries;
-  Jac B;
-  load_const8(B.X, C::gx_m);
-  load_const8(B.Y, C::gy_m);
-  load_const8(B.Z, F::r1);
-  for (uint32_t d = 0; d < 8 * win; d++) pt_dbl<F, C>(B, B);
-  // (j+1) * B by left-to-right double-and-add over the bits of j+1 (<= 128)
-  const uint32_t k = j + 1;
-  int top = 31 - __builtin_clz(k);
-  Jac A;
-  jac_copy(A, B);
-  for (int b = top - 1; b >= 0; b--) {
-    pt_dbl<F, C>(A, A);
-    if ((k >> b) & 1u) {
-      bool same;
-      Jac R;
-      pt_add<F>(R, A, B, &same);  // A = m B, m >= 2: never degenerate
-      jac_copy(A, R);
-    }
-  }
-  uint32_t zi[8], zi2[8], x[8], y[8];
-  mont_inv<F>(zi, A.Z);
-  mont_sqr<F>(zi2, zi);
-  mont_mul<F>(x, A.X, zi2);
-  mont_mul<F>(zi2, zi2, zi);
-  mont_mul<F>(y, A.Y, zi2);
-  uint32_t* o = gtab + (size_t)t * 16;
-  for (int q = 0; q < 8; q++) {
-    o[q] = x[q];
-    o[8 + q] = y[q];
-  }
+  gtab_entry<P>(t, gtab + (size_t)t * kGEntry);
 }
 
 }  // namespace
@@ -97,10 +67,10 @@ namespace bh {
 hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s) {
   const int nt = kCombWindows * kCombEntries;
   if (curve == 0)
-    hipLaunchKernelGGL((k_gtab_build<Fp_p256, Cv_p256>), dim3((nt + 63) / 64), dim3(64), 0, s,
+    hipLaunchKernelGGL((k_gtab_build<F30_p256>), dim3((nt + 63) / 64), dim3(64), 0, s,
                        gtab);
   else
-    hipLaunchKernelGGL((k_gtab_build<Fp_k1, Cv_k1>), dim3((nt + 63) / 64), dim3(64), 0, s, gtab);
+    hipLaunchKernelGGL((k_gtab_build<F30_k1>), dim3((nt + 63) / 64), dim3(64), 0, s, gtab);
   return hipGetLastError();
 }
 
@@ -112,14 +82,14 @@ hipError_t launch_verify(int curve, const BatchIn& in, const Work& w, const uint
   const uint32_t nchunks = (n + chunk - 1) / chunk;
   const dim3 grc((nchunks + 255) / 256);
   if (curve == 0) {
-    hipLaunchKernelGGL((k_prep<Fp_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, in, w, n);
+    hipLaunchKernelGGL((k_prep<F30_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, in, w, n);
     hipLaunchKernelGGL((k_inv<Fn_p256>), grc, blk, 0, s, w, n, chunk);
-    hipLaunchKernelGGL((k_ladder<Fp_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, w, gtab, n, bitmap,
+    hipLaunchKernelGGL((k_ladder<F30_p256>), grd, blk, 0, s, w, gtab, n, bitmap,
                        reason);
   } else {
-    hipLaunchKernelGGL((k_prep<Fp_k1, Fn_k1, Cv_k1>), grd, blk, 0, s, in, w, n);
+    hipLaunchKernelGGL((k_prep<F30_k1, Fn_k1, Cv_k1>), grd, blk, 0, s, in, w, n);
     hipLaunchKernelGGL((k_inv<Fn_k1>), grc, blk, 0, s, w, n, chunk);
-    hipLaunchKernelGGL((k_ladder<Fp_k1, Fn_k1, Cv_k1>), grd, blk, 0, s, w, gtab, n, bitmap,
+    hipLaunchKernelGGL((k_ladder<F30_k1>), grd, blk, 0, s, w, gtab, n, bitmap,
                        reason);
   }
   return hipGetLastError();
@@ -134,11 +104,11 @@ hipError_t launch_verify_timed(int curve, const BatchIn& in, const Work& w, cons
   const uint32_t nchunks = (n + chunk - 1) / chunk;
   const dim3 grc((nchunks + 255) / 256);
   if (hipError_t e = hipEventRecord(ev[0], s)) return e;
-  hipLaunchKernelGGL((k_prep<Fp_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, in, w, n);
+  hipLaunchKernelGGL((k_prep<F30_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, in, w, n);
   if (hipError_t e = hipEventRecord(ev[1], s)) return e;
   hipLaunchKernelGGL((k_inv<Fn_p256>), grc, blk, 0, s, w, n, chunk);
   if (hipError_t e = hipEventRecord(ev[2], s)) return e;
-  hipLaunchKernelGGL((k_ladder<Fp_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, w, gtab, n, bitmap,
+  hipLaunchKernelGGL((k_ladder<F30_p256>), grd, blk, 0, s, w, gtab, n, bitmap,
                      reason);
   if (hipError_t e = hipEventRecord(ev[3], s)) return e;
   return hipGetLastError();
@@ -152,11 +122,11 @@ hipError_t launch_stage(int stage, const BatchIn& in, const Work& w, const uint3
   const uint32_t nchunks = (n + chunk - 1) / chunk;
   const dim3 grc((nchunks + 255) / 256);
   if (stage == 0)
-    hipLaunchKernelGGL((k_prep<Fp_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, in, w, n);
+    hipLaunchKernelGGL((k_prep<F30_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, in, w, n);
   else if (stage == 1)
     hipLaunchKernelGGL((k_inv<Fn_p256>), grc, blk, 0, s, w, n, chunk);
   else
-    hipLaunchKernelGGL((k_ladder<Fp_p256, Fn_p256, Cv_p256>), grd, blk, 0, s, w, gtab, n, bitmap,
+    hipLaunchKernelGGL((k_ladder<F30_p256>), grd, blk, 0, s, w, gtab, n, bitmap,
                        reason);
   return hipGetLastError();
 }

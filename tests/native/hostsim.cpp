@@ -12,40 +12,10 @@ using namespace bh;
 
 static std::vector<uint32_t> g_gtab;
 
-template <class F, class C>
 static void build_gtab() {
-  g_gtab.assign((size_t)kCombWindows * kCombEntries * 16, 0);
-  for (uint32_t t = 0; t < (uint32_t)(kCombWindows * kCombEntries); t++) {
-    const uint32_t win = t / kCombEntries, j = t % kCombEntries;
-    Jac B;
-    load_const8(B.X, C::gx_m);
-    load_const8(B.Y, C::gy_m);
-    load_const8(B.Z, F::r1);
-    for (uint32_t d = 0; d < 8 * win; d++) pt_dbl<F, C>(B, B);
-    const uint32_t k = j + 1;
-    int top = 31 - __builtin_clz(k);
-    Jac A;
-    jac_copy(A, B);
-    for (int b = top - 1; b >= 0; b--) {
-      pt_dbl<F, C>(A, A);
-      if ((k >> b) & 1u) {
-        bool same;
-        Jac R;
-        pt_add<F>(R, A, B, &same);
-        jac_copy(A, R);
-      }
-    }
-    uint32_t zi[8], zi2[8], x[8], y[8];
-    mont_inv<F>(zi, A.Z);
-    mont_sqr<F>(zi2, zi);
-    mont_mul<F>(x, A.X, zi2);
-    mont_mul<F>(zi2, zi2, zi);
-    mont_mul<F>(y, A.Y, zi2);
-    for (int q = 0; q < 8; q++) {
-      g_gtab[(size_t)t * 16 + q] = x[q];
-      g_gtab[(size_t)t * 16 + 8 + q] = y[q];
-    }
-  }
+  g_gtab.assign((size_t)kCombWindows * kCombEntries * kGEntry, 0);
+  for (uint32_t t = 0; t < (uint32_t)(kCombWindows * kCombEntries); t++)
+    gtab_entry<F30_p256>(t, g_gtab.data() + (size_t)t * kGEntry);
 }
 
 extern "C" int hs_verify_dump(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
@@ -62,9 +32,9 @@ extern "C" int hs_verify_dump(const uint8_t* pub, const uint8_t* sig, const uint
                               const uint32_t* slen, const uint8_t* msg, const uint64_t* moff,
                               const uint32_t* mlen, uint32_t n, uint32_t flags, uint32_t chunk,
                               uint8_t* reason, uint32_t* dump) {
-  if (g_gtab.empty()) build_gtab<Fp_p256, Cv_p256>();
+  if (g_gtab.empty()) build_gtab();
   const uint32_t ns = (n + 63) & ~63u;
-  std::vector<uint32_t> buf((size_t)9 * 8 * ns + (size_t)(ns / 64) * kQTab * 24 * 64);
+  std::vector<uint32_t> buf((size_t)9 * 9 * ns + (size_t)(ns / 64) * kQTab * kQPt * 64);
   std::vector<uint8_t> st(ns);
   Work w;
   w.ns = ns;
@@ -73,11 +43,11 @@ extern "C" int hs_verify_dump(const uint8_t* pub, const uint8_t* sig, const uint
   w.r = p; p += 8 * ns;
   w.sm = p; p += 8 * ns;
   w.pre = p; p += 8 * ns;
-  w.qx = p; p += 8 * ns;
-  w.qy = p; p += 8 * ns;
-  w.rm = p; p += 8 * ns;
-  w.r2m = p; p += 8 * ns;
-  p += 8 * ns;
+  w.qx = p; p += 9 * ns;
+  w.qy = p; p += 9 * ns;
+  w.rm = p; p += 9 * ns;
+  w.r2m = p; p += 9 * ns;
+  p += 9 * ns;
   w.qtab = p;
   w.st = st.data();
   BatchIn in{pub, sig, soff, slen, msg, moff, mlen, flags};
@@ -88,16 +58,29 @@ extern "C" int hs_verify_dump(const uint8_t* pub, const uint8_t* sig, const uint
       std::memcpy(dump + ((size_t)stage * 6 + a) * 8 * ns, arrs[a], 8 * (size_t)ns * 4);
     std::memcpy((uint8_t*)(dump + 3 * 6 * 8 * (size_t)ns) + stage * ns, w.st, ns);
   };
-  for (uint32_t i = 0; i < n; i++) stage_prep<Fp_p256, Fn_p256, Cv_p256>(in, w, i);
+  for (uint32_t i = 0; i < n; i++) stage_prep<F30_p256, Fn_p256, Cv_p256>(in, w, i);
   snap(0);
   for (uint32_t lo = 0; lo < n; lo += chunk)
     stage_inv<Fn_p256>(w, lo, lo + chunk < n ? lo + chunk : n);
   snap(1);
   for (uint32_t i = 0; i < n; i++) {
     const bool pre_ok = (w.st[i] & 0x7f) == R_OK;
-    bool ok = stage_ladder<Fp_p256, Fn_p256, Cv_p256>(w, g_gtab.data(), i, i / 64, i % 64);
+    bool ok = stage_ladder<F30_p256>(w, g_gtab.data(), i, i / 64, i % 64);
     reason[i] = pre_ok ? (ok ? R_OK : R_MATH) : (uint8_t)(w.st[i] & 0x7f);
   }
   snap(2);
   return 0;
 }
+
+// ---- field-op probes for tests/test_field30.py (bound stress) ----
+extern "C" void hs_f_mul(const uint32_t* a, const uint32_t* b, uint32_t* r) {
+  f_mul<F30_p256>(r, a, b);
+}
+extern "C" void hs_f_sub32(const uint32_t* a, const uint32_t* b, uint32_t* r) {
+  f_sub<F30_p256, 32>(r, a, b);
+}
+extern "C" void hs_f_sub64(const uint32_t* a, const uint32_t* b, uint32_t* r) {
+  f_sub<F30_p256, 64>(r, a, b);
+}
+extern "C" void hs_f_add(const uint32_t* a, const uint32_t* b, uint32_t* r) { f_add(r, a, b); }
+extern "C" void hs_f_reduce(const uint32_t* a, uint32_t* r) { f_reduce<F30_p256>(r, a); }

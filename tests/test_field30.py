@@ -1,0 +1,91 @@
+"""CPU: the radix-2^30 lazy field (bdls_amd/csrc/fp30.h, compiled for the host by
+the test-only harness) at the edges of its value contract:
+  f_mul needs beta_a * beta_b <= 16384 (tested to 16384; the formulas stay <= 9604) and returns t < 2p, t == a b 2^-270 (mod p);
+  f_sub<K> needs beta_b <= K - 1 and returns a - b + K p with normalised limbs.
+Values are drawn at the bounds (beta p - 1, all-ones limbs, 0, p) to catch
+64-bit column overflow."""
+import ctypes
+import os
+import random
+
+import pytest
+
+from tests.conftest import ROOT
+
+P = 2**256 - 2**224 + 2**192 + 2**96 - 1
+R = 2**270
+M = 2**30 - 1
+LIB = os.path.join(ROOT, "tests", "native", "build", "libhostsim.so")
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not os.path.exists(LIB):
+        pytest.skip("hostsim not built")
+    return ctypes.CDLL(LIB)
+
+
+def to9(v):
+    l = [(v >> (30 * i)) & M for i in range(8)] + [v >> 240]
+    assert l[8] < 2**32
+    return (ctypes.c_uint32 * 9)(*l)
+
+
+def from9(a):
+    return sum(int(a[i]) << (30 * i) for i in range(9))
+
+
+def normalised(a):
+    return all(int(a[i]) <= M for i in range(8))
+
+
+def edge_values(beta, rng, k=40):
+    hi = beta * P - 1
+    vals = [0, 1, P - 1, P, P + 1, hi, hi - P, 2**256 - 1 if 2**256 - 1 <= hi else hi]
+    # all limbs 0..7 at 2^30 - 1 with the largest admissible top limb
+    top = hi >> 240
+    v = sum(M << (30 * i) for i in range(8)) + (top << 240)
+    while v > hi:
+        top -= 1
+        v = sum(M << (30 * i) for i in range(8)) + (top << 240)
+    vals.append(v)
+    vals += [rng.randrange(hi + 1) for _ in range(k)]
+    return [v for v in vals if v <= hi]
+
+
+@pytest.mark.parametrize("ba,bb", [(2, 2), (34, 34), (66, 66), (66, 36), (128, 128), (6, 56),
+                                   (98, 98), (236, 6), (8192, 2), (2, 8192), (90, 90)])
+def test_f_mul_bounds(L, ba, bb):
+    rng = random.Random(ba * 1000 + bb)
+    out = (ctypes.c_uint32 * 9)()
+    Rinv = pow(R, -1, P)
+    for a in edge_values(ba, rng, 25):
+        for b in edge_values(bb, rng, 5):
+            L.hs_f_mul(to9(a), to9(b), out)
+            t = from9(out)
+            assert normalised(out)
+            assert t < 2 * P, (ba, bb)
+            assert t % P == a * b * Rinv % P
+
+
+@pytest.mark.parametrize("K", [32, 64])
+def test_f_sub_bounds(L, K):
+    rng = random.Random(K)
+    out = (ctypes.c_uint32 * 9)()
+    fn = L.hs_f_sub32 if K == 32 else L.hs_f_sub64
+    for a in edge_values(66, rng, 30):
+        for b in edge_values(K - 1, rng, 30):
+            fn(to9(a), to9(b), out)
+            assert normalised(out)
+            assert from9(out) == a - b + K * P
+
+
+def test_f_add_reduce(L):
+    rng = random.Random(3)
+    out = (ctypes.c_uint32 * 9)()
+    for a in edge_values(64, rng, 20):
+        for b in edge_values(64, rng, 5):
+            L.hs_f_add(to9(a), to9(b), out)
+            assert normalised(out) and from9(out) == a + b
+            L.hs_f_reduce(to9(a + b), out)
+            assert from9(out) == (a + b) % P
