@@ -48,44 +48,47 @@ BH_HD void f_const(uint32_t r[9], const C& c) {
 }
 
 // Montgomery product t = a b / 2^270 mod p (lazy, beta 2).
+// Two phases for instruction-level parallelism: (1) the 17 product columns are
+// accumulated independently (17 parallel v_mad_u64_u32 chains of <= 9), then
+// (2) one short sequential pass folds the carries and the reduction terms
+// (critical path ~2 instructions per column). Column bound: <= 9 products
+// < 2^60 plus reduction terms < 2^60 + 2^46 + 2^42 + 2^36 and the carry, < 2^64.
+// Phase 2 of the Montgomery product: fold carries and reduction into r.
 template <class F>
-BH_HD void f_mul(uint32_t r[9], const uint32_t a[9], const uint32_t b[9]) {
+BH_HD void f_redc(uint32_t r[9], uint64_t C[17]) {
   uint64_t acc = 0;
-  uint32_t m[9];
+  if constexpr (F::sparse_p256) {
+    // p = 2^256 - 2^224 + 2^192 + 2^96 - 1 and -p^-1 = 1 mod 2^30, so m_k is the
+    // low limb of the running column and m_k p, limb-aligned at column k, is
+    //   -m_k               (col k: cancels the low limb exactly -> just shift)
+    //   + m_k 2^96  = m_k << 6   at col k+3
+    //   + m_k 2^192 = m_k << 12  at col k+6
+    //   + m_k (2^256 - 2^224) = m_k p[7] at col k+7 + m_k p[8] at col k+8
 #pragma unroll
-  for (int k = 0; k < 17; k++) {
-#pragma unroll
-    for (int i = 0; i < 9; i++) {
-      const int j = k - i;
-      if (j >= 0 && j < 9) acc += (uint64_t)a[i] * b[j];
-    }
-    if constexpr (F::sparse_p256) {
-      // p = 2^256 - 2^224 + 2^192 + 2^96 - 1; -p^-1 = 1 mod 2^30, so m_k is the
-      // low limb. m_k * p, limb-aligned at column k:
-      //   -m_k (col k: cancels the low limb exactly, hence just the shift)
-      //   + m_k 2^96  = m_k << 6   at col k+3
-      //   + m_k 2^192 = m_k << 12  at col k+6
-      //   - m_k 2^224 + m_k 2^256 = m_k p[7] at col k+7 + m_k p[8] at col k+8
-      if (k >= 3 && k - 3 < 9) acc += (uint64_t)m[k - 3] << 6;
-      if (k >= 6 && k - 6 < 9) acc += (uint64_t)m[k - 6] << 12;
-      if (k >= 7 && k - 7 < 9) acc += (uint64_t)m[k - 7] * F::p[7];
-      if (k >= 8 && k - 8 < 9) acc += (uint64_t)m[k - 8] * F::p[8];
+    for (int k = 0; k < 17; k++) {
+      acc += C[k];
+      const uint32_t m = (uint32_t)acc & kM30;
       if (k < 9) {
-        m[k] = (uint32_t)acc & kM30;
+        C[k + 3] += (uint64_t)m << 6;
+        C[k + 6] += (uint64_t)m << 12;
+        C[k + 7] += (uint64_t)m * F::p[7];
+        C[k + 8] += (uint64_t)m * F::p[8];
       } else {
-        r[k - 9] = (uint32_t)acc & kM30;
+        r[k - 9] = m;
       }
       acc >>= 30;
-    } else {
-      // generic product-scanning Montgomery (FIPS order)
+    }
+  } else {
+    // generic: m_k = low limb * (-p^-1) mod 2^30; m_k p added column-wise
 #pragma unroll
-      for (int i = 0; i < 9; i++) {
-        const int j = k - i;
-        if (i < k && j >= 1 && j < 9 && F::p[j]) acc += (uint64_t)m[i] * F::p[j];
-      }
+    for (int k = 0; k < 17; k++) {
+      acc += C[k];
       if (k < 9) {
-        m[k] = ((uint32_t)acc * F::n0) & kM30;
-        acc += (uint64_t)m[k] * F::p[0];  // low 30 bits become zero
+        const uint32_t m = ((uint32_t)acc * F::n0) & kM30;
+        acc += (uint64_t)m * F::p[0];  // low 30 bits become zero
+#pragma unroll
+        for (int j = 1; j < 9; j++)
+          if (F::p[j]) C[k + j] += (uint64_t)m * F::p[j];
       } else {
         r[k - 9] = (uint32_t)acc & kM30;
       }
@@ -96,8 +99,35 @@ BH_HD void f_mul(uint32_t r[9], const uint32_t a[9], const uint32_t b[9]) {
 }
 
 template <class F>
+BH_HD void f_mul(uint32_t r[9], const uint32_t a[9], const uint32_t b[9]) {
+  uint64_t C[17];
+#pragma unroll
+  for (int k = 0; k < 17; k++) C[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++)
+#pragma unroll
+    for (int j = 0; j < 9; j++) C[i + j] += (uint64_t)a[i] * b[j];
+  f_redc<F>(r, C);
+}
+
+// Squaring: 9 squares + 36 doubled cross products (2 a_i) a_j. A column holds
+// <= 4 cross products < 2^61 plus one square < 2^60: the same < 2^64 bound.
+// Precondition as f_mul, and limb 8 < 2^30 (always: beta <= 2^14).
+template <class F>
 BH_HD void f_sqr(uint32_t r[9], const uint32_t a[9]) {
-  f_mul<F>(r, a, a);
+  uint64_t C[17];
+  uint32_t d[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) d[i] = a[i] << 1;
+#pragma unroll
+  for (int k = 0; k < 17; k++) C[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    C[2 * i] += (uint64_t)a[i] * a[i];
+#pragma unroll
+    for (int j = i + 1; j < 9; j++) C[i + j] += (uint64_t)d[i] * a[j];
+  }
+  f_redc<F>(r, C);
 }
 
 // r = a + b, limbs re-normalised.

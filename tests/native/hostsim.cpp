@@ -84,3 +84,4 @@ extern "C" void hs_f_sub64(const uint32_t* a, const uint32_t* b, uint32_t* r) {
 }
 extern "C" void hs_f_add(const uint32_t* a, const uint32_t* b, uint32_t* r) { f_add(r, a, b); }
 extern "C" void hs_f_reduce(const uint32_t* a, uint32_t* r) { f_reduce<F30_p256>(r, a); }
+extern "C" void hs_f_sqr(const uint32_t* a, uint32_t* r) { f_sqr<F30_p256>(r, a); }

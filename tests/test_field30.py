@@ -89,3 +89,15 @@ def test_f_add_reduce(L):
             assert normalised(out) and from9(out) == a + b
             L.hs_f_reduce(to9(a + b), out)
             assert from9(out) == (a + b) % P
+
+
+@pytest.mark.parametrize("ba", [2, 34, 66, 98, 128])
+def test_f_sqr_bounds(L, ba):
+    rng = random.Random(ba)
+    out = (ctypes.c_uint32 * 9)()
+    Rinv = pow(R, -1, P)
+    for a in edge_values(ba, rng, 200):
+        L.hs_f_sqr(to9(a), out)
+        t = from9(out)
+        assert normalised(out) and t < 2 * P
+        assert t % P == a * a * Rinv % P
