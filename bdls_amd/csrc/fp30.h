@@ -53,6 +53,23 @@ BH_HD void f_const(uint32_t r[9], const C& c) {
 // (2) one short sequential pass folds the carries and the reduction terms
 // (critical path ~2 instructions per column). Column bound: <= 9 products
 // < 2^60 plus reduction terms < 2^60 + 2^46 + 2^42 + 2^36 and the carry, < 2^64.
+// c += m * k as ONE v_mad_u64_u32. For power-of-two k hipcc otherwise emits a
+// 64-bit shift of the whole column plus two masks and an add (4 instructions).
+// k must be wave-uniform (an SGPR or an inline constant); the carry-out goes to
+// VCC, which is declared clobbered.
+template <uint32_t K>
+BH_HD void mac_k(uint64_t& c, uint32_t m) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (K <= 64) {
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c) : "v"(m), "i"(K) : "vcc");
+  } else {
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c) : "v"(m), "s"(K) : "vcc");
+  }
+#else
+  c += (uint64_t)m * K;
+#endif
+}
+
 // Phase 2 of the Montgomery product: fold carries and reduction into r.
 template <class F>
 BH_HD void f_redc(uint32_t r[9], uint64_t C[17]) {
@@ -69,10 +86,10 @@ BH_HD void f_redc(uint32_t r[9], uint64_t C[17]) {
       acc += C[k];
       const uint32_t m = (uint32_t)acc & kM30;
       if (k < 9) {
-        C[k + 3] += (uint64_t)m << 6;
-        C[k + 6] += (uint64_t)m << 12;
-        C[k + 7] += (uint64_t)m * F::p[7];
-        C[k + 8] += (uint64_t)m * F::p[8];
+        mac_k<64u>(C[k + 3], m);
+        mac_k<4096u>(C[k + 6], m);
+        mac_k<F::p[7]>(C[k + 7], m);
+        mac_k<F::p[8]>(C[k + 8], m);
       } else {
         r[k - 9] = m;
       }

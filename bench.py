@@ -60,7 +60,8 @@ def mac_peak_default() -> tuple[float, str]:
     if os.path.exists(path):
         with open(path) as f:
             u = json.load(f)
-        return float(u["mad_u64_u32_per_s"]), "profiles/ubench.json (measured v_mad_u64_u32)"
+        return (float(u.get("mad_u64_u32_per_s_32ch", u["mad_u64_u32_per_s"])),
+                "profiles/ubench.json: measured chip-wide v_mad_u64_u32 throughput (32 chains/lane)")
     # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz / 4 (quarter-rate assumption)
     return 256 * 4 * 32 * 2.4e9 / 4, "assumed quarter-rate v_mad_u64_u32"
 
