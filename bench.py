@@ -68,14 +68,9 @@ def mac_peak_default() -> tuple[float, str]:
 
 def main():
     a = parse()
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
-    from bdls_amd import _lib, workload
+    from bdls_amd import _lib, dist, workload
+    rank, world, local = dist.env_rank()
+    dist.init(world)
 
     nkeys = a.n if a.config == 5 else a.nkeys
     corrupt = 64 if a.config == 5 else a.corrupt_den
@@ -111,8 +106,7 @@ def main():
     for _ in range(a.warmup):
         step(None)
     _lib.check(L.bh_sync(local))
-    if world > 1:
-        dist.barrier()
+    dist.barrier(world)
     _lib.check(L.bh_sync(local))
     t0 = time.perf_counter()
     kern = {"prep_ms": 0.0, "inv_ms": 0.0, "ladder_ms": 0.0}
@@ -122,23 +116,15 @@ def main():
             kern[k] += getattr(tm, k)
     _lib.check(L.bh_sync(local))
     t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = t1 - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt[0])
+    dist.barrier(world)
+    elapsed = dist.max_over_ranks(t1 - t0, world)
 
     # parity of the last pass: bit-exact vs the expected results of the batch
     got_reason = reason.to_numpy(np.uint8, n)
     bits = np.unpackbits(words.to_numpy(np.uint64, (n + 63) // 64).view(np.uint8),
                          bitorder="little")[:n].astype(bool)
     parity_ok = bool((got_reason == w.reason).all() and (bits == w.expected_valid).all())
-    if world > 1:
-        pt = torch.tensor([1 if parity_ok else 0], dtype=torch.int32)
-        dist.all_reduce(pt, op=dist.ReduceOp.MIN)
-        parity_ok = bool(pt[0])
+    parity_ok = dist.all_true(parity_ok, world)
 
     total = n * world * a.steps
     value = total / elapsed
@@ -203,8 +189,7 @@ def main():
         }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    dist.finalize(world)
     return 0 if parity_ok else 3
 
 
