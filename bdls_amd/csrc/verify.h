@@ -53,7 +53,7 @@ struct Work {
   uint32_t* rm;     // [9][ns]  r * 2^270 mod p (canonical)
   uint32_t* r2m;    // [9][ns]  (r + n) * 2^270 mod p   (valid iff ST_R2OK)
   uint8_t* st;      // [ns]
-  uint32_t* qtab;   // [ns/64][16][27][64]  per-wave Q multiples 1..16 (Jacobian, radix 2^30)
+  uint32_t* qtab;   // [ns/64][64 lanes][16][28]  per-lane Q multiples 1..16 (Jacobian, radix 2^30)
 };
 
 // G comb table: window w in [0, 33), entry j in [0, 128): (j+1) * 2^(8w) * G,
@@ -63,7 +63,7 @@ constexpr int kCombWindows = 33;
 constexpr int kCombEntries = 128;
 constexpr int kGEntry = 18;
 constexpr int kQTab = 16;
-constexpr int kQPt = 27;  // words per Jacobian point in the Q table
+constexpr int kQPt = 28;  // words per Jacobian point in the Q table (27 + pad)
 
 BH_HD void ld8(uint32_t v[8], const uint32_t* base, uint32_t i, uint32_t ns) {
 #pragma unroll
@@ -224,26 +224,49 @@ BH_HD void booth5(uint32_t in6, uint32_t* mag, bool* neg) {
   *neg = sgn != 0;
 }
 
-// Q-table slot address for (wave, entry, word-of-27, lane)
-BH_HD size_t qtab_idx(uint32_t wave, uint32_t entry, uint32_t limb, uint32_t lane) {
-  return (((size_t)wave * kQTab + entry) * kQPt + limb) * 64 + lane;
+// Q table: each lane owns a contiguous run of 16 entries x 28 words (27 used:
+// X, Y, Z radix 2^30; padded to 112 B = 7 x 16 B) at
+// ((wave * 64 + lane) * 16 + entry) * 28. A lookup is seven 16-byte loads that
+// touch ~2 cache lines per lane; the earlier lane-interleaved layout touched
+// one line per distinct digit per word (measured ~16x L2-miss traffic).
+struct alignas(16) W4 {
+  uint32_t x, y, z, w;
+};
+
+BH_HD uint32_t* qtab_entry(uint32_t* tab, uint32_t wave, uint32_t entry, uint32_t lane) {
+  return tab + (((size_t)wave * 64 + lane) * kQTab + entry) * kQPt;
 }
 
 BH_HD void qtab_store(uint32_t* tab, uint32_t wave, uint32_t entry, uint32_t lane, const J30& P) {
+  uint32_t v[28];
 #pragma unroll
   for (int k = 0; k < 9; k++) {
-    tab[qtab_idx(wave, entry, k, lane)] = P.X[k];
-    tab[qtab_idx(wave, entry, 9 + k, lane)] = P.Y[k];
-    tab[qtab_idx(wave, entry, 18 + k, lane)] = P.Z[k];
+    v[k] = P.X[k];
+    v[9 + k] = P.Y[k];
+    v[18 + k] = P.Z[k];
   }
+  v[27] = 0;
+  W4* d = reinterpret_cast<W4*>(qtab_entry(tab, wave, entry, lane));
+#pragma unroll
+  for (int q = 0; q < 7; q++) d[q] = W4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
 }
 
 BH_HD void qtab_load(J30& P, const uint32_t* tab, uint32_t wave, uint32_t entry, uint32_t lane) {
+  const W4* s = reinterpret_cast<const W4*>(qtab_entry(const_cast<uint32_t*>(tab), wave, entry, lane));
+  uint32_t v[28];
+#pragma unroll
+  for (int q = 0; q < 7; q++) {
+    const W4 t = s[q];
+    v[4 * q] = t.x;
+    v[4 * q + 1] = t.y;
+    v[4 * q + 2] = t.z;
+    v[4 * q + 3] = t.w;
+  }
 #pragma unroll
   for (int k = 0; k < 9; k++) {
-    P.X[k] = tab[qtab_idx(wave, entry, k, lane)];
-    P.Y[k] = tab[qtab_idx(wave, entry, 9 + k, lane)];
-    P.Z[k] = tab[qtab_idx(wave, entry, 18 + k, lane)];
+    P.X[k] = v[k];
+    P.Y[k] = v[9 + k];
+    P.Z[k] = v[18 + k];
   }
 }
 
