@@ -41,7 +41,12 @@ class BhBatch(ctypes.Structure):
 
 class BhTiming(ctypes.Structure):
     _fields_ = [("prep_ms", ctypes.c_float), ("inv_ms", ctypes.c_float),
-                ("ladder_ms", ctypes.c_float)]
+                ("plan_ms", ctypes.c_float), ("ktab_ms", ctypes.c_float),
+                ("keycomb_ms", ctypes.c_float), ("ladder_ms", ctypes.c_float),
+                ("n_keycomb", ctypes.c_uint32), ("n_ladder", ctypes.c_uint32),
+                ("n_keytables", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+    STAGES = ("prep_ms", "inv_ms", "plan_ms", "ktab_ms", "keycomb_ms", "ladder_ms")
 
 
 class EngineError(RuntimeError):

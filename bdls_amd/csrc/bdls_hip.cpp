@@ -20,9 +20,9 @@
 
 namespace bh {
 hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s);
-hipError_t launch_verify(int curve, const BatchIn& in, const Work& w, const uint32_t* gtab,
-                         uint32_t n, uint32_t chunk, uint64_t* bitmap, uint8_t* reason,
-                         hipStream_t s);
+hipError_t launch_verify(int curve, const BatchIn& in, const Work& w, const Plan& pl,
+                         const uint32_t* gtab, uint32_t n, uint32_t chunk, uint64_t* bitmap,
+                         uint8_t* reason, hipStream_t s, hipEvent_t* ev);
 }  // namespace bh
 
 namespace {
@@ -72,7 +72,7 @@ struct Dev {
   DevBuf ws;        // Work arrays
   DevBuf in_fix;    // host-API staging: pub, offsets, lengths
   DevBuf in_sig, in_msg, out;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   std::mutex mu;
 };
 
@@ -81,13 +81,28 @@ std::vector<Dev*> g_devs;
 
 size_t round64(size_t n) { return (n + 63) & ~size_t(63); }
 
-size_t work_bytes(size_t ns) {
-  // 4 scalar SoA arrays (8 limbs) + 4 base-field SoA arrays (9 limbs) + status
-  // + per-wave Q tables, each carve rounded to 256 bytes
-  return 4 * 32 * ns + 4 * 36 * ns + ns + (ns / 64) * bh::kQTab * bh::kQPt * 64 * 4 + 256 * 16;
+size_t pow2_at_least(size_t v) {
+  size_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
 }
 
-int carve_work(Dev& d, size_t n, bh::Work* w) {
+size_t max_tables_for(size_t ns) {
+  return std::min<size_t>(ns / bh::kMinUses, size_t(1) << 16);
+}
+
+size_t work_bytes(size_t ns) {
+  // 4 scalar SoA arrays (8 limbs) + 4 base-field SoA arrays (9 limbs) + status
+  // + per-lane Q tables; then the key plan (fingerprint table, lists, key
+  // tables). Every carve is rounded to 256 bytes.
+  const size_t hc = pow2_at_least(2 * ns);
+  const size_t mt = max_tables_for(ns);
+  return 4 * 32 * ns + 4 * 36 * ns + ns + (ns / 64) * 64 * bh::kQTab * bh::kQPt * 4 +
+         hc * (8 + 4 + 4 + 4) + ns * 12 + 16 + mt * 4 + mt * (size_t)bh::kKTabWords * 4 +
+         256 * 24;
+}
+
+int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl) {
   const size_t ns = round64(n);
   int rc = d.ws.ensure(work_bytes(ns));
   if (rc) return rc;
@@ -107,7 +122,21 @@ int carve_work(Dev& d, size_t n, bh::Work* w) {
   w->rm = (uint32_t*)take(36 * ns);
   w->r2m = (uint32_t*)take(36 * ns);
   w->st = (uint8_t*)take(ns);
-  w->qtab = (uint32_t*)take((ns / 64) * bh::kQTab * bh::kQPt * 64 * 4);
+  w->qtab = (uint32_t*)take((ns / 64) * 64 * bh::kQTab * bh::kQPt * 4);
+  const size_t hc = pow2_at_least(2 * ns);
+  const size_t mt = max_tables_for(ns);
+  pl->hc = (uint32_t)hc;
+  pl->max_tables = (uint32_t)mt;
+  pl->slot_hash = (uint64_t*)take(hc * 8);
+  pl->slot_rep = (uint32_t*)take(hc * 4);
+  pl->slot_cnt = (uint32_t*)take(hc * 4);
+  pl->slot_tab = (uint32_t*)take(hc * 4);
+  pl->rec_slot = (uint32_t*)take(ns * 4);
+  pl->comb_list = (uint32_t*)take(ns * 4);
+  pl->ladder_list = (uint32_t*)take(ns * 4);
+  pl->counters = (uint32_t*)take(16);
+  pl->tab_rec = (uint32_t*)take(mt * 4 + 4);
+  pl->tables = (uint32_t*)take(mt * (size_t)bh::kKTabWords * 4 + 4);
   return BH_OK;
 }
 
@@ -157,37 +186,42 @@ uint32_t inv_chunk(size_t n) {
 }
 
 // Core device-resident pass (caller holds d.mu and has set the device).
+// With t != nullptr, events bracket every stage and the call synchronises.
 int run_dev(Dev& d, int curve, const bh_batch* b, size_t n, uint32_t flags, uint64_t* bitmap,
-            uint8_t* reason, hipStream_t s) {
+            uint8_t* reason, hipStream_t s, bh_timing* t) {
+  if (t) *t = bh_timing{};
   for (size_t base = 0; base < n; base += kMaxChunk) {
     const size_t m = std::min(kMaxChunk, n - base);
     bh::Work w;
-    int rc = carve_work(d, m, &w);
+    bh::Plan pl;
+    int rc = carve_work(d, m, &w, &pl);
     if (rc) return rc;
-    bh::BatchIn in;
-    in.pub = b->pub + base * 64;
-    in.sig = b->sig;
-    in.sig_off = b->sig_off + base;
-    in.sig_len = b->sig_len + base;
-    in.msg = b->msg;
-    in.msg_off = b->msg_off + base;
-    in.msg_len = b->msg_len + base;
-    in.flags = flags;
-    HIPCHK(bh::launch_verify(curve, in, w, d.gtab[curve], (uint32_t)m, inv_chunk(m),
-                             bitmap + base / 64, reason + base, s));
+    bh::BatchIn in{b->pub + base * 64, b->sig, b->sig_off + base, b->sig_len + base,
+                   b->msg, b->msg_off + base, b->msg_len + base, flags};
+    HIPCHK(bh::launch_verify(curve, in, w, pl, d.gtab[curve], (uint32_t)m, inv_chunk(m),
+                             bitmap + base / 64, reason + base, s, t ? d.ev : nullptr));
+    if (t) {
+      HIPCHK(hipEventSynchronize(d.ev[6]));
+      float ms[6];
+      for (int k = 0; k < 6; k++) HIPCHK(hipEventElapsedTime(&ms[k], d.ev[k], d.ev[k + 1]));
+      t->prep_ms += ms[0];
+      t->inv_ms += ms[1];
+      t->plan_ms += ms[2];
+      t->ktab_ms += ms[3];
+      t->keycomb_ms += ms[4];
+      t->ladder_ms += ms[5];
+      uint32_t cnt[4];
+      HIPCHK(hipMemcpy(cnt, pl.counters, 16, hipMemcpyDeviceToHost));
+      t->n_keycomb += cnt[0];
+      t->n_ladder += cnt[1];
+      t->n_keytables += std::min<uint32_t>(cnt[2], pl.max_tables);
+    }
   }
   return BH_OK;
 }
 
 }  // namespace
 
-// ---------------------------------------------------------------------------
-// timed variant of the launch sequence: events between the three kernels
-namespace bh {
-hipError_t launch_verify_timed(int curve, const BatchIn& in, const Work& w, const uint32_t* gtab,
-                               uint32_t n, uint32_t chunk, uint64_t* bitmap, uint8_t* reason,
-                               hipStream_t s, hipEvent_t ev[4]);
-}
 
 extern "C" {
 
@@ -249,31 +283,9 @@ int bh_verify_dev(int device, int curve, const bh_batch* b, size_t n, uint32_t f
   HIPCHK(hipSetDevice(d->id));
   hipStream_t s = stream ? (hipStream_t)stream : d->stream;
   if (n == 0) return BH_OK;
-  if (timing) {
-    *timing = bh_timing{0.f, 0.f, 0.f};
-    for (size_t base = 0; base < n; base += kMaxChunk) {
-      const size_t m = std::min(kMaxChunk, n - base);
-      bh::Work w;
-      int rc = carve_work(*d, m, &w);
-      if (rc) return rc;
-      bh::BatchIn in{b->pub + base * 64, b->sig, b->sig_off + base, b->sig_len + base,
-                     b->msg, b->msg_off + base, b->msg_len + base, flags};
-      HIPCHK(bh::launch_verify_timed(curve, in, w, d->gtab[curve], (uint32_t)m, inv_chunk(m),
-                                     bitmap_words + base / 64, reason + base, s, d->ev));
-      HIPCHK(hipEventSynchronize(d->ev[3]));
-      float a = 0, bb = 0, c = 0;
-      HIPCHK(hipEventElapsedTime(&a, d->ev[0], d->ev[1]));
-      HIPCHK(hipEventElapsedTime(&bb, d->ev[1], d->ev[2]));
-      HIPCHK(hipEventElapsedTime(&c, d->ev[2], d->ev[3]));
-      timing->prep_ms += a;
-      timing->inv_ms += bb;
-      timing->ladder_ms += c;
-    }
-    return BH_OK;
-  }
-  int rc = run_dev(*d, curve, b, n, flags, bitmap_words, reason, s);
+  int rc = run_dev(*d, curve, b, n, flags, bitmap_words, reason, s, timing);
   if (rc) return rc;
-  if (sync) HIPCHK(hipStreamSynchronize(s));
+  if (sync && !timing) HIPCHK(hipStreamSynchronize(s));
   return BH_OK;
 }
 
@@ -342,7 +354,7 @@ int bh_verify(int curve, const bh_batch* b, size_t n, uint32_t flags, uint8_t* b
       if (mmax > mmin)
         HIPCHK(hipMemcpyAsync(d.in_msg.p, b->msg + mmin, mmax - mmin, hipMemcpyHostToDevice, s));
       bh_batch db{dpub, (const uint8_t*)d.in_sig.p, dso, dsl, (const uint8_t*)d.in_msg.p, dmo, dml};
-      rc = run_dev(d, curve, &db, m, flags, dbm, drs, s);
+      rc = run_dev(d, curve, &db, m, flags, dbm, drs, s, nullptr);
       if (rc) return rc;
       std::vector<uint64_t> words(round64(m) / 64);
       HIPCHK(hipMemcpyAsync(words.data(), dbm, words.size() * 8, hipMemcpyDeviceToHost, s));
@@ -451,38 +463,3 @@ int bh_sync(int device) {
 
 }  // extern "C"
 
-// ---------------------------------------------------------------------------
-// Debug-only export (not in the public header): run the three stages on a
-// device-resident batch and copy every intermediate SoA array back to `dump`
-// after each stage: layout = 3 snapshots x [e, r, sm, qx, qy, rm][8][ns] u32
-// followed by 3 x st[ns] bytes. Used by tools/ to bisect device/host
-// differences against tests/native/hostsim.cpp.
-namespace bh {
-hipError_t launch_stage(int stage, const BatchIn& in, const Work& w, const uint32_t* gtab,
-                        uint32_t n, uint32_t chunk, uint64_t* bitmap, uint8_t* reason,
-                        hipStream_t s);
-}
-extern "C" int bhx_debug_verify(int device, const bh_batch* b, size_t n, uint32_t flags,
-                                uint64_t* bitmap_words, uint8_t* reason, uint32_t* dump) {
-  Dev* d = get_dev(device);
-  if (!d) return fail(BH_E_NOT_INIT, "device not initialised");
-  std::lock_guard<std::mutex> g(d->mu);
-  HIPCHK(hipSetDevice(d->id));
-  bh::Work w;
-  int rc = carve_work(*d, n, &w);
-  if (rc) return rc;
-  bh::BatchIn in{b->pub, b->sig, b->sig_off, b->sig_len, b->msg, b->msg_off, b->msg_len, flags};
-  const size_t ns = w.ns;
-  uint32_t* arrs[6] = {w.e, w.r, w.sm, w.qx, w.qy, w.rm};  // first 8 limbs of each
-  uint8_t* stdump = (uint8_t*)(dump + 3 * 6 * 8 * ns);
-  for (int stage = 0; stage < 3; stage++) {
-    HIPCHK(bh::launch_stage(stage, in, w, d->gtab[0], (uint32_t)n, inv_chunk(n), bitmap_words,
-                            reason, d->stream));
-    HIPCHK(hipStreamSynchronize(d->stream));
-    for (int a = 0; a < 6; a++)
-      HIPCHK(hipMemcpy(dump + ((size_t)stage * 6 + a) * 8 * ns, arrs[a], 8 * ns * 4,
-                       hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(stdump + stage * ns, w.st, ns, hipMemcpyDeviceToHost));
-  }
-  return BH_OK;
-}

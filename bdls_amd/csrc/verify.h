@@ -56,6 +56,24 @@ struct Work {
   uint32_t* qtab;   // [ns/64][64 lanes][16][28]  per-lane Q multiples 1..16 (Jacobian, radix 2^30)
 };
 
+// Per-batch key plan (device): open-addressed fingerprint table for key
+// dedup, per-record slot, work lists and per-key comb tables.
+struct Plan {
+  uint32_t hc;          // fingerprint table capacity (power of two >= 2 n)
+  uint32_t max_tables;  // key tables available
+  uint64_t* slot_hash;  // [hc] 0 = empty
+  uint32_t* slot_rep;   // [hc] smallest record index with this fingerprint
+  uint32_t* slot_cnt;   // [hc] records verified equal to the representative key
+  uint32_t* slot_tab;   // [hc] key-table index or kNone
+  uint32_t* rec_slot;   // [ns] slot or kNone
+  uint32_t* comb_list;  // [ns] records on the key-comb path
+  uint32_t* ladder_list;  // [ns] records on the variable-base ladder path
+  uint32_t* counters;   // [0] n_comb, [1] n_ladder, [2] n_tables
+  uint32_t* tab_rec;    // [max_tables] record whose Q builds the table
+  uint32_t* tables;     // [max_tables][kKWin][kKEnt][kQPt]
+};
+constexpr uint32_t kNone = 0xffffffffu;
+
 // G comb table: window w in [0, 33), entry j in [0, 128): (j+1) * 2^(8w) * G,
 // affine, canonical radix-2^30 Montgomery x (limbs 0..8) and y (limbs 9..17),
 // padded to kGEntry words.
@@ -311,84 +329,13 @@ BH_HD void gtab_entry(uint32_t t, uint32_t* out) {
   }
 }
 
-// Returns true iff the signature equation holds (valid). Lanes whose prep
-// failed run on placeholder inputs (Q = G, u1 = u2 = 1) and are masked by the
-// caller.
+// ---- shared tail: u1 G by the fixed-base comb, then A + B and the x check
+// u1 G: 8-bit signed windows over the L2-resident affine table (33 mixed adds).
 template <class P>
-BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_t wave,
-                        uint32_t lane) {
-  uint32_t u1[8], u2[8], qx[9], qy[9];
-  ld8(u1, w.e, i, w.ns);
-  ld8(u2, w.r, i, w.ns);
-  ld9(qx, w.qx, i, w.ns);
-  ld9(qy, w.qy, i, w.ns);
+BH_HD void g_comb(J30& B, bool& b_inf, const uint32_t* gtab, const uint32_t u1[8]) {
   uint32_t one[9];
   f_const(one, P::r1);
-
-  // ---- Q multiples 1..16 (Jacobian) into this wave's scratch slab
-  J30 T;
-  f_copy(T.X, qx);
-  f_copy(T.Y, qy);
-  f_copy(T.Z, one);
-  qtab_store(w.qtab, wave, 0, lane, T);
-  j_dbl<P>(T, T);
-  qtab_store(w.qtab, wave, 1, lane, T);
-  for (uint32_t k = 2; k < kQTab; k++) {
-    bool same;
-    j_madd<P>(T, T, qx, qy, &same);  // (k+1) Q = k Q + Q, never degenerate for 2 <= k < 16
-    qtab_store(w.qtab, wave, k, lane, T);
-  }
-
-  // ---- u2 Q: Booth w=5 windows, most significant first. K = u2 << 28 (288 bits)
-  uint32_t K[9];
-  K[0] = u2[0] << 28;
-#pragma unroll
-  for (int k = 1; k < 8; k++) K[k] = (u2[k] << 28) | (u2[k - 1] >> 4);
-  K[8] = u2[7] >> 4;
-
-  J30 A;
-  bool a_inf;
-  {
-    uint32_t mag;
-    bool neg;
-    booth5(K[8] >> 26, &mag, &neg);
-#pragma unroll
-    for (int k = 8; k > 0; k--) K[k] = (K[k] << 5) | (K[k - 1] >> 27);
-    K[0] <<= 5;
-    qtab_load(A, w.qtab, wave, mag ? mag - 1 : 0, lane);
-    if (neg) f_neg<P, 64>(A.Y, A.Y);
-    a_inf = (mag == 0);
-  }
-  for (int win = 50; win >= 0; win--) {
-    uint32_t mag;
-    bool neg;
-    booth5(K[8] >> 26, &mag, &neg);
-#pragma unroll
-    for (int k = 8; k > 0; k--) K[k] = (K[k] << 5) | (K[k - 1] >> 27);
-    K[0] <<= 5;
-    J30 T2;
-    qtab_load(T2, w.qtab, wave, mag ? mag - 1 : 0, lane);  // issued before the doublings
-    for (int d = 0; d < 5; d++) j_dbl<P>(A, A);
-    if (neg) f_neg<P, 64>(T2.Y, T2.Y);
-    J30 R;
-    bool same;
-    const bool deg = j_add<P>(R, A, T2, &same);
-    const bool take = mag != 0;
-    const bool use_t = take && a_inf;
-    const bool use_r = take && !a_inf && !deg;
-    const bool rare = take && !a_inf && deg;
-    j_sel(A, use_r, R, A);
-    j_sel(A, use_t, T2, A);
-    if (rare) {  // A == +-T: only reachable at the last window for crafted u2
-      if (same) j_dbl<P>(A, T2);
-      else a_inf = true;
-    }
-    if (use_t) a_inf = false;
-  }
-
-  // ---- u1 G: fixed-base comb, 8-bit signed windows, affine table in HBM/L2
-  J30 B;
-  bool b_inf = true;
+  b_inf = true;
   f_copy(B.X, one);
   f_copy(B.Y, one);
   f_copy(B.Z, one);
@@ -445,8 +392,13 @@ BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_
     }
     if (use_t) b_inf = false;
   }
+}
 
-  // ---- Pt = A + B, then x(Pt) mod n == r  <=>  X == r Z^2  or  X == (r+n) Z^2
+// Pt = A + B (explicit doubling / infinity), then x(Pt) mod n == r  <=>
+// X == r Z^2  or  (r + n < p and) X == (r + n) Z^2.
+template <class P>
+BH_HD bool finish_check(const Work& w, uint32_t i, const J30& A, bool a_inf, const J30& B,
+                        bool b_inf) {
   J30 Pt;
   bool p_inf;
   if (b_inf) {
@@ -479,6 +431,240 @@ BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_
     ok = ok || f_eq(t, x);
   }
   return ok && !p_inf && !z_zero;
+}
+
+// Variable-base path: Q multiples 1..16 in the lane's scratch slab (slot =
+// (wave, lane)), Booth w=5 windows over u2, most significant first.
+template <class P>
+BH_HD void q_ladder(J30& A, bool& a_inf, const Work& w, uint32_t i, uint32_t wave,
+                    uint32_t lane) {
+  uint32_t u2[8], qx[9], qy[9], one[9];
+  ld8(u2, w.r, i, w.ns);
+  ld9(qx, w.qx, i, w.ns);
+  ld9(qy, w.qy, i, w.ns);
+  f_const(one, P::r1);
+  J30 T;
+  f_copy(T.X, qx);
+  f_copy(T.Y, qy);
+  f_copy(T.Z, one);
+  qtab_store(w.qtab, wave, 0, lane, T);
+  j_dbl<P>(T, T);
+  qtab_store(w.qtab, wave, 1, lane, T);
+  for (uint32_t k = 2; k < kQTab; k++) {
+    bool same;
+    j_madd<P>(T, T, qx, qy, &same);  // (k+1) Q = k Q + Q, never degenerate for 2 <= k < 16
+    qtab_store(w.qtab, wave, k, lane, T);
+  }
+  // K = u2 << 28 (288 bits): window i's 6 Booth bits sit at the top after 51-i shifts
+  uint32_t K[9];
+  K[0] = u2[0] << 28;
+#pragma unroll
+  for (int k = 1; k < 8; k++) K[k] = (u2[k] << 28) | (u2[k - 1] >> 4);
+  K[8] = u2[7] >> 4;
+  {
+    uint32_t mag;
+    bool neg;
+    booth5(K[8] >> 26, &mag, &neg);
+#pragma unroll
+    for (int k = 8; k > 0; k--) K[k] = (K[k] << 5) | (K[k - 1] >> 27);
+    K[0] <<= 5;
+    qtab_load(A, w.qtab, wave, mag ? mag - 1 : 0, lane);
+    if (neg) f_neg<P, 64>(A.Y, A.Y);
+    a_inf = (mag == 0);
+  }
+  for (int win = 50; win >= 0; win--) {
+    uint32_t mag;
+    bool neg;
+    booth5(K[8] >> 26, &mag, &neg);
+#pragma unroll
+    for (int k = 8; k > 0; k--) K[k] = (K[k] << 5) | (K[k - 1] >> 27);
+    K[0] <<= 5;
+    J30 T2;
+    qtab_load(T2, w.qtab, wave, mag ? mag - 1 : 0, lane);  // issued before the doublings
+    for (int d = 0; d < 5; d++) j_dbl<P>(A, A);
+    if (neg) f_neg<P, 64>(T2.Y, T2.Y);
+    J30 R;
+    bool same;
+    const bool deg = j_add<P>(R, A, T2, &same);
+    const bool take = mag != 0;
+    const bool use_t = take && a_inf;
+    const bool use_r = take && !a_inf && !deg;
+    const bool rare = take && !a_inf && deg;
+    j_sel(A, use_r, R, A);
+    j_sel(A, use_t, T2, A);
+    if (rare) {  // A == +-T: only reachable at the last window for crafted u2
+      if (same) j_dbl<P>(A, T2);
+      else a_inf = true;
+    }
+    if (use_t) a_inf = false;
+  }
+}
+
+// Returns true iff the signature equation holds (valid). Lanes whose prep
+// failed run on placeholder inputs (Q = G, u1 = u2 = 1) and are masked by the
+// caller.
+template <class P>
+BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_t wave,
+                        uint32_t lane) {
+  J30 A, B;
+  bool a_inf, b_inf;
+  q_ladder<P>(A, a_inf, w, i, wave, lane);
+  uint32_t u1[8];
+  ld8(u1, w.e, i, w.ns);
+  g_comb<P>(B, b_inf, gtab, u1);
+  return finish_check<P>(w, i, A, a_inf, B, b_inf);
+}
+
+// ---------------------------------------------------------------- per-key comb
+// Records whose public key occurs >= kMinUses times in the batch share one
+// fixed-base table for their key, built inside the same step:
+//   entry (win, j) = (j+1) 2^(4 win) Q,  win in [0, 65), j in [0, 8)
+// (Jacobian, 28 words). u2 Q is then 65 table additions with 4-bit signed
+// digits in [-7, 8] and no doublings.
+constexpr int kKWin = 65;
+constexpr int kKEnt = 8;
+constexpr uint32_t kKTabWords = (uint32_t)kKWin * kKEnt * kQPt;
+constexpr uint32_t kMinUses = 4;
+
+BH_HD void ktab_store(uint32_t* tab, uint32_t win, uint32_t j, const J30& P) {
+  uint32_t v[28];
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    v[k] = P.X[k];
+    v[9 + k] = P.Y[k];
+    v[18 + k] = P.Z[k];
+  }
+  v[27] = 0;
+  W4* d = reinterpret_cast<W4*>(tab + ((size_t)win * kKEnt + j) * kQPt);
+#pragma unroll
+  for (int q = 0; q < 7; q++) d[q] = W4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+}
+
+BH_HD void ktab_load(J30& P, const uint32_t* tab, uint32_t win, uint32_t j) {
+  const W4* s = reinterpret_cast<const W4*>(tab + ((size_t)win * kKEnt + j) * kQPt);
+  uint32_t v[28];
+#pragma unroll
+  for (int q = 0; q < 7; q++) {
+    const W4 t = s[q];
+    v[4 * q] = t.x;
+    v[4 * q + 1] = t.y;
+    v[4 * q + 2] = t.z;
+    v[4 * q + 3] = t.w;
+  }
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    P.X[k] = v[k];
+    P.Y[k] = v[9 + k];
+    P.Z[k] = v[18 + k];
+  }
+}
+
+// Build one key table from the canonical Montgomery (qx, qy) of record `rec`.
+template <class P>
+BH_HD void ktab_build(uint32_t* tab, const Work& w, uint32_t rec) {
+  J30 B, E2, E3, E4, T;
+  ld9(B.X, w.qx, rec, w.ns);
+  ld9(B.Y, w.qy, rec, w.ns);
+  f_const(B.Z, P::r1);
+  bool same;
+  for (uint32_t win = 0; win < (uint32_t)kKWin; win++) {
+    ktab_store(tab, win, 0, B);                 // 1 B
+    j_dbl<P>(E2, B);
+    ktab_store(tab, win, 1, E2);                // 2 B
+    j_add<P>(E3, E2, B, &same);
+    ktab_store(tab, win, 2, E3);                // 3 B
+    j_dbl<P>(E4, E2);
+    ktab_store(tab, win, 3, E4);                // 4 B
+    j_add<P>(T, E4, B, &same);
+    ktab_store(tab, win, 4, T);                 // 5 B
+    j_dbl<P>(T, E3);
+    ktab_store(tab, win, 5, T);                 // 6 B
+    j_add<P>(T, T, B, &same);
+    ktab_store(tab, win, 6, T);                 // 7 B
+    j_dbl<P>(T, E4);
+    ktab_store(tab, win, 7, T);                 // 8 B
+    j_dbl<P>(B, T);                             // next window base: 16 B
+  }
+}
+
+// u2 Q from a key table: 4-bit signed windows (least significant first).
+template <class P>
+BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab) {
+  uint32_t k2[8];
+  ld8(k2, w.r, i, w.ns);
+  a_inf = true;
+  f_const(A.X, P::r1);
+  f_const(A.Y, P::r1);
+  f_const(A.Z, P::r1);
+  uint32_t carry = 0;
+  for (int win = 0; win < kKWin; win++) {
+    uint32_t v = (k2[0] & 0xfu) + carry;
+#pragma unroll
+    for (int k = 0; k < 7; k++) k2[k] = (k2[k] >> 4) | (k2[k + 1] << 28);
+    k2[7] >>= 4;
+    uint32_t mag;
+    bool neg;
+    if (v > 8u) {
+      mag = 16u - v;
+      neg = true;
+      carry = 1;
+    } else {
+      mag = v;
+      neg = false;
+      carry = 0;
+    }
+    J30 T;
+    ktab_load(T, tab, win, mag ? mag - 1 : 0);
+    if (neg) f_neg<P, 64>(T.Y, T.Y);
+    J30 R;
+    bool same;
+    const bool deg = j_add<P>(R, A, T, &same);
+    const bool take = mag != 0;
+    const bool use_t = take && a_inf;
+    const bool use_r = take && !a_inf && !deg;
+    const bool rare = take && !a_inf && deg;  // only via the mod-n wrap of the top window
+    j_sel(A, use_r, R, A);
+    j_sel(A, use_t, T, A);
+    if (rare) {
+      if (same) j_dbl<P>(A, T);
+      else a_inf = true;
+    }
+    if (use_t) a_inf = false;
+  }
+}
+
+template <class P>
+BH_HD bool stage_keycomb(const Work& w, const uint32_t* gtab, uint32_t i, const uint32_t* tab) {
+  J30 A, B;
+  bool a_inf, b_inf;
+  q_keycomb<P>(A, a_inf, w, i, tab);
+  uint32_t u1[8];
+  ld8(u1, w.e, i, w.ns);
+  g_comb<P>(B, b_inf, gtab, u1);
+  return finish_check<P>(w, i, A, a_inf, B, b_inf);
+}
+
+// 64-bit key fingerprint of the canonical Montgomery Q (never 0).
+BH_HD uint64_t key_hash(const Work& w, uint32_t i) {
+  uint64_t h = 0x9e3779b97f4a7c15ull;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    h ^= w.qx[(size_t)k * w.ns + i];
+    h *= 0xff51afd7ed558ccdull;
+    h ^= (uint64_t)w.qy[(size_t)k * w.ns + i] << 32;
+    h ^= h >> 29;
+  }
+  return h ? h : 1;
+}
+
+BH_HD bool same_key(const Work& w, uint32_t a, uint32_t b) {
+  uint32_t d = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    d |= w.qx[(size_t)k * w.ns + a] ^ w.qx[(size_t)k * w.ns + b];
+    d |= w.qy[(size_t)k * w.ns + a] ^ w.qy[(size_t)k * w.ns + b];
+  }
+  return d == 0;
 }
 
 }  // namespace bh

@@ -27,9 +27,14 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# Algorithmic work per verify (SURVEY.md 8(d) schedule S0):
-# 3.2e3 F_p mul/sqr x 128 u32 MACs (64 product + 64 reduction) = 4.1e5 MACs.
-MACS_PER_VERIFY = 4.1e5
+# Algorithmic work per verify in SURVEY.md 8(d) units: F_p mul/sqr x 128 u32
+# MACs (64 product + 64 reduction). The variable-base ladder is schedule S0
+# (3.2e3 F_p ops = 4.1e5 MACs). The per-key comb path does 65 Jacobian adds
+# (16 ops) + 33 mixed adds (11 ops) + ~23 for the final add/x check = 1,426
+# F_p ops per verify, plus 65 x (5 dbl x 8 + 3 add x 16) = 5,720 per key table.
+MAC_PER_FP = 128
+FP_OPS = {"ladder_ms": 3200, "keycomb_ms": 1426, "ktab_ms": 5720}
+MACS_PER_VERIFY = FP_OPS["ladder_ms"] * MAC_PER_FP
 # Algorithmic HBM bytes per verify record (config 2): pub 64 + sig ~71 + msg 256
 # + offsets/lengths 24 + reason 1 + bitmap 1/8.
 def alg_bytes_per_record(msg_len: int) -> float:
@@ -109,11 +114,12 @@ def main():
     dist.barrier(world)
     _lib.check(L.bh_sync(local))
     t0 = time.perf_counter()
-    kern = {"prep_ms": 0.0, "inv_ms": 0.0, "ladder_ms": 0.0}
+    kern = {k: 0.0 for k in _lib.BhTiming.STAGES}
     for _ in range(a.steps):
-        step(tm)  # HIP events around each kernel (synchronises at the end of each step)
+        step(tm)  # HIP events around each stage (synchronises at the end of each step)
         for k in kern:
             kern[k] += getattr(tm, k)
+    routes = {"keycomb": tm.n_keycomb, "ladder": tm.n_ladder, "key_tables": tm.n_keytables}
     _lib.check(L.bh_sync(local))
     t1 = time.perf_counter()
     dist.barrier(world)
@@ -129,9 +135,13 @@ def main():
     total = n * world * a.steps
     value = total / elapsed
     ms_per_step = elapsed * 1e3 / a.steps
-    ladder_avg_s = kern["ladder_ms"] * 1e-3 / a.steps
     peak, peak_src = (a.mac_peak, "--mac-peak") if a.mac_peak else mac_peak_default()
-    achieved = n * MACS_PER_VERIFY / ladder_avg_s if ladder_avg_s > 0 else 0.0
+    # dominant kernel of the step and its algorithmic work per launch
+    dom = max(("ladder_ms", "keycomb_ms", "ktab_ms"), key=lambda k: kern[k])
+    units = {"ladder_ms": routes["ladder"], "keycomb_ms": routes["keycomb"],
+             "ktab_ms": routes["key_tables"]}[dom]
+    dom_avg_s = kern[dom] * 1e-3 / a.steps
+    achieved = units * FP_OPS[dom] * MAC_PER_FP / dom_avg_s if dom_avg_s > 0 else 0.0
 
     out = {
         "metric": "P-256 ECDSA verifies/sec (fused SHA-256, bit-exact vs Go crypto/ecdsa + Fabric low-S)",
@@ -154,14 +164,17 @@ def main():
         },
         "parity": parity_ok,
         "kernel_ms_per_step": {k: round(v / a.steps, 3) for k, v in kern.items()},
+        "routes": routes,
         "roofline": {
             "bound": "valu",
-            "kernel": "k_ladder",
+            "kernel": {"ladder_ms": "k_ladder", "keycomb_ms": "k_keycomb", "ktab_ms": "k_ktab_build"}[dom],
             "achieved": achieved / 1e12,
             "peak": peak / 1e12,
             "unit": "TMAC/s (u32 x u32 -> u64)",
             "frac": achieved / peak if peak else None,
-            "work_per_unit": f"{MACS_PER_VERIFY:.2e} MAC/verify (SURVEY 8(d) S0)",
+            "work_per_unit": f"{FP_OPS[dom]} F_p mul/sqr x {MAC_PER_FP} u32 MACs per "
+                             f"{'key table' if dom == 'ktab_ms' else 'verify'} (SURVEY 8(d) units)",
+            "units_per_launch": units,
             "peak_source": peak_src,
             "traffic": None,
             "alg_bytes_per_record": alg_bytes_per_record(a.msg_len),

@@ -71,11 +71,19 @@ typedef struct bh_batch {
   const uint32_t *msg_len; /* n lengths (digest mode: 0 -> BH_R_EMPTY_DIGEST)            */
 } bh_batch;
 
-/* Per-call kernel timing (milliseconds, HIP events on the launch stream). */
+/* Per-call stage timing (milliseconds, HIP events on the launch stream) and
+ * routing counts. */
 typedef struct bh_timing {
-  float prep_ms;   /* parse + checks + SHA-256 + Montgomery inputs */
-  float inv_ms;    /* batched s^-1 mod n, u1, u2 */
-  float ladder_ms; /* u1 G + u2 Q + x check + bitmap */
+  float prep_ms;       /* parse + checks + SHA-256 + Montgomery inputs */
+  float inv_ms;        /* batched s^-1 mod n, u1, u2 */
+  float plan_ms;       /* public-key dedup + routing */
+  float ktab_ms;       /* per-key fixed-base tables (keys used >= 4 times) */
+  float keycomb_ms;    /* u2 Q from key tables + u1 G + x check */
+  float ladder_ms;     /* u2 Q by variable-base ladder + u1 G + x check, bitmap */
+  uint32_t n_keycomb;  /* records verified on the key-table path */
+  uint32_t n_ladder;   /* records verified on the ladder path */
+  uint32_t n_keytables;
+  uint32_t reserved;
 } bh_timing;
 
 /* Initialise the devices in device_mask (bit d = HIP device d; 0 = all

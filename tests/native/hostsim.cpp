@@ -4,6 +4,7 @@
 // no GPU. Never linked into libbdlship.so; the product path has no CPU fallback.
 #include <cstdlib>
 #include <cstring>
+#include <unordered_map>
 #include <vector>
 
 #include "../../bdls_amd/csrc/verify.h"
@@ -18,23 +19,16 @@ static void build_gtab() {
     gtab_entry<F30_p256>(t, g_gtab.data() + (size_t)t * kGEntry);
 }
 
-extern "C" int hs_verify_dump(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
-                              const uint32_t* slen, const uint8_t* msg, const uint64_t* moff,
-                              const uint32_t* mlen, uint32_t n, uint32_t flags, uint32_t chunk,
-                              uint8_t* reason, uint32_t* dump);
-extern "C" int hs_verify(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
-                         const uint32_t* slen, const uint8_t* msg, const uint64_t* moff,
-                         const uint32_t* mlen, uint32_t n, uint32_t flags, uint32_t chunk,
-                         uint8_t* reason) {
-  return hs_verify_dump(pub, sig, soff, slen, msg, moff, mlen, n, flags, chunk, reason, nullptr);
-}
-extern "C" int hs_verify_dump(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
-                              const uint32_t* slen, const uint8_t* msg, const uint64_t* moff,
-                              const uint32_t* mlen, uint32_t n, uint32_t flags, uint32_t chunk,
-                              uint8_t* reason, uint32_t* dump) {
+// Sequential restatement of the device launch sequence (verify_kernels.hip
+// seq()): prep, inv, key dedup / plan / split, key tables, both verify paths.
+// min_uses overrides kMinUses so tests can force either path.
+extern "C" int hs_verify2(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
+                          const uint32_t* slen, const uint8_t* msg, const uint64_t* moff,
+                          const uint32_t* mlen, uint32_t n, uint32_t flags, uint32_t chunk,
+                          uint32_t min_uses, uint8_t* reason, uint32_t* n_comb) {
   if (g_gtab.empty()) build_gtab();
   const uint32_t ns = (n + 63) & ~63u;
-  std::vector<uint32_t> buf((size_t)9 * 9 * ns + (size_t)(ns / 64) * kQTab * kQPt * 64);
+  std::vector<uint32_t> buf((size_t)9 * 9 * ns + (size_t)(ns / 64) * 64 * kQTab * kQPt);
   std::vector<uint8_t> st(ns);
   Work w;
   w.ns = ns;
@@ -51,25 +45,54 @@ extern "C" int hs_verify_dump(const uint8_t* pub, const uint8_t* sig, const uint
   w.qtab = p;
   w.st = st.data();
   BatchIn in{pub, sig, soff, slen, msg, moff, mlen, flags};
-  uint32_t* arrs[6] = {w.e, w.r, w.sm, w.qx, w.qy, w.rm};
-  auto snap = [&](int stage) {
-    if (!dump) return;
-    for (int a = 0; a < 6; a++)
-      std::memcpy(dump + ((size_t)stage * 6 + a) * 8 * ns, arrs[a], 8 * (size_t)ns * 4);
-    std::memcpy((uint8_t*)(dump + 3 * 6 * 8 * (size_t)ns) + stage * ns, w.st, ns);
-  };
   for (uint32_t i = 0; i < n; i++) stage_prep<F30_p256, Fn_p256, Cv_p256>(in, w, i);
-  snap(0);
   for (uint32_t lo = 0; lo < n; lo += chunk)
     stage_inv<Fn_p256>(w, lo, lo + chunk < n ? lo + chunk : n);
-  snap(1);
+  // dedup: representative = first record with an equal key
+  std::vector<uint32_t> rep(n, kNone), cnt(n, 0);
+  std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;
   for (uint32_t i = 0; i < n; i++) {
-    const bool pre_ok = (w.st[i] & 0x7f) == R_OK;
-    bool ok = stage_ladder<F30_p256>(w, g_gtab.data(), i, i / 64, i % 64);
-    reason[i] = pre_ok ? (ok ? R_OK : R_MATH) : (uint8_t)(w.st[i] & 0x7f);
+    if ((w.st[i] & 0x7f) != R_OK) continue;
+    auto& v = by_hash[key_hash(w, i)];
+    uint32_t r = kNone;
+    if (!v.empty() && same_key(w, i, v[0])) r = v[0];
+    if (v.empty()) { v.push_back(i); r = i; }
+    rep[i] = r;
+    if (r != kNone) cnt[r]++;
   }
-  snap(2);
+  std::vector<uint32_t> tab_of(n, kNone);
+  std::vector<std::vector<uint32_t>> tables;
+  uint32_t combs = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if ((w.st[i] & 0x7f) != R_OK) {
+      reason[i] = w.st[i] & 0x7f;
+      continue;
+    }
+    const uint32_t r = rep[i];
+    bool ok;
+    if (r != kNone && cnt[r] >= min_uses) {
+      if (tab_of[r] == kNone) {
+        tab_of[r] = (uint32_t)tables.size();
+        tables.emplace_back(kKTabWords);
+        ktab_build<F30_p256>(tables.back().data(), w, r);
+      }
+      ok = stage_keycomb<F30_p256>(w, g_gtab.data(), i, tables[tab_of[r]].data());
+      combs++;
+    } else {
+      ok = stage_ladder<F30_p256>(w, g_gtab.data(), i, i / 64, i % 64);
+    }
+    reason[i] = ok ? R_OK : R_MATH;
+  }
+  if (n_comb) *n_comb = combs;
   return 0;
+}
+
+extern "C" int hs_verify(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
+                         const uint32_t* slen, const uint8_t* msg, const uint64_t* moff,
+                         const uint32_t* mlen, uint32_t n, uint32_t flags, uint32_t chunk,
+                         uint8_t* reason) {
+  return hs_verify2(pub, sig, soff, slen, msg, moff, mlen, n, flags, chunk, kMinUses, reason,
+                    nullptr);
 }
 
 // ---- field-op probes for tests/test_field30.py (bound stress) ----

@@ -92,7 +92,9 @@ def test_device_api(csp):
     bits = np.unpackbits(words.to_numpy(np.uint64, (w.n + 63) // 64).view(np.uint8),
                          bitorder="little")[:w.n]
     assert (bits.astype(bool) == w.expected_valid).all()
-    assert tm.ladder_ms > 0 and tm.prep_ms > 0
+    assert tm.prep_ms > 0 and tm.keycomb_ms + tm.ladder_ms > 0
+    # 100 keys over 5000 records: the key-table path is taken
+    assert tm.n_keytables > 0 and tm.n_keycomb > 0
     # async form + explicit sync gives the same answer
     _lib.check(_lib.lib().bh_verify_dev(0, 0, ctypes.byref(b), w.n, _lib.BH_F_HASH_SHA256,
                                         words.ptr, reason.ptr, None, 0, None))
@@ -183,3 +185,23 @@ def test_concurrent_callers(csp, golden):
     [t.start() for t in th]
     [t.join() for t in th]
     assert not errors
+
+
+@pytest.mark.parametrize("nkeys,min_frac", [(1, 0.99), (7, 0.99), (20_000, 0.0)])
+def test_key_routing(csp, nkeys, min_frac):
+    """Both verify paths, bit-exact: repeated keys -> per-key tables, unique keys -> ladder."""
+    from bdls_amd import workload
+    w = workload.generate(20_000, nkeys, 200, 8, seed=nkeys)
+    DA = _lib.DeviceArray
+    t = [DA.from_numpy(0, x) for x in w.arrays()]
+    words = DA(0, ((w.n + 63) // 64) * 8)
+    reason = DA(0, w.n)
+    b = _lib.BhBatch(*[x.ptr for x in t])
+    tm = _lib.BhTiming()
+    _lib.check(_lib.lib().bh_verify_dev(0, 0, ctypes.byref(b), w.n, _lib.BH_F_HASH_SHA256,
+                                        words.ptr, reason.ptr, None, 1, ctypes.byref(tm)))
+    assert (reason.to_numpy(np.uint8, w.n) == w.reason).all()
+    routed = tm.n_keycomb + tm.n_ladder
+    assert tm.n_keycomb >= min_frac * routed
+    if nkeys >= 20_000:
+        assert tm.n_keytables == 0

@@ -20,6 +20,7 @@ def hs():
     L = ctypes.CDLL(LIB)
     vp = ctypes.c_void_p
     L.hs_verify.argtypes = [vp] * 7 + [ctypes.c_uint32] * 3 + [vp]
+    L.hs_verify2.argtypes = [vp] * 7 + [ctypes.c_uint32] * 4 + [vp, vp]
     return L
 
 
@@ -45,4 +46,33 @@ def test_hostsim_workload(hs):
     from bdls_amd import workload
     w = workload.generate(700, 50, 256, 4, seed=11, nthreads=4)
     out = run(hs, w.arrays(), True, 16)
+    assert (out == w.reason).all()
+
+
+def run2(L, arrs, fused, min_uses):
+    pub, sig, so, sl, msg, mo, ml = arrs
+    n = len(sl)
+    out = np.zeros(n, np.uint8)
+    ncomb = ctypes.c_uint32()
+    L.hs_verify2(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data, msg.ctypes.data,
+                 mo.ctypes.data, ml.ctypes.data, n, 1 if fused else 0, 4, min_uses,
+                 out.ctypes.data, ctypes.byref(ncomb))
+    return out, ncomb.value
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_hostsim_golden_keycomb_path(hs, golden, fused):
+    """min_uses = 1 forces every record through the per-key table path."""
+    recs = [r for r in golden if (not fused) or "msg" in r]
+    out, ncomb = run2(hs, pack(recs, fused), fused, 1)
+    assert ncomb > 0
+    bad = [(r["tag"], int(o), r["reason"]) for r, o in zip(recs, out) if o != r["reason"]]
+    assert not bad
+
+
+def test_hostsim_workload_mixed_paths(hs):
+    from bdls_amd import workload
+    w = workload.generate(900, 60, 256, 4, seed=13, nthreads=4)
+    out, ncomb = run2(hs, w.arrays(), True, 4)
+    assert 0 < ncomb < w.n
     assert (out == w.reason).all()
