@@ -23,7 +23,7 @@ EXPORTS = (
     "bh_init", "bh_shutdown", "bh_device_count", "bh_last_error", "bh_version",
     "bh_workspace_bytes", "bh_verify", "bh_verify_dev", "bh_csp_verify_p256",
     "bh_parse_der_sig", "bh_dev_alloc", "bh_dev_free", "bh_memcpy_h2d", "bh_memcpy_d2h",
-    "bh_sync",
+    "bh_sync", "bh_verify_bdls", "bh_verify_bdls_dev",
 )
 
 
@@ -37,6 +37,12 @@ class BhBatch(ctypes.Structure):
         ("msg_off", ctypes.c_void_p),
         ("msg_len", ctypes.c_void_p),
     ]
+
+
+class BhBdlsBatch(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in
+                ("xy", "r", "r_off", "r_len", "s", "s_off", "s_len", "version", "msg",
+                 "msg_off", "msg_len")]
 
 
 class BhTiming(ctypes.Structure):
@@ -84,6 +90,11 @@ def lib() -> ctypes.CDLL:
         L.bh_csp_verify_p256.restype = i32
         L.bh_parse_der_sig.argtypes = [vp, sz, vp, vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         L.bh_parse_der_sig.restype = i32
+        L.bh_verify_bdls.argtypes = [i32, ctypes.POINTER(BhBdlsBatch), sz, vp, vp]
+        L.bh_verify_bdls.restype = i32
+        L.bh_verify_bdls_dev.argtypes = [i32, i32, ctypes.POINTER(BhBdlsBatch), sz, vp, vp, vp,
+                                         i32, ctypes.POINTER(BhTiming)]
+        L.bh_verify_bdls_dev.restype = i32
         L.bh_dev_alloc.argtypes = [i32, sz, ctypes.POINTER(vp)]
         L.bh_dev_alloc.restype = i32
         L.bh_dev_free.argtypes = [i32, vp]

@@ -23,6 +23,9 @@ hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s);
 hipError_t launch_verify(int curve, const BatchIn& in, const Work& w, const Plan& pl,
                          const uint32_t* gtab, uint32_t n, uint32_t chunk, uint64_t* bitmap,
                          uint8_t* reason, hipStream_t s, hipEvent_t* ev);
+hipError_t launch_verify_bdls(int curve, const BdlsIn& in, const Work& w, const Plan& pl,
+                              const uint32_t* gtab, uint32_t n, uint32_t chunk, uint64_t* bitmap,
+                              uint8_t* reason, hipStream_t s, hipEvent_t* ev);
 }  // namespace bh
 
 namespace {
@@ -185,9 +188,31 @@ uint32_t inv_chunk(size_t n) {
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(16, c));
 }
 
+// Record-range views of the two input kinds (for kMaxChunk passes).
+bh::BatchIn slice(const bh_batch* b, size_t base, uint32_t flags) {
+  return bh::BatchIn{b->pub + base * 64, b->sig, b->sig_off + base, b->sig_len + base,
+                     b->msg, b->msg_off + base, b->msg_len + base, flags};
+}
+bh::BdlsIn slice(const bh_bdls_batch* b, size_t base, uint32_t flags) {
+  return bh::BdlsIn{b->xy + base * 64, b->r, b->r_off + base, b->r_len + base,
+                    b->s, b->s_off + base, b->s_len + base, b->version + base,
+                    b->msg, b->msg_off + base, b->msg_len + base, flags};
+}
+hipError_t launch(int curve, const bh::BatchIn& in, const bh::Work& w, const bh::Plan& pl,
+                  const uint32_t* gtab, uint32_t n, uint32_t chunk, uint64_t* bm, uint8_t* rs,
+                  hipStream_t s, hipEvent_t* ev) {
+  return bh::launch_verify(curve, in, w, pl, gtab, n, chunk, bm, rs, s, ev);
+}
+hipError_t launch(int curve, const bh::BdlsIn& in, const bh::Work& w, const bh::Plan& pl,
+                  const uint32_t* gtab, uint32_t n, uint32_t chunk, uint64_t* bm, uint8_t* rs,
+                  hipStream_t s, hipEvent_t* ev) {
+  return bh::launch_verify_bdls(curve, in, w, pl, gtab, n, chunk, bm, rs, s, ev);
+}
+
 // Core device-resident pass (caller holds d.mu and has set the device).
 // With t != nullptr, events bracket every stage and the call synchronises.
-int run_dev(Dev& d, int curve, const bh_batch* b, size_t n, uint32_t flags, uint64_t* bitmap,
+template <class B>
+int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* bitmap,
             uint8_t* reason, hipStream_t s, bh_timing* t) {
   if (t) *t = bh_timing{};
   for (size_t base = 0; base < n; base += kMaxChunk) {
@@ -196,10 +221,8 @@ int run_dev(Dev& d, int curve, const bh_batch* b, size_t n, uint32_t flags, uint
     bh::Plan pl;
     int rc = carve_work(d, m, &w, &pl);
     if (rc) return rc;
-    bh::BatchIn in{b->pub + base * 64, b->sig, b->sig_off + base, b->sig_len + base,
-                   b->msg, b->msg_off + base, b->msg_len + base, flags};
-    HIPCHK(bh::launch_verify(curve, in, w, pl, d.gtab[curve], (uint32_t)m, inv_chunk(m),
-                             bitmap + base / 64, reason + base, s, t ? d.ev : nullptr));
+    HIPCHK(launch(curve, slice(b, base, flags), w, pl, d.gtab[curve], (uint32_t)m, inv_chunk(m),
+                  bitmap + base / 64, reason + base, s, t ? d.ev : nullptr));
     if (t) {
       HIPCHK(hipEventSynchronize(d.ev[6]));
       float ms[6];
@@ -459,6 +482,111 @@ int bh_sync(int device) {
   HIPCHK(hipSetDevice(d->id));
   HIPCHK(hipStreamSynchronize(d->stream));
   return BH_OK;
+}
+
+// ---- BDLS consensus messages (SignedProto.Verify) --------------------------
+int bh_verify_bdls_dev(int device, int curve, const bh_bdls_batch* b, size_t n,
+                       uint64_t* bitmap_words, uint8_t* reason, void* stream, int sync,
+                       bh_timing* timing) {
+  if (!b || (n && (!b->xy || !b->r || !b->r_off || !b->r_len || !b->s || !b->s_off ||
+                   !b->s_len || !b->version || !b->msg || !b->msg_off || !b->msg_len ||
+                   !bitmap_words || !reason)))
+    return fail(BH_E_INVALID, "null pointer in batch");
+  if (curve != BH_CURVE_P256 && curve != BH_CURVE_SECP256K1)
+    return fail(BH_E_INVALID, "unknown curve");
+  if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
+  Dev* d = get_dev(device);
+  if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
+  std::lock_guard<std::mutex> g(d->mu);
+  HIPCHK(hipSetDevice(d->id));
+  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  if (n == 0) return BH_OK;
+  int rc = run_dev(*d, curve, b, n, 0u, bitmap_words, reason, s, timing);
+  if (rc) return rc;
+  if (sync && !timing) HIPCHK(hipStreamSynchronize(s));
+  return BH_OK;
+}
+
+int bh_verify_bdls(int curve, const bh_bdls_batch* b, size_t n, uint8_t* bitmap,
+                   uint8_t* reason) {
+  if (!b || (n && (!b->xy || !b->r_off || !b->r_len || !b->s_off || !b->s_len || !b->version ||
+                   !b->msg_off || !b->msg_len || !bitmap || !reason)))
+    return fail(BH_E_INVALID, "null pointer in batch");
+  Dev* d = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    if (!g_devs.empty()) d = g_devs[0];
+  }
+  if (!d) return fail(BH_E_NOT_INIT, "bh_init not called");
+  std::memset(bitmap, 0, (n + 7) / 8);
+  if (n == 0) return BH_OK;
+  // stage: one contiguous device buffer per host array (BDLS rounds are small)
+  auto span = [&](const uint64_t* off, const uint32_t* len, uint64_t* lo) {
+    uint64_t a = UINT64_MAX, z = 0;
+    for (size_t i = 0; i < n; i++) {
+      a = std::min<uint64_t>(a, off[i]);
+      z = std::max<uint64_t>(z, off[i] + len[i]);
+    }
+    *lo = a;
+    return z - a;
+  };
+  uint64_t rlo, slo, mlo;
+  const uint64_t rsz = span(b->r_off, b->r_len, &rlo), ssz = span(b->s_off, b->s_len, &slo),
+                 msz = span(b->msg_off, b->msg_len, &mlo);
+  std::vector<uint64_t> ro(n), so(n), mo(n);
+  for (size_t i = 0; i < n; i++) {
+    ro[i] = b->r_off[i] - rlo;
+    so[i] = b->s_off[i] - slo;
+    mo[i] = b->msg_off[i] - mlo;
+  }
+  std::vector<void*> bufs;
+  auto cleanup = [&]() {
+    for (void* p : bufs) (void)hipFree(p);
+  };
+  auto up = [&](const void* src, size_t bytes, void** dst) -> int {
+    hipError_t e = hipMalloc(dst, bytes + 16);
+    if (e != hipSuccess) return fail(BH_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    bufs.push_back(*dst);
+    if (bytes) {
+      e = hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
+      if (e != hipSuccess) return fail(BH_E_DEVICE, std::string("hipMemcpy: ") + hipGetErrorString(e));
+    }
+    return BH_OK;
+  };
+  std::lock_guard<std::mutex> g(d->mu);
+  HIPCHK(hipSetDevice(d->id));
+  void *dxy, *dr, *ds, *dm, *dro, *dso, *dmo, *drl, *dsl, *dml, *dver, *dbm, *drs;
+  int rc = 0;
+  if (!rc) rc = up(b->xy, n * 64, &dxy);
+  if (!rc) rc = up(b->r ? b->r + rlo : nullptr, b->r ? rsz : 0, &dr);
+  if (!rc) rc = up(b->s ? b->s + slo : nullptr, b->s ? ssz : 0, &ds);
+  if (!rc) rc = up(b->msg ? b->msg + mlo : nullptr, b->msg ? msz : 0, &dm);
+  if (!rc) rc = up(ro.data(), n * 8, &dro);
+  if (!rc) rc = up(so.data(), n * 8, &dso);
+  if (!rc) rc = up(mo.data(), n * 8, &dmo);
+  if (!rc) rc = up(b->r_len, n * 4, &drl);
+  if (!rc) rc = up(b->s_len, n * 4, &dsl);
+  if (!rc) rc = up(b->msg_len, n * 4, &dml);
+  if (!rc) rc = up(b->version, n * 4, &dver);
+  if (!rc) rc = up(nullptr, round64(n) / 8, &dbm);
+  if (!rc) rc = up(nullptr, n, &drs);
+  if (!rc) {
+    bh_bdls_batch db{(const uint8_t*)dxy, (const uint8_t*)dr, (const uint64_t*)dro,
+                     (const uint32_t*)drl, (const uint8_t*)ds, (const uint64_t*)dso,
+                     (const uint32_t*)dsl, (const uint32_t*)dver, (const uint8_t*)dm,
+                     (const uint64_t*)dmo, (const uint32_t*)dml};
+    rc = run_dev(*d, curve, &db, n, 0u, (uint64_t*)dbm, (uint8_t*)drs, d->stream, nullptr);
+  }
+  if (!rc) {
+    std::vector<uint64_t> words(round64(n) / 64);
+    hipError_t e = hipStreamSynchronize(d->stream);
+    if (e == hipSuccess) e = hipMemcpy(words.data(), dbm, words.size() * 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(reason, drs, n, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = fail(BH_E_DEVICE, std::string("hipMemcpy: ") + hipGetErrorString(e));
+    else std::memcpy(bitmap, words.data(), (n + 7) / 8);
+  }
+  cleanup();
+  return rc;
 }
 
 }  // extern "C"

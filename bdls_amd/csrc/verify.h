@@ -16,6 +16,7 @@
 // value, limb-major with stride `ns`), so every per-limb access by a wave is one
 // coalesced 256-byte transaction.
 #pragma once
+#include "blake2b.h"
 #include "der.h"
 #include "ec.h"
 #include "ec30.h"
@@ -36,6 +37,23 @@ struct BatchIn {  // device pointers (see include/bdls_hip.h bh_batch)
   const uint8_t* sig;
   const uint64_t* sig_off;
   const uint32_t* sig_len;
+  const uint8_t* msg;
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+  uint32_t flags;
+};
+
+// BDLS consensus messages: vendor/github.com/BDLS-bft/bdls/message.go SignedProto
+// fields (device pointers; see include/bdls_hip.h bh_bdls_batch).
+struct BdlsIn {
+  const uint8_t* xy;  // n * 64: X || Y (PubKeyAxis, 32 B each)
+  const uint8_t* r;
+  const uint64_t* r_off;
+  const uint32_t* r_len;
+  const uint8_t* s;
+  const uint64_t* s_off;
+  const uint32_t* s_len;
+  const uint32_t* version;
   const uint8_t* msg;
   const uint64_t* msg_off;
   const uint32_t* msg_len;
@@ -190,6 +208,102 @@ BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
   } else {
     // keep the arithmetic of failed lanes well defined: e = r = 1, s = 1 (Mont),
     // Q = G
+    for (int k = 0; k < 8; k++) { e[k] = r[k] = 0; }
+    e[0] = r[0] = 1;
+    load_const8(s, N::r1);
+    f_const(qx30, P::gx_m);
+    f_const(qy30, P::gy_m);
+  }
+  st8(w.e, i, w.ns, e);
+  st8(w.r, i, w.ns, r);
+  st8(w.sm, i, w.ns, s);
+  st9(w.qx, i, w.ns, qx30);
+  st9(w.qy, i, w.ns, qy30);
+  w.st[i] = st;
+}
+
+// big.Int.SetBytes on a big-endian byte string of any length: value (if it
+// fits 256 bits), *big if it does not, *zero if it is 0.
+BH_HD void setbytes_u256(const uint8_t* b, uint32_t len, uint32_t v[8], bool* big, bool* zero) {
+  uint32_t lo = 0;
+  while (lo < len && b[lo] == 0) lo++;
+  const uint32_t L = len - lo;
+  *zero = (L == 0);
+  *big = (L > 32);
+#pragma unroll
+  for (int k = 0; k < 8; k++) v[k] = 0;
+  if (L > 32) return;
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    uint32_t x = 0;
+    if ((uint32_t)j < L) x = b[len - 1 - j];
+    v[j >> 2] |= x << (8 * (j & 3));
+  }
+}
+
+// SignedProto.Verify (message.go:170-184): hash = SignedProto.Hash(), then Go
+// crypto/ecdsa.Verify(pub{curve, X, Y}, hash, R, S) with R, S from SetBytes.
+// secp256k1 takes verifyLegacy; P-256 takes verifyNISTEC. No low-S rule.
+// Off-curve / out-of-range keys are rejected (BH_R_BAD_KEY) on both curves:
+// for secp256k1 Go would compute on them, but consensus.go:456-466 admits only
+// registered participants' keys, so such inputs never reach Verify in BDLS.
+template <class P, class N, class C>
+BH_HD void stage_prep(const BdlsIn& in, const Work& w, uint32_t i) {
+  uint8_t reason = R_OK;
+  uint32_t r[8], s[8], e[8], qx[8], qy[8], nn[8], pp[8];
+  uint32_t qx30[9], qy30[9];
+  load_const8(nn, C::n);
+  load_const8(pp, C::p);
+  bool rbig, rzero, sbig, szero;
+  setbytes_u256(in.r + in.r_off[i], in.r_len[i], r, &rbig, &rzero);
+  setbytes_u256(in.s + in.s_off[i], in.s_len[i], s, &sbig, &szero);
+  if (rzero) reason = R_R_NONPOS;       // ecdsa.Verify: r.Sign() <= 0
+  else if (szero) reason = R_S_NONPOS;
+  const uint8_t* q = in.xy + (size_t)i * 64;
+  be32_to_limbs(qx, q);
+  be32_to_limbs(qy, q + 32);
+  if (reason == R_OK) {
+    if (geq8(qx, pp) || geq8(qy, pp)) {
+      reason = R_BAD_KEY;
+    } else {
+      f_from_u256(qx30, qx);
+      f_from_u256(qy30, qy);
+      f_to_mont<P>(qx30, qx30);
+      f_to_mont<P>(qy30, qy30);
+      f_canon<P>(qx30, qx30);
+      f_canon<P>(qy30, qy30);
+      if (!j_on_curve<P>(qx30, qy30)) reason = R_BAD_KEY;
+    }
+  }
+  if (reason == R_OK && (rbig || geq8(r, nn))) reason = R_R_RANGE;
+  if (reason == R_OK && (sbig || geq8(s, nn))) reason = R_S_RANGE;
+  if (reason == R_OK) {
+    uint8_t hsh[32];
+    bdls_signed_proto_hash(hsh, in.version[i], q, q + 32, in.msg + in.msg_off[i], in.msg_len[i]);
+    be32_to_limbs(e, hsh);  // hashToInt / hashToNat: 32 bytes, then mod n
+    uint32_t t[8];
+    if (!sub8(t, e, nn)) copy8(e, t);
+  }
+  uint8_t st = reason;
+  if (reason == R_OK) {
+    uint32_t pmn[8], rn[8], rm[9], r2m[9];
+    load_const8(pmn, C::p_minus_n);
+    f_from_u256(rm, r);
+    f_to_mont<P>(rm, rm);
+    f_canon<P>(rm, rm);
+    if (!geq8(r, pmn)) {
+      st |= ST_R2OK;
+      add8(rn, r, nn);
+      f_from_u256(r2m, rn);
+      f_to_mont<P>(r2m, r2m);
+      f_canon<P>(r2m, r2m);
+    } else {
+      f_copy(r2m, rm);
+    }
+    st9(w.rm, i, w.ns, rm);
+    st9(w.r2m, i, w.ns, r2m);
+    to_mont<N>(s, s);
+  } else {
     for (int k = 0; k < 8; k++) { e[k] = r[k] = 0; }
     e[0] = r[0] = 1;
     load_const8(s, N::r1);
@@ -525,6 +639,9 @@ constexpr int kKWin = 65;
 constexpr int kKEnt = 8;
 constexpr uint32_t kKTabWords = (uint32_t)kKWin * kKEnt * kQPt;
 constexpr uint32_t kMinUses = 4;
+// Below this batch size the step is latency-bound (one table build is a
+// serial 1.07M-instruction lane, more than one ladder), so key tables are off.
+constexpr uint32_t kKeyTableMinBatch = 8192;
 
 BH_HD void ktab_store(uint32_t* tab, uint32_t win, uint32_t j, const J30& P) {
   uint32_t v[28];

@@ -17,8 +17,8 @@ using namespace bh;
 
 namespace {
 
-template <class P, class N, class C>
-__global__ __launch_bounds__(256) void k_prep(BatchIn in, Work w, uint32_t n) {
+template <class P, class N, class C, class IN>
+__global__ __launch_bounds__(256) void k_prep(IN in, Work w, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   stage_prep<P, N, C>(in, w, i);
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void k_key_count(Work w, Plan pl, uint32_t n) 
 
 __global__ __launch_bounds__(256) void k_key_plan(Plan pl, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || n < kKeyTableMinBatch) return;
   const uint32_t p = pl.rec_slot[i];
   if (p == kNone || pl.slot_rep[p] != i || pl.slot_cnt[p] < kMinUses) return;
   const uint32_t t = atomicAdd(&pl.counters[2], 1u);
@@ -171,8 +171,8 @@ hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s) {
 
 // Full launch sequence. ev (optional, 6 events) brackets: prep | inv | plan
 // (dedup + split) | key tables | key comb | ladder+bitmap.
-template <class P, class N, class C>
-static hipError_t seq(const BatchIn& in, const Work& w, const Plan& pl, const uint32_t* gtab,
+template <class P, class N, class C, class IN>
+static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const uint32_t* gtab,
                       uint32_t n, uint32_t chunk, uint64_t* bitmap, uint8_t* reason, hipStream_t s,
                       hipEvent_t* ev) {
   const dim3 blk(256);
@@ -190,7 +190,7 @@ static hipError_t seq(const BatchIn& in, const Work& w, const Plan& pl, const ui
   if ((e = hipMemsetAsync(pl.slot_tab, 0xff, (size_t)pl.hc * 4, s))) return e;
   if ((e = hipMemsetAsync(pl.counters, 0, 16, s))) return e;
   REC(0);
-  hipLaunchKernelGGL((k_prep<P, N, C>), grd, blk, 0, s, in, w, n);
+  hipLaunchKernelGGL((k_prep<P, N, C, IN>), grd, blk, 0, s, in, w, n);
   REC(1);
   hipLaunchKernelGGL((k_inv<N>), grc, blk, 0, s, w, n, chunk);
   REC(2);
@@ -214,6 +214,15 @@ static hipError_t seq(const BatchIn& in, const Work& w, const Plan& pl, const ui
 hipError_t launch_verify(int curve, const BatchIn& in, const Work& w, const Plan& pl,
                          const uint32_t* gtab, uint32_t n, uint32_t chunk, uint64_t* bitmap,
                          uint8_t* reason, hipStream_t s, hipEvent_t* ev) {
+  // Fabric / BCCSP records: P-256 only (the low-S table of bccsp/utils covers
+  // the NIST curves; secp256k1 never reaches bccsp/sw).
+  if (curve != 0) return hipErrorInvalidValue;
+  return seq<F30_p256, Fn_p256, Cv_p256>(in, w, pl, gtab, n, chunk, bitmap, reason, s, ev);
+}
+
+hipError_t launch_verify_bdls(int curve, const BdlsIn& in, const Work& w, const Plan& pl,
+                              const uint32_t* gtab, uint32_t n, uint32_t chunk, uint64_t* bitmap,
+                              uint8_t* reason, hipStream_t s, hipEvent_t* ev) {
   if (curve == 0)
     return seq<F30_p256, Fn_p256, Cv_p256>(in, w, pl, gtab, n, chunk, bitmap, reason, s, ev);
   return seq<F30_k1, Fn_k1, Cv_k1>(in, w, pl, gtab, n, chunk, bitmap, reason, s, ev);

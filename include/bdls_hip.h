@@ -99,7 +99,8 @@ size_t bh_workspace_bytes(size_t n);
 
 /* Host-memory batch: copies to the devices, shards [0,n) over all initialised
  * devices (contiguous ranges, no collective), gathers bitmap and reasons.
- * curve: BH_CURVE_P256 (secp256k1: see bh_verify_secp256k1_bdls). */
+ * curve: BH_CURVE_P256 (the Fabric/BCCSP path; secp256k1 BDLS messages use
+ * bh_verify_bdls). */
 int bh_verify(int curve, const bh_batch *b, size_t n, uint32_t flags, uint8_t *bitmap,
               uint8_t *reason);
 
@@ -124,6 +125,40 @@ int bh_csp_verify_p256(const uint8_t pub[64], const uint8_t *sig, size_t sig_len
  * bits. Pure host code, no device needed. */
 int bh_parse_der_sig(const uint8_t *der, size_t len, uint8_t r[32], uint8_t s[32], int *r_big,
                      int *s_big);
+
+/* ---- BDLS consensus messages -------------------------------------------
+ * One record = one vendor/github.com/BDLS-bft/bdls/message.go SignedProto.
+ * Verification restates SignedProto.Verify (message.go:170-184): hash =
+ * SignedProto.Hash() (BLAKE2b-256 over "BDLS_CONSENSUS_SIGNATURE" || Version
+ * u32-LE || X || Y || len(Message) u32-LE || Message, message.go:97-138), then
+ * Go crypto/ecdsa.Verify with R, S = big.Int.SetBytes(R), SetBytes(S).
+ * curve BH_CURVE_SECP256K1: as wired in orderer/consensus/bdls/chain.go:60-61
+ * (Go verifyLegacy); BH_CURVE_P256: the curve-generic BDLS library with P-256
+ * keys (verifyNISTEC). No low-S rule. Result reasons: BH_R_OK or a reject
+ * code (every reject is Verify() == false). Off-curve keys are rejected with
+ * BH_R_BAD_KEY on both curves (BDLS only admits registered participants'
+ * keys, consensus.go:456-466). */
+typedef struct bh_bdls_batch {
+  const uint8_t *xy;       /* n * 64: SignedProto.X || SignedProto.Y (32 B each)    */
+  const uint8_t *r;        /* concatenated SignedProto.R (big-endian, any length)   */
+  const uint64_t *r_off;
+  const uint32_t *r_len;
+  const uint8_t *s;        /* concatenated SignedProto.S                            */
+  const uint64_t *s_off;
+  const uint32_t *s_len;
+  const uint32_t *version; /* SignedProto.Version                                   */
+  const uint8_t *msg;      /* concatenated SignedProto.Message                      */
+  const uint64_t *msg_off;
+  const uint32_t *msg_len;
+} bh_bdls_batch;
+
+/* Host buffers, first initialised device (BDLS rounds are hundreds of records). */
+int bh_verify_bdls(int curve, const bh_bdls_batch *b, size_t n, uint8_t *bitmap,
+                   uint8_t *reason);
+/* Device-resident; semantics of bh_verify_dev. */
+int bh_verify_bdls_dev(int device, int curve, const bh_bdls_batch *b, size_t n,
+                       uint64_t *bitmap_words, uint8_t *reason, void *stream, int sync,
+                       bh_timing *timing);
 
 /* ---- device buffers on an initialised device (callers that keep batches
  * resident in HBM, e.g. bench.py; the library owns the HIP runtime so callers

@@ -11,22 +11,27 @@
 
 using namespace bh;
 
-static std::vector<uint32_t> g_gtab;
+static std::vector<uint32_t> g_gtab, g_gtab_k1;
 
-static void build_gtab() {
-  g_gtab.assign((size_t)kCombWindows * kCombEntries * kGEntry, 0);
-  for (uint32_t t = 0; t < (uint32_t)(kCombWindows * kCombEntries); t++)
-    gtab_entry<F30_p256>(t, g_gtab.data() + (size_t)t * kGEntry);
+template <class P>
+static const uint32_t* gtab_for() {
+  std::vector<uint32_t>& g = P::sparse_p256 ? g_gtab : g_gtab_k1;
+  if (g.empty()) {
+    g.assign((size_t)kCombWindows * kCombEntries * kGEntry, 0);
+    for (uint32_t t = 0; t < (uint32_t)(kCombWindows * kCombEntries); t++)
+      gtab_entry<P>(t, g.data() + (size_t)t * kGEntry);
+  }
+  return g.data();
 }
 
 // Sequential restatement of the device launch sequence (verify_kernels.hip
 // seq()): prep, inv, key dedup / plan / split, key tables, both verify paths.
-// min_uses overrides kMinUses so tests can force either path.
-extern "C" int hs_verify2(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
-                          const uint32_t* slen, const uint8_t* msg, const uint64_t* moff,
-                          const uint32_t* mlen, uint32_t n, uint32_t flags, uint32_t chunk,
-                          uint32_t min_uses, uint8_t* reason, uint32_t* n_comb) {
-  if (g_gtab.empty()) build_gtab();
+// min_uses overrides kMinUses (and the batch-size gate) so tests can force
+// either path.
+template <class P, class N, class C, class IN>
+static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, uint8_t* reason,
+                   uint32_t* n_comb) {
+  const uint32_t* gtab = gtab_for<P>();
   const uint32_t ns = (n + 63) & ~63u;
   std::vector<uint32_t> buf((size_t)9 * 9 * ns + (size_t)(ns / 64) * 64 * kQTab * kQPt);
   std::vector<uint8_t> st(ns);
@@ -44,10 +49,8 @@ extern "C" int hs_verify2(const uint8_t* pub, const uint8_t* sig, const uint64_t
   p += 9 * ns;
   w.qtab = p;
   w.st = st.data();
-  BatchIn in{pub, sig, soff, slen, msg, moff, mlen, flags};
-  for (uint32_t i = 0; i < n; i++) stage_prep<F30_p256, Fn_p256, Cv_p256>(in, w, i);
-  for (uint32_t lo = 0; lo < n; lo += chunk)
-    stage_inv<Fn_p256>(w, lo, lo + chunk < n ? lo + chunk : n);
+  for (uint32_t i = 0; i < n; i++) stage_prep<P, N, C>(in, w, i);
+  for (uint32_t lo = 0; lo < n; lo += chunk) stage_inv<N>(w, lo, lo + chunk < n ? lo + chunk : n);
   // dedup: representative = first record with an equal key
   std::vector<uint32_t> rep(n, kNone), cnt(n, 0);
   std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;
@@ -56,7 +59,10 @@ extern "C" int hs_verify2(const uint8_t* pub, const uint8_t* sig, const uint64_t
     auto& v = by_hash[key_hash(w, i)];
     uint32_t r = kNone;
     if (!v.empty() && same_key(w, i, v[0])) r = v[0];
-    if (v.empty()) { v.push_back(i); r = i; }
+    if (v.empty()) {
+      v.push_back(i);
+      r = i;
+    }
     rep[i] = r;
     if (r != kNone) cnt[r]++;
   }
@@ -74,17 +80,46 @@ extern "C" int hs_verify2(const uint8_t* pub, const uint8_t* sig, const uint64_t
       if (tab_of[r] == kNone) {
         tab_of[r] = (uint32_t)tables.size();
         tables.emplace_back(kKTabWords);
-        ktab_build<F30_p256>(tables.back().data(), w, r);
+        ktab_build<P>(tables.back().data(), w, r);
       }
-      ok = stage_keycomb<F30_p256>(w, g_gtab.data(), i, tables[tab_of[r]].data());
+      ok = stage_keycomb<P>(w, gtab, i, tables[tab_of[r]].data());
       combs++;
     } else {
-      ok = stage_ladder<F30_p256>(w, g_gtab.data(), i, i / 64, i % 64);
+      ok = stage_ladder<P>(w, gtab, i, i / 64, i % 64);
     }
     reason[i] = ok ? R_OK : R_MATH;
   }
   if (n_comb) *n_comb = combs;
   return 0;
+}
+
+extern "C" int hs_verify2(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
+                          const uint32_t* slen, const uint8_t* msg, const uint64_t* moff,
+                          const uint32_t* mlen, uint32_t n, uint32_t flags, uint32_t chunk,
+                          uint32_t min_uses, uint8_t* reason, uint32_t* n_comb) {
+  BatchIn in{pub, sig, soff, slen, msg, moff, mlen, flags};
+  return run_seq<F30_p256, Fn_p256, Cv_p256>(in, n, chunk, min_uses, reason, n_comb);
+}
+
+// secp256k1 with the Fabric record layout but BHF_NO_LOW_S and a caller-chosen
+// digest: reaches the curve-level edge cases (x wrap, infinity, u1 G == u2 Q)
+// that BLAKE2b-hashed BDLS messages cannot be steered into.
+extern "C" int hs_verify_k1_digest(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
+                                   const uint32_t* slen, const uint8_t* dg, const uint64_t* doff,
+                                   const uint32_t* dlen, uint32_t n, uint32_t min_uses,
+                                   uint8_t* reason) {
+  BatchIn in{pub, sig, soff, slen, dg, doff, dlen, BHF_NO_LOW_S};
+  return run_seq<F30_k1, Fn_k1, Cv_k1>(in, n, 4, min_uses, reason, nullptr);
+}
+
+extern "C" int hs_verify_bdls(int curve, const uint8_t* xy, const uint8_t* r, const uint64_t* roff,
+                              const uint32_t* rlen, const uint8_t* s, const uint64_t* soff,
+                              const uint32_t* slen, const uint32_t* ver, const uint8_t* msg,
+                              const uint64_t* moff, const uint32_t* mlen, uint32_t n,
+                              uint32_t min_uses, uint8_t* reason) {
+  BdlsIn in{xy, r, roff, rlen, s, soff, slen, ver, msg, moff, mlen, 0};
+  if (curve == 0) return run_seq<F30_p256, Fn_p256, Cv_p256>(in, n, 4, min_uses, reason, nullptr);
+  return run_seq<F30_k1, Fn_k1, Cv_k1>(in, n, 4, min_uses, reason, nullptr);
 }
 
 extern "C" int hs_verify(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
@@ -108,3 +143,7 @@ extern "C" void hs_f_sub64(const uint32_t* a, const uint32_t* b, uint32_t* r) {
 extern "C" void hs_f_add(const uint32_t* a, const uint32_t* b, uint32_t* r) { f_add(r, a, b); }
 extern "C" void hs_f_reduce(const uint32_t* a, uint32_t* r) { f_reduce<F30_p256>(r, a); }
 extern "C" void hs_f_sqr(const uint32_t* a, uint32_t* r) { f_sqr<F30_p256>(r, a); }
+extern "C" void hs_bdls_hash(uint32_t version, const uint8_t* x32, const uint8_t* y32,
+                             const uint8_t* msg, uint32_t mlen, uint8_t* out) {
+  bdls_signed_proto_hash(out, version, x32, y32, msg, mlen);
+}
