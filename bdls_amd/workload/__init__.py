@@ -63,3 +63,90 @@ def generate(n: int, nkeys: int, msg_len: int = 256, corrupt_den: int = 16, seed
     if rc != 0:
         raise RuntimeError(f"gen_p256 failed: {rc}")
     return w
+
+
+@dataclass
+class BdlsRound:
+    """One BDLS height/round of SignedProto records (BASELINE config 4)."""
+    curve: int           # 0 P-256, 1 secp256k1 (bh_curve)
+    xy: np.ndarray       # n*64 u8
+    r: np.ndarray
+    r_off: np.ndarray
+    r_len: np.ndarray
+    s: np.ndarray
+    s_off: np.ndarray
+    s_len: np.ndarray
+    version: np.ndarray  # u32
+    msg: np.ndarray
+    msg_off: np.ndarray
+    msg_len: np.ndarray
+
+    @property
+    def n(self) -> int:
+        return len(self.version)
+
+    def arrays(self):
+        return (self.xy, self.r, self.r_off, self.r_len, self.s, self.s_off, self.s_len,
+                self.version, self.msg, self.msg_off, self.msg_len)
+
+
+def generate_bdls_round(nval: int = 100, curve: int = 1, small_len: int = 200,
+                        seed: int = 4) -> BdlsRound:
+    """nval roundchange + lock (+2t+1 proofs) + nval commit + decide (+2t+1
+    proofs), t = (nval-1)//3, all valid, signed by the validators' keys."""
+    if not os.path.exists(_LIB):
+        raise RuntimeError(f"{_LIB} not built (run `make`)")
+    L = ctypes.CDLL(_LIB)
+    vp = ctypes.c_void_p
+    L.gen_bdls_round.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_uint64, ctypes.c_int] + [vp] * 9 + [
+                                     ctypes.c_uint64, vp, vp]
+    L.gen_bdls_round.restype = ctypes.c_int
+    t = (nval - 1) // 3
+    t2p1 = 2 * t + 1
+    cap = 2 * nval + 2 * (1 + t2p1)
+    msg_cap = 2 * nval * small_len + 2 * t2p1 * (small_len + 200) * 2 + 64
+    b = BdlsRound(curve=curve, xy=np.zeros(cap * 64, np.uint8), r=np.zeros(cap * 33, np.uint8),
+                  r_off=np.zeros(cap, np.uint64), r_len=np.zeros(cap, np.uint32),
+                  s=np.zeros(cap * 33, np.uint8), s_off=np.zeros(cap, np.uint64),
+                  s_len=np.zeros(cap, np.uint32), version=np.zeros(cap, np.uint32),
+                  msg=np.zeros(msg_cap, np.uint8), msg_off=np.zeros(cap, np.uint64),
+                  msg_len=np.zeros(cap, np.uint32))
+    rc = L.gen_bdls_round(curve, nval, t2p1, small_len, seed, cap, b.xy.ctypes.data,
+                          b.r.ctypes.data, b.r_off.ctypes.data, b.r_len.ctypes.data,
+                          b.s.ctypes.data, b.s_off.ctypes.data, b.s_len.ctypes.data,
+                          b.version.ctypes.data, b.msg.ctypes.data, msg_cap,
+                          b.msg_off.ctypes.data, b.msg_len.ctypes.data)
+    if rc != cap:
+        raise RuntimeError(f"gen_bdls_round failed: {rc}")
+    return b
+
+
+def concat(parts: list[Workload]) -> Workload:
+    """One batch from several (offsets rebased)."""
+    msg_base = np.cumsum([0] + [len(p.msg) for p in parts[:-1]]).astype(np.uint64)
+    sig_base = np.cumsum([0] + [len(p.sig) for p in parts[:-1]]).astype(np.uint64)
+    return Workload(
+        pub=np.concatenate([p.pub for p in parts]), msg=np.concatenate([p.msg for p in parts]),
+        msg_off=np.concatenate([p.msg_off + b for p, b in zip(parts, msg_base)]),
+        msg_len=np.concatenate([p.msg_len for p in parts]),
+        sig=np.concatenate([p.sig for p in parts]),
+        sig_off=np.concatenate([p.sig_off + b for p, b in zip(parts, sig_base)]),
+        sig_len=np.concatenate([p.sig_len for p in parts]),
+        reason=np.concatenate([p.reason for p in parts]),
+        cls=np.concatenate([p.cls for p in parts]))
+
+
+def generate_block(ntx: int = 500, endorsements: int = 3, norgs: int = 4, nclients: int = 50,
+                   creator_len: int = 4096, endorse_len: int = 1536, corrupt_den: int = 100,
+                   seed: int = 3) -> Workload:
+    """BASELINE config 3: one block's signatures as txvalidator checks them --
+    per tx a creator signature over the ~4 KB envelope payload
+    (core/common/validation/msgvalidation.go:245-256 checkSignatureFromCreator)
+    and `endorsements` endorser signatures over proposal-response-payload ||
+    endorser (core/common/validation/... via policy evaluation,
+    common/policies/policy.go:363-395). Endorsers are the norgs peers, creators
+    nclients client identities; 1/corrupt_den of the records corrupted."""
+    creators = generate(ntx, nclients, creator_len, corrupt_den, seed=seed * 7 + 1)
+    endorse = generate(ntx * endorsements, norgs, endorse_len, corrupt_den, seed=seed * 7 + 2)
+    return concat([creators, endorse])

@@ -240,3 +240,221 @@ int gen_p256(size_t n, int nkeys, int msg_len, int corrupt_den, uint64_t seed, i
   free(kpriv);
   return 0;
 }
+
+/* ---------------------------------------------------------------------------
+ * BDLS round (BASELINE config 4): one height/round at `nval` validators as
+ * consensus.go drives it: nval <roundchange>, one <lock> from the leader whose
+ * message embeds t2p1 = 2t+1 roundchange proofs, those t2p1 proof SignedProtos
+ * (re-verified by verifyLockMessage, consensus.go:549-584), nval <commit>, one
+ * <decide> embedding t2p1 commit proofs and those proofs again
+ * (verifyDecideMessage, :852-885). Records are SignedProto (message.go):
+ * X, Y (32 B), R, S (big.Int.Bytes()), Version = 1, Message; hash =
+ * BLAKE2b-256(prefix || ver || X || Y || len || msg) (:97-138).
+ * ------------------------------------------------------------------------- */
+static const uint64_t B2IV[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull,
+                                 0x3c6ef372fe94f82bull, 0xa54ff53a5f1d36f1ull,
+                                 0x510e527fade682d1ull, 0x9b05688c2b3e6c1full,
+                                 0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
+static const uint8_t B2S[12][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11}, {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+#define ROTR64(x, n) (((x) >> (n)) | ((x) << (64 - (n))))
+#define B2G(a, b, c, d, x, y)              \
+  do {                                     \
+    v[a] = v[a] + v[b] + (x);              \
+    v[d] = ROTR64(v[d] ^ v[a], 32);        \
+    v[c] = v[c] + v[d];                    \
+    v[b] = ROTR64(v[b] ^ v[c], 24);        \
+    v[a] = v[a] + v[b] + (y);              \
+    v[d] = ROTR64(v[d] ^ v[a], 16);        \
+    v[c] = v[c] + v[d];                    \
+    v[b] = ROTR64(v[b] ^ v[c], 63);        \
+  } while (0)
+
+static void b2_block(uint64_t h[8], const uint8_t blk[128], uint64_t t, int last) {
+  uint64_t m[16], v[16];
+  for (int i = 0; i < 16; i++) {
+    uint64_t w = 0;
+    for (int b = 7; b >= 0; b--) w = (w << 8) | blk[8 * i + b];
+    m[i] = w;
+  }
+  for (int i = 0; i < 8; i++) {
+    v[i] = h[i];
+    v[i + 8] = B2IV[i];
+  }
+  v[12] ^= t;
+  if (last) v[14] = ~v[14];
+  for (int r = 0; r < 12; r++) {
+    const uint8_t *s = B2S[r];
+    B2G(0, 4, 8, 12, m[s[0]], m[s[1]]);
+    B2G(1, 5, 9, 13, m[s[2]], m[s[3]]);
+    B2G(2, 6, 10, 14, m[s[4]], m[s[5]]);
+    B2G(3, 7, 11, 15, m[s[6]], m[s[7]]);
+    B2G(0, 5, 10, 15, m[s[8]], m[s[9]]);
+    B2G(1, 6, 11, 12, m[s[10]], m[s[11]]);
+    B2G(2, 7, 8, 13, m[s[12]], m[s[13]]);
+    B2G(3, 4, 9, 14, m[s[14]], m[s[15]]);
+  }
+  for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[i + 8];
+}
+
+/* SignedProto.Hash */
+static void bdls_hash(uint8_t out[32], uint32_t ver, const uint8_t *x, const uint8_t *y,
+                      const uint8_t *msg, uint32_t len) {
+  static const char prefix[] = "BDLS_CONSENSUS_SIGNATURE";
+  size_t total = 96 + (size_t)len;
+  uint8_t *buf = malloc(total + 128);
+  memcpy(buf, prefix, 24);
+  for (int i = 0; i < 4; i++) buf[24 + i] = (uint8_t)(ver >> (8 * i));
+  memcpy(buf + 28, x, 32);
+  memcpy(buf + 60, y, 32);
+  for (int i = 0; i < 4; i++) buf[92 + i] = (uint8_t)(len >> (8 * i));
+  memcpy(buf + 96, msg, len);
+  uint64_t h[8];
+  for (int i = 0; i < 8; i++) h[i] = B2IV[i];
+  h[0] ^= 0x01010000ull ^ 32ull;
+  size_t pos = 0;
+  for (;;) {
+    uint8_t blk[128] = {0};
+    int last = total - pos <= 128;
+    size_t take = last ? total - pos : 128;
+    memcpy(blk, buf + pos, take);
+    b2_block(h, blk, last ? total : pos + 128, last);
+    if (last) break;
+    pos += 128;
+  }
+  for (int i = 0; i < 32; i++) out[i] = (uint8_t)(h[i >> 3] >> (8 * (i & 7)));
+  free(buf);
+}
+
+typedef struct {
+  uint8_t x[32], y[32], r[33], s[33];
+  uint32_t rl, sl, ver, ml;
+  uint8_t *msg;
+} sproto;
+
+static void sp_sign(sproto *o, EC_GROUP *g, BN_CTX *ctx, const BIGNUM *d, const uint8_t *x,
+                    const uint8_t *y, const uint8_t *msg, uint32_t ml, uint64_t *st) {
+  BIGNUM *n = BN_new(), *k = BN_new(), *kinv = BN_new(), *r = BN_new(), *s = BN_new(),
+         *e = BN_new(), *t = BN_new(), *xr = BN_new();
+  EC_POINT *R = EC_POINT_new(g);
+  EC_GROUP_get_order(g, n, ctx);
+  memcpy(o->x, x, 32);
+  memcpy(o->y, y, 32);
+  o->ver = 1;
+  o->ml = ml;
+  o->msg = malloc(ml ? ml : 1);
+  memcpy(o->msg, msg, ml);
+  uint8_t dg[32];
+  bdls_hash(dg, 1, x, y, msg, ml);
+  BN_bin2bn(dg, 32, e);
+  BN_nnmod(e, e, n, ctx);
+  do {
+    rand_scalar(st, k, n, ctx);
+    EC_POINT_mul(g, R, k, NULL, NULL, ctx);
+    EC_POINT_get_affine_coordinates(g, R, xr, NULL, ctx);
+    BN_nnmod(r, xr, n, ctx);
+    BN_mod_inverse(kinv, k, n, ctx);
+    BN_mod_mul(t, r, d, n, ctx);
+    BN_mod_add(t, t, e, n, ctx);
+    BN_mod_mul(s, kinv, t, n, ctx);
+  } while (BN_is_zero(r) || BN_is_zero(s));
+  o->rl = (uint32_t)BN_bn2bin(r, o->r);
+  o->sl = (uint32_t)BN_bn2bin(s, o->s);
+  EC_POINT_free(R);
+  BIGNUM *v[] = {n, k, kinv, r, s, e, t, xr};
+  for (int i = 0; i < 8; i++) BN_free(v[i]);
+}
+
+/* Writes up to cap records; returns the record count (2 nval + 2 (1 + t2p1)).
+ * Buffers: xy cap*64, r/s cap*33 (+off/len), ver cap, msg msg_cap bytes. */
+int gen_bdls_round(int curve, int nval, int t2p1, int small_len, uint64_t seed, int cap,
+                   uint8_t *xy, uint8_t *rbuf, uint64_t *roff, uint32_t *rlen, uint8_t *sbuf,
+                   uint64_t *soff, uint32_t *slen, uint32_t *ver, uint8_t *msg, uint64_t msg_cap,
+                   uint64_t *moff, uint32_t *mlen) {
+  const int total = 2 * nval + 2 * (1 + t2p1);
+  if (total > cap || t2p1 > nval || nval < 1) return -1;
+  EC_GROUP *g = EC_GROUP_new_by_curve_name(curve == 0 ? NID_X9_62_prime256v1 : NID_secp256k1);
+  BN_CTX *ctx = BN_CTX_new();
+  BIGNUM *n = BN_new(), *px = BN_new(), *py = BN_new();
+  EC_GROUP_get_order(g, n, ctx);
+  EC_POINT *Q = EC_POINT_new(g);
+  BIGNUM **d = malloc(sizeof(BIGNUM *) * nval);
+  uint8_t(*kx)[32] = malloc(32 * (size_t)nval), (*ky)[32] = malloc(32 * (size_t)nval);
+  uint64_t st = seed * 0x9e3779b97f4a7c15ull + 0xbd15ull;
+  for (int v = 0; v < nval; v++) {
+    d[v] = BN_new();
+    rand_scalar(&st, d[v], n, ctx);
+    EC_POINT_mul(g, Q, d[v], NULL, NULL, ctx);
+    EC_POINT_get_affine_coordinates(g, Q, px, py, ctx);
+    BN_bn2binpad(px, kx[v], 32);
+    BN_bn2binpad(py, ky[v], 32);
+  }
+  sproto *rec = calloc((size_t)total, sizeof(sproto));
+  uint8_t *tmp = malloc((size_t)small_len + 64);
+  int k = 0;
+  /* phase 0: roundchange, phase 1: commit */
+  for (int ph = 0; ph < 2; ph++) {
+    int first = k;
+    for (int v = 0; v < nval; v++) {
+      rand_bytes(&st, tmp, (size_t)small_len);
+      tmp[0] = (uint8_t)(ph ? 0x3a : 0x2a); /* message type tag */
+      sp_sign(&rec[k++], g, ctx, d[v], kx[v], ky[v], tmp, (uint32_t)small_len, &st);
+    }
+    /* <lock> / <decide> by the leader, embedding t2p1 proofs */
+    size_t agg_len = 0;
+    for (int p = 0; p < t2p1; p++) agg_len += 64 + rec[first + p].rl + rec[first + p].sl + rec[first + p].ml + 8;
+    uint8_t *agg = malloc(agg_len + 16), *a = agg;
+    for (int p = 0; p < t2p1; p++) {
+      sproto *q = &rec[first + p];
+      memcpy(a, q->x, 32); a += 32;
+      memcpy(a, q->y, 32); a += 32;
+      memcpy(a, q->r, q->rl); a += q->rl;
+      memcpy(a, q->s, q->sl); a += q->sl;
+      memcpy(a, q->msg, q->ml); a += q->ml;
+      for (int b = 0; b < 8; b++) *a++ = (uint8_t)p;
+    }
+    sp_sign(&rec[k++], g, ctx, d[0], kx[0], ky[0], agg, (uint32_t)agg_len, &st);
+    free(agg);
+    for (int p = 0; p < t2p1; p++) { /* proofs re-verified as their own records */
+      sproto *q = &rec[k++];
+      *q = rec[first + p];
+      q->msg = malloc(q->ml ? q->ml : 1);
+      memcpy(q->msg, rec[first + p].msg, q->ml);
+    }
+  }
+  uint64_t mo = 0;
+  int rc = total;
+  for (int i = 0; i < total; i++) {
+    memcpy(xy + 64 * (size_t)i, rec[i].x, 32);
+    memcpy(xy + 64 * (size_t)i + 32, rec[i].y, 32);
+    memcpy(rbuf + 33 * (size_t)i, rec[i].r, rec[i].rl);
+    memcpy(sbuf + 33 * (size_t)i, rec[i].s, rec[i].sl);
+    roff[i] = 33 * (uint64_t)i;
+    soff[i] = 33 * (uint64_t)i;
+    rlen[i] = rec[i].rl;
+    slen[i] = rec[i].sl;
+    ver[i] = rec[i].ver;
+    if (mo + rec[i].ml > msg_cap) rc = -2;
+    else memcpy(msg + mo, rec[i].msg, rec[i].ml);
+    moff[i] = mo;
+    mlen[i] = rec[i].ml;
+    mo += rec[i].ml;
+    free(rec[i].msg);
+  }
+  free(rec);
+  free(tmp);
+  for (int v = 0; v < nval; v++) BN_free(d[v]);
+  free(d);
+  free(kx);
+  free(ky);
+  EC_POINT_free(Q);
+  BN_free(n); BN_free(px); BN_free(py);
+  BN_CTX_free(ctx);
+  EC_GROUP_free(g);
+  return rc;
+}

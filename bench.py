@@ -47,7 +47,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=1 << 20, help="records per GPU")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 5])
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
+                    help="2/5: throughput; 3 (block) / 4 (BDLS round): latency")
+    ap.add_argument("--curve", type=int, default=1, help="config 4: 1 secp256k1 (as wired), 0 P-256")
+    ap.add_argument("--validators", type=int, default=100, help="config 4")
     ap.add_argument("--nkeys", type=int, default=65536)
     ap.add_argument("--msg-len", type=int, default=256)
     ap.add_argument("--corrupt-den", type=int, default=16)
@@ -71,11 +74,140 @@ def mac_peak_default() -> tuple[float, str]:
     return 256 * 4 * 32 * 2.4e9 / 4, "assumed quarter-rate v_mad_u64_u32"
 
 
+def percentile(v, q):
+    return float(np.percentile(np.asarray(v), q))
+
+
+def bench_latency(a, rank, world, local):
+    """Configs 3 and 4: latency of one batch through the host C ABI (H2D +
+    verify + D2H, what a Go caller sees) and device-resident, p50/p99 over
+    --steps calls. N GPUs run N independent replicas (the path does not shard
+    at this size)."""
+    from bdls_amd import _lib, dist, workload
+    L = _lib.lib()
+    _lib.check(L.bh_init(1 << local, 0))
+    DA = _lib.DeviceArray
+    if a.config == 3:
+        w = workload.generate_block(seed=a.seed + 1000 * rank)
+        n, curve = w.n, _lib.BH_CURVE_P256
+        hb = _lib.BhBatch(*[x.ctypes.data for x in (w.pub, w.sig, w.sig_off, w.sig_len, w.msg,
+                                                    w.msg_off, w.msg_len)])
+        dev = [DA.from_numpy(local, x) for x in (w.pub, w.sig, w.sig_off, w.sig_len, w.msg,
+                                                 w.msg_off, w.msg_len)]
+        db = _lib.BhBatch(*[x.ptr for x in dev])
+        expect = w.reason
+        workload_desc = (f"BASELINE config 3: one block, 500 tx x (creator over 4096 B + 3 "
+                         f"endorsements over 1536 B) = {n} P-256 records, 50 client + 4 peer "
+                         f"keys, 1/100 corrupted, fused SHA-256")
+        flags = _lib.BH_F_HASH_SHA256
+
+        def host_call(bitmap, reason):
+            return L.bh_verify(curve, ctypes.byref(hb), n, flags, bitmap.ctypes.data,
+                               reason.ctypes.data)
+
+        def dev_call(words, reason, tm):
+            return L.bh_verify_dev(local, curve, ctypes.byref(db), n, flags, words.ptr,
+                                   reason.ptr, None, 1, tm)
+    else:
+        r = workload.generate_bdls_round(a.validators, a.curve, seed=a.seed + 1000 * rank)
+        n, curve = r.n, a.curve
+        arrs = r.arrays()
+        hb = _lib.BhBdlsBatch(*[x.ctypes.data for x in arrs])
+        dev = [DA.from_numpy(local, x) for x in arrs]
+        db = _lib.BhBdlsBatch(*[x.ptr for x in dev])
+        expect = np.zeros(n, np.uint8)
+        t2p1 = 2 * ((a.validators - 1) // 3) + 1
+        workload_desc = (f"BASELINE config 4: one BDLS round at {a.validators} validators -- "
+                         f"{a.validators} roundchange + lock + {t2p1} proofs + "
+                         f"{a.validators} commit + decide + {t2p1} proofs = {n} SignedProto "
+                         f"records, {'secp256k1' if curve == 1 else 'P-256'}, BLAKE2b-256")
+
+        def host_call(bitmap, reason):
+            return L.bh_verify_bdls(curve, ctypes.byref(hb), n, bitmap.ctypes.data,
+                                    reason.ctypes.data)
+
+        def dev_call(words, reason, tm):
+            return L.bh_verify_bdls_dev(local, curve, ctypes.byref(db), n, words.ptr,
+                                        reason.ptr, None, 1, tm)
+
+    bitmap = np.zeros((n + 7) // 8, np.uint8)
+    reason = np.zeros(n, np.uint8)
+    dwords = DA(local, ((n + 63) // 64) * 8)
+    dreason = DA(local, n)
+    for _ in range(max(1, a.warmup)):
+        _lib.check(host_call(bitmap, reason))
+        _lib.check(dev_call(dwords, dreason, None))
+    dist.barrier(world)
+    host_ms, dev_ms = [], []
+    tm = _lib.BhTiming()
+    kern = {k: 0.0 for k in _lib.BhTiming.STAGES}
+    for _ in range(a.steps):
+        t = time.perf_counter()
+        _lib.check(host_call(bitmap, reason))
+        host_ms.append((time.perf_counter() - t) * 1e3)
+    for _ in range(a.steps):
+        t = time.perf_counter()
+        _lib.check(dev_call(dwords, dreason, None))
+        dev_ms.append((time.perf_counter() - t) * 1e3)
+    _lib.check(dev_call(dwords, dreason, ctypes.byref(tm)))
+    kern = {k: round(getattr(tm, k), 4) for k in _lib.BhTiming.STAGES}
+    dist.barrier(world)
+    p50 = dist.max_over_ranks(percentile(host_ms, 50), world)
+    parity_ok = bool((reason == expect).all() and (dreason.to_numpy(np.uint8, n) == expect).all()
+                     and (np.unpackbits(bitmap, bitorder="little")[:n].astype(bool)
+                          == (expect == 0)).all())
+    parity_ok = dist.all_true(parity_ok, world)
+    out = {
+        "metric": ("block-validate latency (ms, one block's signatures, host C ABI)"
+                   if a.config == 3 else "BDLS round verify latency (ms, host C ABI)"),
+        "value": round(p50, 4), "unit": "ms", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(p50, 4), "higher_is_better": False,
+        "scaling": "replicas", "vs_baseline": None,
+        "dtype": "u32", "data": "synthetic (seeded keys/signatures, workload/gen.c)",
+        "config": {"workload": workload_desc, "records": n},
+        "parity": parity_ok,
+        "latency_ms": {"host_p50": round(percentile(host_ms, 50), 4),
+                       "host_p99": round(percentile(host_ms, 99), 4),
+                       "device_resident_p50": round(percentile(dev_ms, 50), 4),
+                       "device_resident_p99": round(percentile(dev_ms, 99), 4)},
+        "kernel_ms": kern,
+        "routes": {"keycomb": tm.n_keycomb, "ladder": tm.n_ladder, "key_tables": tm.n_keytables},
+    }
+    if rank == 0 and a.cpu_baseline:
+        from oracle import orc
+        cpu = []
+        deadline = time.perf_counter() + 10.0
+        while time.perf_counter() < deadline and len(cpu) < a.steps:
+            t = time.perf_counter()
+            if a.config == 3:
+                got = orc.batch_verify(w.pub.reshape(-1, 64), w.msg, w.msg_off, w.msg_len, w.sig,
+                                       w.sig_off, w.sig_len, fused=True, nthreads=a.cpu_threads)
+            else:
+                got = orc.bdls_verify(curve, *arrs)
+            cpu.append((time.perf_counter() - t) * 1e3)
+        cores = a.cpu_threads if a.config == 3 else 1
+        out["cpu_baseline"] = {
+            "value": round(percentile(cpu, 50), 4), "unit": "ms", "cores": cores, "kind": "port",
+            "sample": f"the same {n} records, {len(cpu)} repetitions, p50; "
+                      + ("identity.Verify semantics, OpenSSL ECDSA_do_verify, "
+                         f"{cores} threads" if a.config == 3 else
+                         "serial SignedProto.Verify as the consensus loop runs it "
+                         "(BLAKE2b-256 + OpenSSL ECDSA_do_verify), 1 thread"),
+            "parity": bool((got == expect).all()),
+        }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.finalize(world)
+    return 0 if parity_ok else 3
+
+
 def main():
     a = parse()
     from bdls_amd import _lib, dist, workload
     rank, world, local = dist.env_rank()
     dist.init(world)
+    if a.config in (3, 4):
+        return bench_latency(a, rank, world, local)
 
     nkeys = a.n if a.config == 5 else a.nkeys
     corrupt = 64 if a.config == 5 else a.corrupt_den

@@ -311,3 +311,101 @@ int orc_batch_verify(int curve, int fused, size_t n, const uint8_t *q, const uin
   for (int t = 0; t < used; t++) pthread_join(th[t], NULL);
   return 0;
 }
+
+/* ---- BDLS SignedProto.Verify ---------------------------------------------
+ * vendor/github.com/BDLS-bft/bdls/message.go:97-138 (Hash: BLAKE2b-256 over
+ * prefix || Version LE || X || Y || len(Message) LE || Message) and :170-184
+ * (Verify: ecdsa.Verify(pub, Hash(), SetBytes(R), SetBytes(S))). BLAKE2b per
+ * RFC 7693 (Go's golang.org/x/crypto/blake2b New256, unkeyed). */
+static const uint64_t kIV[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull,
+                                0x3c6ef372fe94f82bull, 0xa54ff53a5f1d36f1ull,
+                                0x510e527fade682d1ull, 0x9b05688c2b3e6c1full,
+                                0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
+static const uint8_t kSig[10][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11}, {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0}};
+
+static uint64_t rr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+static void b2_compress(uint64_t h[8], const uint8_t *blk, uint64_t t, int last) {
+  uint64_t m[16], v[16];
+  for (int i = 0; i < 16; i++) {
+    m[i] = 0;
+    for (int b = 0; b < 8; b++) m[i] |= (uint64_t)blk[8 * i + b] << (8 * b);
+  }
+  memcpy(v, h, 64);
+  memcpy(v + 8, kIV, 64);
+  v[12] ^= t;
+  if (last) v[14] ^= ~0ull;
+  static const int G[8][4] = {{0, 4, 8, 12}, {1, 5, 9, 13}, {2, 6, 10, 14}, {3, 7, 11, 15},
+                              {0, 5, 10, 15}, {1, 6, 11, 12}, {2, 7, 8, 13}, {3, 4, 9, 14}};
+  for (int r = 0; r < 12; r++) {
+    const uint8_t *s = kSig[r % 10];
+    for (int g = 0; g < 8; g++) {
+      int a = G[g][0], b = G[g][1], c = G[g][2], d = G[g][3];
+      v[a] += v[b] + m[s[2 * g]];
+      v[d] = rr64(v[d] ^ v[a], 32);
+      v[c] += v[d];
+      v[b] = rr64(v[b] ^ v[c], 24);
+      v[a] += v[b] + m[s[2 * g + 1]];
+      v[d] = rr64(v[d] ^ v[a], 16);
+      v[c] += v[d];
+      v[b] = rr64(v[b] ^ v[c], 63);
+    }
+  }
+  for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[i + 8];
+}
+
+static void bdls_hash(uint8_t out[32], uint32_t ver, const uint8_t xy[64], const uint8_t *msg,
+                      uint32_t ml) {
+  uint8_t hdr[96];
+  memcpy(hdr, "BDLS_CONSENSUS_SIGNATURE", 24);
+  for (int i = 0; i < 4; i++) hdr[24 + i] = (uint8_t)(ver >> (8 * i));
+  memcpy(hdr + 28, xy, 64);
+  for (int i = 0; i < 4; i++) hdr[92 + i] = (uint8_t)(ml >> (8 * i));
+  uint64_t h[8];
+  memcpy(h, kIV, 64);
+  h[0] ^= 0x01010020ull;
+  const uint64_t total = 96 + (uint64_t)ml;
+  uint8_t blk[128];
+  for (uint64_t pos = 0;; pos += 128) {
+    const int last = total - pos <= 128;
+    for (int k = 0; k < 128; k++) {
+      uint64_t p = pos + k;
+      blk[k] = p >= total ? 0 : p < 96 ? hdr[p] : msg[p - 96];
+    }
+    b2_compress(h, blk, last ? total : pos + 128, last);
+    if (last) break;
+  }
+  for (int i = 0; i < 32; i++) out[i] = (uint8_t)(h[i / 8] >> (8 * (i % 8)));
+}
+
+int orc_bdls_hash(uint32_t ver, const uint8_t xy[64], const uint8_t *msg, uint32_t ml,
+                  uint8_t out[32]) {
+  bdls_hash(out, ver, xy, msg, ml);
+  return 0;
+}
+
+/* Serial, as the consensus loop verifies (consensus.go:456-466 then the
+ * message's own Verify and, for <lock>/<decide>, each proof). */
+int orc_bdls_verify(int curve, size_t n, const uint8_t *xy, const uint8_t *r, const uint64_t *roff,
+                    const uint32_t *rlen, const uint8_t *s, const uint64_t *soff,
+                    const uint32_t *slen, const uint32_t *ver, const uint8_t *msg,
+                    const uint64_t *moff, const uint32_t *mlen, uint8_t *reason) {
+  orc_ctx c;
+  ctx_init(&c, curve);
+  uint8_t dg[32];
+  for (size_t i = 0; i < n; i++) {
+    bdls_hash(dg, ver[i], xy + 64 * i, msg + moff[i], mlen[i]);
+    BN_bin2bn(r + roff[i], (int)rlen[i], c.r);
+    BN_bin2bn(s + soff[i], (int)slen[i], c.s);
+    reason[i] = (uint8_t)(BN_is_zero(c.r)   ? R_R_NONPOS
+                          : BN_is_zero(c.s) ? R_S_NONPOS
+                                            : go_verify(&c, xy + 64 * i, dg, 32));
+  }
+  ctx_free(&c);
+  return 0;
+}

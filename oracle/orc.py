@@ -33,6 +33,9 @@ def lib():
         L.orc_batch_verify.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t] + [u8p] * 7 + \
             [u8p, ctypes.c_int]
         L.orc_batch_verify.restype = ctypes.c_int
+        L.orc_bdls_verify.argtypes = [ctypes.c_int, ctypes.c_size_t] + [u8p] * 12
+        L.orc_bdls_verify.restype = ctypes.c_int
+        L.orc_bdls_hash.argtypes = [ctypes.c_uint32, u8p, u8p, ctypes.c_uint32, u8p]
         _LIB = L
     return _LIB
 
@@ -74,4 +77,22 @@ def batch_verify(q: np.ndarray, msg: np.ndarray, moff: np.ndarray, mlen: np.ndar
     lib().orc_batch_verify(curve, 1 if fused else 0, n, q.ctypes.data, msg.ctypes.data,
                            moff.ctypes.data, mlen.ctypes.data, sig.ctypes.data,
                            soff.ctypes.data, slen.ctypes.data, reason.ctypes.data, nthreads)
+    return reason
+
+
+def bdls_hash(version: int, xy: bytes, msg: bytes) -> bytes:
+    """SignedProto.Hash (message.go:97-138)."""
+    out = ctypes.create_string_buffer(32)
+    lib().orc_bdls_hash(version, _buf(xy), _buf(msg), len(msg), out)
+    return out.raw
+
+
+def bdls_verify(curve: int, xy, r, r_off, r_len, s, s_off, s_len, version, msg, msg_off,
+                msg_len) -> np.ndarray:
+    """Serial SignedProto.Verify over a bh_bdls_batch-shaped SoA; reason per record."""
+    arrs = [np.ascontiguousarray(a) for a in (xy, r, r_off, r_len, s, s_off, s_len, version, msg,
+                                              msg_off, msg_len)]
+    n = len(arrs[7])
+    reason = np.zeros(n, dtype=np.uint8)
+    lib().orc_bdls_verify(curve, n, *[a.ctypes.data for a in arrs], reason.ctypes.data)
     return reason

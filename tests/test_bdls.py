@@ -153,3 +153,82 @@ def test_bdls_gpu_golden(bdls_golden, curve):
     assert not bad
     valid = np.unpackbits(bitmap, bitorder="little")[:n].astype(bool)
     assert [bool(v) for v in valid] == [r["valid"] for r in recs]
+
+
+def _round_records(b, idx):
+    out = []
+    for i in idx:
+        xy = bytes(b.xy[64 * i:64 * i + 64])
+        out.append(dict(x=xy[:32], y=xy[32:],
+                        r=bytes(b.r[b.r_off[i]:b.r_off[i] + b.r_len[i]]),
+                        s=bytes(b.s[b.s_off[i]:b.s_off[i] + b.s_len[i]]),
+                        msg=bytes(b.msg[b.msg_off[i]:b.msg_off[i] + b.msg_len[i]]),
+                        version=int(b.version[i])))
+    return out
+
+
+@pytest.mark.parametrize("curve", [1, 0])
+def test_bdls_round_generator_vs_oracle(curve):
+    """gen.c's round (BASELINE config 4): structure and signatures, checked on
+    the lock/decide records, first/last votes and a proof copy."""
+    from bdls_amd.workload import generate_bdls_round
+    b = generate_bdls_round(nval=10, curve=curve, small_len=50, seed=7)
+    t2p1 = 2 * 3 + 1
+    assert b.n == 2 * 10 + 2 * (1 + t2p1)
+    c = O.SECP256K1 if curve == 1 else O.P256
+    lock, decide = 10, 10 + 1 + t2p1 + 10
+    recs = _round_records(b, [0, 9, lock, lock + 1, decide, b.n - 1])
+    for rec in recs:
+        dg = O.bdls_signed_proto_hash(rec["version"], rec["x"], rec["y"], rec["msg"])
+        rc = O.go_ecdsa_verify(c, int.from_bytes(rec["x"], "big"), int.from_bytes(rec["y"], "big"),
+                               dg, int.from_bytes(rec["r"], "big"), int.from_bytes(rec["s"], "big"))
+        assert rc == O.R_OK
+    assert recs[3] == _round_records(b, [0])[0]  # proof re-verifies roundchange 0
+    assert recs[2]["x"] == recs[0]["x"]          # leader signs <lock>
+    assert len(recs[2]["msg"]) > t2p1 * 50
+
+
+@pytest.mark.parametrize("curve", [1, 0])
+def test_bdls_round_hostsim(hs, curve):
+    from bdls_amd.workload import generate_bdls_round
+    b = generate_bdls_round(nval=16, curve=curve, small_len=120, seed=3)
+    out = np.full(b.n, 255, np.uint8)
+    hs.hs_verify_bdls(curve, *[a.ctypes.data for a in b.arrays()], b.n, 1000, out.ctypes.data)
+    assert not out.any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("curve", [1, 0])
+def test_bdls_round_gpu(curve):
+    from bdls_amd import _lib
+    from bdls_amd.workload import generate_bdls_round
+    _lib.ensure_init()
+    b = generate_bdls_round(nval=100, curve=curve, seed=11)
+    bitmap = np.zeros((b.n + 7) // 8, np.uint8)
+    reason = np.full(b.n, 255, np.uint8)
+    bb = _lib.BhBdlsBatch(*[a.ctypes.data for a in b.arrays()])
+    _lib.check(_lib.lib().bh_verify_bdls(curve, ctypes.byref(bb), b.n, bitmap.ctypes.data,
+                                         reason.ctypes.data))
+    assert not reason.any()
+    assert np.unpackbits(bitmap, bitorder="little")[:b.n].all()
+    # a flipped message byte in the <decide> record is rejected, nothing else changes
+    t2p1 = 2 * 33 + 1
+    dec = 100 + 1 + t2p1 + 100
+    b.msg[b.msg_off[dec] + 5] ^= 0x40
+    _lib.check(_lib.lib().bh_verify_bdls(curve, ctypes.byref(bb), b.n, bitmap.ctypes.data,
+                                         reason.ctypes.data))
+    assert reason[dec] == 9 and np.count_nonzero(reason) == 1
+
+
+def test_c_oracle_bdls_golden(bdls_golden):
+    """oracle/orc.c's BDLS hash + verify against the golden set."""
+    from oracle import orc
+    for curve in ("secp256k1", "P-256"):
+        recs = [r for r in bdls_golden if r["curve"] == curve]
+        for r in recs[:20]:
+            assert orc.bdls_hash(r["version"], bytes.fromhex(r["x"] + r["y"]),
+                                 bytes.fromhex(r["msg"])).hex() == r["digest"]
+        got = orc.bdls_verify(CURVE_ID[curve], *pack_bdls(recs))
+        bad = [(r["tag"], int(g), r["reason"]) for r, g in zip(recs, got)
+               if g != r["reason"] and not (r["reason"] == 7 and g == 9)]
+        assert not bad
