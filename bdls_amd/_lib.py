@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libbdlship.so")
 BH_OK = 0
 BH_F_HASH_SHA256 = 1
 BH_F_NO_LOW_S = 2
+BH_F_KEEP_KEYS = 4
 BH_CURVE_P256 = 0
 BH_CURVE_SECP256K1 = 1
 
@@ -23,8 +24,10 @@ EXPORTS = (
     "bh_init", "bh_shutdown", "bh_device_count", "bh_last_error", "bh_version",
     "bh_workspace_bytes", "bh_verify", "bh_verify_dev", "bh_csp_verify_p256",
     "bh_parse_der_sig", "bh_dev_alloc", "bh_dev_free", "bh_memcpy_h2d", "bh_memcpy_d2h",
-    "bh_sync", "bh_verify_bdls", "bh_verify_bdls_dev",
+    "bh_sync", "bh_verify_bdls", "bh_verify_bdls_dev", "bh_keys_reserve", "bh_keys_register",
+    "bh_keys_clear", "bh_keys_count",
 )
+KEY_FULL = 255  # bh_keys_register status: registry full
 
 
 class BhBatch(ctypes.Structure):
@@ -47,12 +50,12 @@ class BhBdlsBatch(ctypes.Structure):
 
 class BhTiming(ctypes.Structure):
     _fields_ = [("prep_ms", ctypes.c_float), ("inv_ms", ctypes.c_float),
-                ("plan_ms", ctypes.c_float), ("ktab_ms", ctypes.c_float),
-                ("keycomb_ms", ctypes.c_float), ("ladder_ms", ctypes.c_float),
+                ("plan_ms", ctypes.c_float), ("build_ladder_ms", ctypes.c_float),
+                ("publish_ms", ctypes.c_float), ("keycomb_ms", ctypes.c_float),
                 ("n_keycomb", ctypes.c_uint32), ("n_ladder", ctypes.c_uint32),
-                ("n_keytables", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("n_keytables", ctypes.c_uint32), ("wide", ctypes.c_uint32)]
 
-    STAGES = ("prep_ms", "inv_ms", "plan_ms", "ktab_ms", "keycomb_ms", "ladder_ms")
+    STAGES = ("prep_ms", "inv_ms", "plan_ms", "build_ladder_ms", "publish_ms", "keycomb_ms")
 
 
 class EngineError(RuntimeError):
@@ -105,6 +108,14 @@ def lib() -> ctypes.CDLL:
         L.bh_memcpy_d2h.restype = i32
         L.bh_sync.argtypes = [i32]
         L.bh_sync.restype = i32
+        L.bh_keys_reserve.argtypes = [i32, i32, sz]
+        L.bh_keys_reserve.restype = i32
+        L.bh_keys_register.argtypes = [i32, i32, vp, sz, vp]
+        L.bh_keys_register.restype = i32
+        L.bh_keys_clear.argtypes = [i32, i32]
+        L.bh_keys_clear.restype = i32
+        L.bh_keys_count.argtypes = [i32, i32, ctypes.POINTER(sz)]
+        L.bh_keys_count.restype = i32
         _lib = L
     return _lib
 

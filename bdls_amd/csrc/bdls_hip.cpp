@@ -1,15 +1,18 @@
-// libbdlship.so host runtime: device contexts, workspaces, C ABI (include/bdls_hip.h).
+// libbdlship.so host runtime: device contexts, workspaces, key registries,
+// C ABI (include/bdls_hip.h).
 //
 // One context per initialised GPU: a HIP stream, the fixed-base G tables (one
-// per curve) and a growable workspace. The host-buffer API shards a batch
-// into contiguous record ranges (multiples of 64 so bitmap words concatenate)
-// and drives each device from its own host thread -- no collective, since
-// records are independent.
+// per curve), a growable workspace, a staging buffer for host batches and one
+// key registry per curve. The host-buffer API shards a batch into contiguous
+// record ranges (multiples of 64 so bitmap words concatenate) and drives each
+// device from its own host thread -- no collective, since records are
+// independent.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -21,11 +24,14 @@
 namespace bh {
 hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s);
 hipError_t launch_verify(int curve, const BatchIn& in, const Work& w, const Plan& pl,
-                         const uint32_t* gtab, uint32_t n, uint32_t chunk, uint64_t* bitmap,
-                         uint8_t* reason, hipStream_t s, hipEvent_t* ev);
+                         const KeyReg& g, const uint32_t* gtab, uint32_t n, const LaunchOpts& o,
+                         uint64_t* bitmap, uint8_t* reason, hipStream_t s, hipEvent_t* ev);
 hipError_t launch_verify_bdls(int curve, const BdlsIn& in, const Work& w, const Plan& pl,
-                              const uint32_t* gtab, uint32_t n, uint32_t chunk, uint64_t* bitmap,
-                              uint8_t* reason, hipStream_t s, hipEvent_t* ev);
+                              const KeyReg& g, const uint32_t* gtab, uint32_t n,
+                              const LaunchOpts& o, uint64_t* bitmap, uint8_t* reason,
+                              hipStream_t s, hipEvent_t* ev);
+hipError_t launch_register(int curve, const uint8_t* pub, const Work& w, const Plan& pl,
+                           const KeyReg& g, uint32_t n, uint8_t* status, hipStream_t s);
 }  // namespace bh
 
 namespace {
@@ -46,6 +52,16 @@ int fail(int code, const std::string& msg) {
 
 constexpr size_t kMaxChunk = size_t(1) << 22;  // records per kernel pass (workspace bound)
 constexpr size_t kGtabWords = size_t(bh::kCombWindows) * bh::kCombEntries * bh::kGEntry;
+constexpr size_t kDefaultRegCap = size_t(1) << 16;
+
+size_t round64(size_t n) { return (n + 63) & ~size_t(63); }
+size_t round256(size_t n) { return (n + 255) & ~size_t(255); }
+
+size_t pow2_at_least(size_t v) {
+  size_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
 
 struct DevBuf {
   void* p = nullptr;
@@ -68,51 +84,55 @@ struct DevBuf {
   }
 };
 
+struct Registry {
+  DevBuf mem;
+  bh::KeyReg g{};  // cap == 0: not allocated
+};
+
 struct Dev {
   int id = -1;
   hipStream_t stream = nullptr;
   uint32_t* gtab[2] = {nullptr, nullptr};
-  DevBuf ws;        // Work arrays
-  DevBuf in_fix;    // host-API staging: pub, offsets, lengths
-  DevBuf in_sig, in_msg, out;
+  DevBuf ws;     // Work + Plan
+  DevBuf stage;  // host-API inputs
+  DevBuf out;    // host-API bitmap words + reasons
+  Registry reg[2];
   hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t done = nullptr;  // end of the last pass (orders passes across streams)
+  bool done_recorded = false;
   std::mutex mu;
 };
 
 std::mutex g_mu;
 std::vector<Dev*> g_devs;
 
-size_t round64(size_t n) { return (n + 63) & ~size_t(63); }
-
-size_t pow2_at_least(size_t v) {
-  size_t p = 1;
-  while (p < v) p <<= 1;
-  return p;
-}
-
-size_t max_tables_for(size_t ns) {
-  return std::min<size_t>(ns / bh::kMinUses, size_t(1) << 16);
+// Table builds per pass: verify needs >= 2 uses per table (at most ns / 2);
+// registration builds one per key straight into the registry (no per-batch
+// table memory).
+size_t max_tables_for(size_t ns, bool reg = false) {
+  return std::min<size_t>(reg ? ns : ns / 2, size_t(1) << 16);
 }
 
 size_t work_bytes(size_t ns) {
   // 4 scalar SoA arrays (8 limbs) + 4 base-field SoA arrays (9 limbs) + status
-  // + per-lane Q tables; then the key plan (fingerprint table, lists, key
-  // tables). Every carve is rounded to 256 bytes.
+  // + per-lane Q tables; then the key plan (fingerprint table, per-record
+  // slot / table id / lists, build jobs, per-batch tables). Every carve is
+  // rounded to 256 bytes.
   const size_t hc = pow2_at_least(2 * ns);
   const size_t mt = max_tables_for(ns);
   return 4 * 32 * ns + 4 * 36 * ns + ns + (ns / 64) * 64 * bh::kQTab * bh::kQPt * 4 +
-         hc * (8 + 4 + 4 + 4) + ns * 12 + 16 + mt * 4 + mt * (size_t)bh::kKTabWords * 4 +
-         256 * 24;
+         hc * (8 + 4 + 4 + 4) + ns * 16 + 16 + mt * 8 + mt * (size_t)bh::kKTabWords * 4 +
+         256 * 26;
 }
 
-int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl) {
+int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl, bool reg = false) {
   const size_t ns = round64(n);
   int rc = d.ws.ensure(work_bytes(ns));
   if (rc) return rc;
   char* p = (char*)d.ws.p;
   auto take = [&](size_t bytes) {
     char* q = p;
-    p += (bytes + 255) & ~size_t(255);
+    p += round256(bytes);
     return q;
   };
   w->ns = (uint32_t)ns;
@@ -127,7 +147,7 @@ int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl) {
   w->st = (uint8_t*)take(ns);
   w->qtab = (uint32_t*)take((ns / 64) * 64 * bh::kQTab * bh::kQPt * 4);
   const size_t hc = pow2_at_least(2 * ns);
-  const size_t mt = max_tables_for(ns);
+  const size_t mt = max_tables_for(ns, reg);
   pl->hc = (uint32_t)hc;
   pl->max_tables = (uint32_t)mt;
   pl->slot_hash = (uint64_t*)take(hc * 8);
@@ -137,9 +157,44 @@ int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl) {
   pl->rec_slot = (uint32_t*)take(ns * 4);
   pl->comb_list = (uint32_t*)take(ns * 4);
   pl->ladder_list = (uint32_t*)take(ns * 4);
+  pl->rec_tab = (uint32_t*)take(ns * 4);
   pl->counters = (uint32_t*)take(16);
   pl->tab_rec = (uint32_t*)take(mt * 4 + 4);
-  pl->tables = (uint32_t*)take(mt * (size_t)bh::kKTabWords * 4 + 4);
+  pl->tab_dst = (uint32_t*)take(mt * 4 + 4);
+  pl->tables = (uint32_t*)take(reg ? 4 : mt * (size_t)bh::kKTabWords * 4 + 4);
+  return BH_OK;
+}
+
+// (Re)allocate and clear a key registry (caller holds d.mu, device set).
+int reg_alloc(Dev& d, int curve, size_t cap) {
+  Registry& r = d.reg[curve];
+  if (cap == 0 || cap > (size_t(1) << 24)) return fail(BH_E_INVALID, "registry capacity out of range");
+  const size_t hc = pow2_at_least(2 * cap);
+  const size_t bytes = round256(hc * 8) + round256(hc * 4) + round256(cap * 72) +
+                       round256(cap * (size_t)bh::kKTabWords * 4) + 256;
+  if (d.done_recorded) HIPCHK(hipEventSynchronize(d.done));
+  r.mem.release();
+  r.g = bh::KeyReg{};
+  int rc = r.mem.ensure(bytes);
+  if (rc) return rc;
+  char* p = (char*)r.mem.p;
+  auto take = [&](size_t b) {
+    char* q = p;
+    p += round256(b);
+    return q;
+  };
+  bh::KeyReg g{};
+  g.cap = (uint32_t)cap;
+  g.hc = (uint32_t)hc;
+  g.slot_hash = (uint64_t*)take(hc * 8);
+  g.slot_tab = (uint32_t*)take(hc * 4);
+  g.keys = (uint32_t*)take(cap * 72);
+  g.tables = (uint32_t*)take(cap * (size_t)bh::kKTabWords * 4);
+  g.count = (uint32_t*)take(4);
+  HIPCHK(hipMemsetAsync(g.slot_hash, 0, hc * 8, d.stream));
+  HIPCHK(hipMemsetAsync(g.count, 0, 4, d.stream));
+  HIPCHK(hipStreamSynchronize(d.stream));
+  r.g = g;
   return BH_OK;
 }
 
@@ -157,22 +212,24 @@ int dev_init(Dev& d, int id) {
     HIPCHK(bh::launch_gtab_build(c, d.gtab[c], d.stream));
   }
   for (auto& e : d.ev) HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
   HIPCHK(hipStreamSynchronize(d.stream));
   return BH_OK;
 }
 
 void dev_free(Dev& d) {
   (void)hipSetDevice(d.id);
+  if (d.done_recorded) (void)hipEventSynchronize(d.done);
   if (d.stream) (void)hipStreamSynchronize(d.stream);
   for (auto& g : d.gtab)
     if (g) (void)hipFree(g);
   d.ws.release();
-  d.in_fix.release();
-  d.in_sig.release();
-  d.in_msg.release();
+  d.stage.release();
   d.out.release();
+  for (auto& r : d.reg) r.mem.release();
   for (auto& e : d.ev)
     if (e) (void)hipEventDestroy(e);
+  if (d.done) (void)hipEventDestroy(d.done);
   if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
@@ -183,9 +240,22 @@ Dev* get_dev(int device) {
   return nullptr;
 }
 
-uint32_t inv_chunk(size_t n) {
-  size_t c = n / 65536;
-  return (uint32_t)std::max<size_t>(1, std::min<size_t>(16, c));
+std::vector<Dev*> all_devs() {
+  std::lock_guard<std::mutex> g(g_mu);
+  return g_devs;
+}
+
+bh::LaunchOpts launch_opts(size_t m, uint32_t flags) {
+  bh::LaunchOpts o;
+  o.inv_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(16, m / 65536));
+  o.keep = (flags & BH_F_KEEP_KEYS) != 0;
+  // kept tables pay off over later calls, so a second use in the batch is
+  // enough; per-batch tables must pay off inside this batch
+  o.min_uses = o.keep ? 2u : bh::kMinUses;
+  o.min_batch = o.keep ? 0u : bh::kKeyTableMinBatch;
+  // below chip size, spread each key-table record over 16 or 4 lanes
+  o.wide = m <= 8192 ? 16 : m <= 32768 ? 4 : 1;
+  return o;
 }
 
 // Record-range views of the two input kinds (for kMaxChunk passes).
@@ -199,14 +269,14 @@ bh::BdlsIn slice(const bh_bdls_batch* b, size_t base, uint32_t flags) {
                     b->msg, b->msg_off + base, b->msg_len + base, flags};
 }
 hipError_t launch(int curve, const bh::BatchIn& in, const bh::Work& w, const bh::Plan& pl,
-                  const uint32_t* gtab, uint32_t n, uint32_t chunk, uint64_t* bm, uint8_t* rs,
-                  hipStream_t s, hipEvent_t* ev) {
-  return bh::launch_verify(curve, in, w, pl, gtab, n, chunk, bm, rs, s, ev);
+                  const bh::KeyReg& g, const uint32_t* gtab, uint32_t n, const bh::LaunchOpts& o,
+                  uint64_t* bm, uint8_t* rs, hipStream_t s, hipEvent_t* ev) {
+  return bh::launch_verify(curve, in, w, pl, g, gtab, n, o, bm, rs, s, ev);
 }
 hipError_t launch(int curve, const bh::BdlsIn& in, const bh::Work& w, const bh::Plan& pl,
-                  const uint32_t* gtab, uint32_t n, uint32_t chunk, uint64_t* bm, uint8_t* rs,
-                  hipStream_t s, hipEvent_t* ev) {
-  return bh::launch_verify_bdls(curve, in, w, pl, gtab, n, chunk, bm, rs, s, ev);
+                  const bh::KeyReg& g, const uint32_t* gtab, uint32_t n, const bh::LaunchOpts& o,
+                  uint64_t* bm, uint8_t* rs, hipStream_t s, hipEvent_t* ev) {
+  return bh::launch_verify_bdls(curve, in, w, pl, g, gtab, n, o, bm, rs, s, ev);
 }
 
 // Core device-resident pass (caller holds d.mu and has set the device).
@@ -215,14 +285,22 @@ template <class B>
 int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* bitmap,
             uint8_t* reason, hipStream_t s, bh_timing* t) {
   if (t) *t = bh_timing{};
+  if ((flags & BH_F_KEEP_KEYS) && d.reg[curve].g.cap == 0) {
+    int rc = reg_alloc(d, curve, kDefaultRegCap);
+    if (rc) return rc;
+  }
+  // the workspace is shared by every pass on this device: a pass on another
+  // stream starts after the previous one ended
+  if (d.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.done, 0));
   for (size_t base = 0; base < n; base += kMaxChunk) {
     const size_t m = std::min(kMaxChunk, n - base);
     bh::Work w;
     bh::Plan pl;
     int rc = carve_work(d, m, &w, &pl);
     if (rc) return rc;
-    HIPCHK(launch(curve, slice(b, base, flags), w, pl, d.gtab[curve], (uint32_t)m, inv_chunk(m),
-                  bitmap + base / 64, reason + base, s, t ? d.ev : nullptr));
+    const bh::LaunchOpts o = launch_opts(m, flags);
+    HIPCHK(launch(curve, slice(b, base, flags), w, pl, d.reg[curve].g, d.gtab[curve],
+                  (uint32_t)m, o, bitmap + base / 64, reason + base, s, t ? d.ev : nullptr));
     if (t) {
       HIPCHK(hipEventSynchronize(d.ev[6]));
       float ms[6];
@@ -230,26 +308,207 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
       t->prep_ms += ms[0];
       t->inv_ms += ms[1];
       t->plan_ms += ms[2];
-      t->ktab_ms += ms[3];
-      t->keycomb_ms += ms[4];
-      t->ladder_ms += ms[5];
+      t->build_ladder_ms += ms[3];
+      t->publish_ms += ms[4];
+      t->keycomb_ms += ms[5];
       uint32_t cnt[4];
       HIPCHK(hipMemcpy(cnt, pl.counters, 16, hipMemcpyDeviceToHost));
       t->n_keycomb += cnt[0];
       t->n_ladder += cnt[1];
       t->n_keytables += std::min<uint32_t>(cnt[2], pl.max_tables);
+      t->wide = (uint32_t)o.wide;
     }
+  }
+  HIPCHK(hipEventRecord(d.done, s));
+  d.done_recorded = true;
+  return BH_OK;
+}
+
+// ---- host-buffer staging ---------------------------------------------------
+// A variable-length field over records [lo, lo + m): its byte range in the
+// caller's buffer and the offsets rebased to that range.
+struct VarField {
+  uint64_t lo = 0, bytes = 0;
+  std::vector<uint64_t> off;
+};
+
+VarField rebase(const uint64_t* off, const uint32_t* len, size_t lo, size_t m) {
+  VarField v;
+  uint64_t a = UINT64_MAX, z = 0;
+  for (size_t i = lo; i < lo + m; i++) {
+    a = std::min<uint64_t>(a, off[i]);
+    z = std::max<uint64_t>(z, off[i] + len[i]);
+  }
+  v.lo = (a == UINT64_MAX) ? 0 : a;
+  v.bytes = z > v.lo ? z - v.lo : 0;
+  v.off.resize(m);
+  for (size_t i = 0; i < m; i++) v.off[i] = off[lo + i] - v.lo;
+  return v;
+}
+
+// Carves the device staging buffer and queues one H2D copy per array.
+struct Uploader {
+  char* base;
+  hipStream_t s;
+  size_t used = 0;
+  hipError_t err = hipSuccess;
+  template <class T>
+  const T* put(const T* src, size_t count) {
+    char* dst = base + used;
+    const size_t bytes = count * sizeof(T);
+    used += round256(bytes + 1);
+    if (bytes && src && err == hipSuccess)
+      err = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+    return (const T*)dst;
+  }
+  const uint8_t* put(const uint8_t* data, const VarField& v) {
+    return put<uint8_t>(data ? data + v.lo : nullptr, data ? v.bytes : 0);
+  }
+};
+
+struct HostFields {
+  std::vector<VarField> var;
+  size_t bytes = 0;  // staging bytes
+};
+
+HostFields fields(const bh_batch* b, size_t lo, size_t m) {
+  HostFields f;
+  f.var.push_back(rebase(b->sig_off, b->sig_len, lo, m));
+  f.var.push_back(rebase(b->msg_off, b->msg_len, lo, m));
+  f.bytes = round256(m * 64 + 1) + 4 * round256(m * 8 + 1) + round256(f.var[0].bytes + 1) +
+            round256(f.var[1].bytes + 1);
+  return f;
+}
+
+bh_batch upload(Uploader& u, const bh_batch* b, size_t lo, size_t m, const HostFields& f) {
+  bh_batch d;
+  d.pub = u.put(b->pub + lo * 64, m * 64);
+  d.sig_off = u.put(f.var[0].off.data(), m);
+  d.sig_len = u.put(b->sig_len + lo, m);
+  d.msg_off = u.put(f.var[1].off.data(), m);
+  d.msg_len = u.put(b->msg_len + lo, m);
+  d.sig = u.put(b->sig, f.var[0]);
+  d.msg = u.put(b->msg, f.var[1]);
+  return d;
+}
+
+HostFields fields(const bh_bdls_batch* b, size_t lo, size_t m) {
+  HostFields f;
+  f.var.push_back(rebase(b->r_off, b->r_len, lo, m));
+  f.var.push_back(rebase(b->s_off, b->s_len, lo, m));
+  f.var.push_back(rebase(b->msg_off, b->msg_len, lo, m));
+  f.bytes = round256(m * 64 + 1) + 7 * round256(m * 8 + 1);
+  for (auto& v : f.var) f.bytes += round256(v.bytes + 1);
+  return f;
+}
+
+bh_bdls_batch upload(Uploader& u, const bh_bdls_batch* b, size_t lo, size_t m,
+                     const HostFields& f) {
+  bh_bdls_batch d;
+  d.xy = u.put(b->xy + lo * 64, m * 64);
+  d.r_off = u.put(f.var[0].off.data(), m);
+  d.r_len = u.put(b->r_len + lo, m);
+  d.s_off = u.put(f.var[1].off.data(), m);
+  d.s_len = u.put(b->s_len + lo, m);
+  d.version = u.put(b->version + lo, m);
+  d.msg_off = u.put(f.var[2].off.data(), m);
+  d.msg_len = u.put(b->msg_len + lo, m);
+  d.r = u.put(b->r, f.var[0]);
+  d.s = u.put(b->s, f.var[1]);
+  d.msg = u.put(b->msg, f.var[2]);
+  return d;
+}
+
+// One device's share [lo, lo + m) of a host batch: stage, verify, gather.
+template <class B>
+int host_shard(Dev& d, int curve, const B* b, size_t lo, size_t m, uint32_t flags,
+               uint8_t* bitmap, uint8_t* reason) {
+  std::lock_guard<std::mutex> g(d.mu);
+  HIPCHK(hipSetDevice(d.id));
+  const HostFields f = fields(b, lo, m);
+  int rc;
+  if ((rc = d.stage.ensure(f.bytes + 4096))) return rc;
+  if ((rc = d.out.ensure(round64(m) / 8 + m + 1024))) return rc;
+  hipStream_t s = d.stream;
+  // the staging buffer may still feed a pass queued by an earlier call
+  if (d.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.done, 0));
+  Uploader u{(char*)d.stage.p, s};
+  const B db = upload(u, b, lo, m, f);
+  HIPCHK(u.err);
+  uint64_t* dbm = (uint64_t*)d.out.p;
+  uint8_t* drs = (uint8_t*)(dbm + round64(m) / 64);
+  if ((rc = run_dev(d, curve, &db, m, flags, dbm, drs, s, nullptr))) return rc;
+  std::vector<uint64_t> words(round64(m) / 64);
+  HIPCHK(hipMemcpyAsync(words.data(), dbm, words.size() * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(reason + lo, drs, m, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::memcpy(bitmap + lo / 8, words.data(), (m + 7) / 8);  // lo is a multiple of 64
+  return BH_OK;
+}
+
+// Host batch over all initialised devices: contiguous 64-aligned shards, one
+// host thread per device.
+template <class B>
+int host_verify(int curve, const B* b, size_t n, uint32_t flags, uint8_t* bitmap,
+                uint8_t* reason) {
+  std::vector<Dev*> devs = all_devs();
+  if (devs.empty()) return fail(BH_E_NOT_INIT, "bh_init not called");
+  std::memset(bitmap, 0, (n + 7) / 8);
+  if (n == 0) return BH_OK;
+  const size_t nd = std::min(devs.size(), (n + 63) / 64);
+  const size_t per = round64((n + nd - 1) / nd);
+  std::vector<int> rcs(nd, BH_OK);
+  std::vector<std::string> errs(nd);
+  auto work = [&](size_t k) {
+    const size_t lo = k * per, hi = std::min(n, lo + per);
+    if (lo >= hi) return;
+    rcs[k] = host_shard(*devs[k], curve, b, lo, hi - lo, flags, bitmap, reason);
+    if (rcs[k]) errs[k] = g_err;
+  };
+  if (nd == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < nd; k++) th.emplace_back(work, k);
+    for (auto& t : th) t.join();
+  }
+  for (size_t k = 0; k < nd; k++)
+    if (rcs[k]) return fail(rcs[k], errs[k]);
+  return BH_OK;
+}
+
+int check_curve(int curve) {
+  if (curve != BH_CURVE_P256 && curve != BH_CURVE_SECP256K1)
+    return fail(BH_E_INVALID, "unknown curve");
+  return BH_OK;
+}
+
+// device >= 0: that device; -1: every initialised device.
+int for_devices(int device, const std::function<int(Dev&)>& fn) {
+  std::vector<Dev*> ds;
+  if (device < 0) {
+    ds = all_devs();
+    if (ds.empty()) return fail(BH_E_NOT_INIT, "bh_init not called");
+  } else {
+    Dev* d = get_dev(device);
+    if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
+    ds.push_back(d);
+  }
+  for (Dev* d : ds) {
+    std::lock_guard<std::mutex> g(d->mu);
+    HIPCHK(hipSetDevice(d->id));
+    int rc = fn(*d);
+    if (rc) return rc;
   }
   return BH_OK;
 }
 
 }  // namespace
 
-
 extern "C" {
 
 const char* bh_last_error(void) { return g_err.c_str(); }
-const char* bh_version(void) { return "bdls-hip 0.1.0 (gfx950)"; }
+const char* bh_version(void) { return "bdls-hip 0.2.0 (gfx950)"; }
 
 int bh_init(uint32_t device_mask, uint32_t flags) {
   (void)flags;
@@ -318,90 +577,8 @@ int bh_verify(int curve, const bh_batch* b, size_t n, uint32_t flags, uint8_t* b
                    !bitmap || !reason)))
     return fail(BH_E_INVALID, "null pointer in batch");
   if (curve != BH_CURVE_P256) return fail(BH_E_INVALID, "curve not supported by bh_verify");
-  std::vector<Dev*> devs;
-  {
-    std::lock_guard<std::mutex> g(g_mu);
-    devs = g_devs;
-  }
-  if (devs.empty()) return fail(BH_E_NOT_INIT, "bh_init not called");
-  std::memset(bitmap, 0, (n + 7) / 8);
-  if (n == 0) return BH_OK;
-  // contiguous shards, 64-record aligned
-  const size_t nd = std::min(devs.size(), (n + 63) / 64);
-  const size_t per = round64((n + nd - 1) / nd);
-  std::vector<int> rcs(nd, BH_OK);
-  std::vector<std::string> errs(nd);
-  auto work = [&](size_t k) {
-    const size_t lo = k * per, hi = std::min(n, lo + per);
-    if (lo >= hi) return;
-    const size_t m = hi - lo;
-    Dev& d = *devs[k];
-    std::lock_guard<std::mutex> g(d.mu);
-    auto body = [&]() -> int {
-      HIPCHK(hipSetDevice(d.id));
-      // byte ranges of sig / msg used by this shard; offsets rebased
-      uint64_t smin = UINT64_MAX, smax = 0, mmin = UINT64_MAX, mmax = 0;
-      for (size_t i = lo; i < hi; i++) {
-        smin = std::min<uint64_t>(smin, b->sig_off[i]);
-        smax = std::max<uint64_t>(smax, b->sig_off[i] + b->sig_len[i]);
-        mmin = std::min<uint64_t>(mmin, b->msg_off[i]);
-        mmax = std::max<uint64_t>(mmax, b->msg_off[i] + b->msg_len[i]);
-      }
-      std::vector<uint64_t> so(m), mo(m);
-      for (size_t i = 0; i < m; i++) {
-        so[i] = b->sig_off[lo + i] - smin;
-        mo[i] = b->msg_off[lo + i] - mmin;
-      }
-      const size_t fix = m * 64 + m * 8 * 2 + m * 4 * 2;
-      int rc;
-      if ((rc = d.in_fix.ensure(fix + 1024))) return rc;
-      if ((rc = d.in_sig.ensure(smax - smin + 16))) return rc;
-      if ((rc = d.in_msg.ensure(mmax - mmin + 16))) return rc;
-      if ((rc = d.out.ensure(round64(m) / 8 + m + 1024))) return rc;
-      char* f = (char*)d.in_fix.p;
-      uint8_t* dpub = (uint8_t*)f;
-      uint64_t* dso = (uint64_t*)(f + ((m * 64 + 255) & ~size_t(255)));
-      uint64_t* dmo = dso + m;
-      uint32_t* dsl = (uint32_t*)(dmo + m);
-      uint32_t* dml = dsl + m;
-      uint64_t* dbm = (uint64_t*)d.out.p;
-      uint8_t* drs = (uint8_t*)(dbm + round64(m) / 64);
-      hipStream_t s = d.stream;
-      HIPCHK(hipMemcpyAsync(dpub, b->pub + lo * 64, m * 64, hipMemcpyHostToDevice, s));
-      HIPCHK(hipMemcpyAsync(dso, so.data(), m * 8, hipMemcpyHostToDevice, s));
-      HIPCHK(hipMemcpyAsync(dmo, mo.data(), m * 8, hipMemcpyHostToDevice, s));
-      HIPCHK(hipMemcpyAsync(dsl, b->sig_len + lo, m * 4, hipMemcpyHostToDevice, s));
-      HIPCHK(hipMemcpyAsync(dml, b->msg_len + lo, m * 4, hipMemcpyHostToDevice, s));
-      if (smax > smin)
-        HIPCHK(hipMemcpyAsync(d.in_sig.p, b->sig + smin, smax - smin, hipMemcpyHostToDevice, s));
-      if (mmax > mmin)
-        HIPCHK(hipMemcpyAsync(d.in_msg.p, b->msg + mmin, mmax - mmin, hipMemcpyHostToDevice, s));
-      bh_batch db{dpub, (const uint8_t*)d.in_sig.p, dso, dsl, (const uint8_t*)d.in_msg.p, dmo, dml};
-      rc = run_dev(d, curve, &db, m, flags, dbm, drs, s, nullptr);
-      if (rc) return rc;
-      std::vector<uint64_t> words(round64(m) / 64);
-      HIPCHK(hipMemcpyAsync(words.data(), dbm, words.size() * 8, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipMemcpyAsync(reason + lo, drs, m, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-      // lo is a multiple of 64 -> byte-aligned splice
-      uint8_t* dst = bitmap + lo / 8;
-      const size_t nbytes = (m + 7) / 8;
-      std::memcpy(dst, words.data(), nbytes);
-      return BH_OK;
-    };
-    rcs[k] = body();
-    if (rcs[k]) errs[k] = g_err;
-  };
-  if (nd == 1) {
-    work(0);
-  } else {
-    std::vector<std::thread> th;
-    for (size_t k = 0; k < nd; k++) th.emplace_back(work, k);
-    for (auto& t : th) t.join();
-  }
-  for (size_t k = 0; k < nd; k++)
-    if (rcs[k]) return fail(rcs[k], errs[k]);
-  return BH_OK;
+  if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
+  return host_verify(curve, b, n, flags, bitmap, reason);
 }
 
 int bh_csp_verify_p256(const uint8_t pub[64], const uint8_t* sig, size_t sig_len,
@@ -479,7 +656,9 @@ int bh_memcpy_d2h(int device, void* dst, const void* src, size_t bytes) {
 int bh_sync(int device) {
   Dev* d = get_dev(device);
   if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
+  std::lock_guard<std::mutex> g(d->mu);
   HIPCHK(hipSetDevice(d->id));
+  if (d->done_recorded) HIPCHK(hipEventSynchronize(d->done));
   HIPCHK(hipStreamSynchronize(d->stream));
   return BH_OK;
 }
@@ -492,8 +671,7 @@ int bh_verify_bdls_dev(int device, int curve, const bh_bdls_batch* b, size_t n,
                    !b->s_len || !b->version || !b->msg || !b->msg_off || !b->msg_len ||
                    !bitmap_words || !reason)))
     return fail(BH_E_INVALID, "null pointer in batch");
-  if (curve != BH_CURVE_P256 && curve != BH_CURVE_SECP256K1)
-    return fail(BH_E_INVALID, "unknown curve");
+  if (int rc = check_curve(curve)) return rc;
   if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
   Dev* d = get_dev(device);
   if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
@@ -512,82 +690,81 @@ int bh_verify_bdls(int curve, const bh_bdls_batch* b, size_t n, uint8_t* bitmap,
   if (!b || (n && (!b->xy || !b->r_off || !b->r_len || !b->s_off || !b->s_len || !b->version ||
                    !b->msg_off || !b->msg_len || !bitmap || !reason)))
     return fail(BH_E_INVALID, "null pointer in batch");
-  Dev* d = nullptr;
-  {
-    std::lock_guard<std::mutex> g(g_mu);
-    if (!g_devs.empty()) d = g_devs[0];
-  }
-  if (!d) return fail(BH_E_NOT_INIT, "bh_init not called");
-  std::memset(bitmap, 0, (n + 7) / 8);
-  if (n == 0) return BH_OK;
-  // stage: one contiguous device buffer per host array (BDLS rounds are small)
-  auto span = [&](const uint64_t* off, const uint32_t* len, uint64_t* lo) {
-    uint64_t a = UINT64_MAX, z = 0;
-    for (size_t i = 0; i < n; i++) {
-      a = std::min<uint64_t>(a, off[i]);
-      z = std::max<uint64_t>(z, off[i] + len[i]);
+  if (int rc = check_curve(curve)) return rc;
+  if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
+  return host_verify(curve, b, n, 0u, bitmap, reason);
+}
+
+// ---- key registry ----------------------------------------------------------
+int bh_keys_reserve(int device, int curve, size_t capacity) {
+  if (int rc = check_curve(curve)) return rc;
+  return for_devices(device, [&](Dev& d) { return reg_alloc(d, curve, capacity); });
+}
+
+int bh_keys_register(int device, int curve, const uint8_t* pub, size_t n, uint8_t* status) {
+  if (int rc = check_curve(curve)) return rc;
+  if (n && !pub) return fail(BH_E_INVALID, "null pub");
+  if (status) std::memset(status, 0, n);
+  constexpr size_t kRegChunk = size_t(1) << 16;
+  std::vector<uint8_t> st(std::min(n, kRegChunk));
+  return for_devices(device, [&](Dev& d) -> int {
+    if (d.reg[curve].g.cap == 0) {
+      int rc = reg_alloc(d, curve, kDefaultRegCap);
+      if (rc) return rc;
     }
-    *lo = a;
-    return z - a;
-  };
-  uint64_t rlo, slo, mlo;
-  const uint64_t rsz = span(b->r_off, b->r_len, &rlo), ssz = span(b->s_off, b->s_len, &slo),
-                 msz = span(b->msg_off, b->msg_len, &mlo);
-  std::vector<uint64_t> ro(n), so(n), mo(n);
-  for (size_t i = 0; i < n; i++) {
-    ro[i] = b->r_off[i] - rlo;
-    so[i] = b->s_off[i] - slo;
-    mo[i] = b->msg_off[i] - mlo;
-  }
-  std::vector<void*> bufs;
-  auto cleanup = [&]() {
-    for (void* p : bufs) (void)hipFree(p);
-  };
-  auto up = [&](const void* src, size_t bytes, void** dst) -> int {
-    hipError_t e = hipMalloc(dst, bytes + 16);
-    if (e != hipSuccess) return fail(BH_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
-    bufs.push_back(*dst);
-    if (bytes) {
-      e = hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
-      if (e != hipSuccess) return fail(BH_E_DEVICE, std::string("hipMemcpy: ") + hipGetErrorString(e));
+    for (size_t lo = 0; lo < n; lo += kRegChunk) {
+      const size_t m = std::min(kRegChunk, n - lo);
+      int rc;
+      if ((rc = d.stage.ensure(m * 64 + 256))) return rc;
+      if ((rc = d.out.ensure(m + 256))) return rc;
+      bh::Work w;
+      bh::Plan pl;
+      if ((rc = carve_work(d, m, &w, &pl, true))) return rc;
+      hipStream_t s = d.stream;
+      if (d.done_recorded) HIPCHK(hipEventSynchronize(d.done));
+      HIPCHK(hipMemcpyAsync(d.stage.p, pub + lo * 64, m * 64, hipMemcpyHostToDevice, s));
+      HIPCHK(bh::launch_register(curve, (const uint8_t*)d.stage.p, w, pl, d.reg[curve].g,
+                                 (uint32_t)m, (uint8_t*)d.out.p, s));
+      HIPCHK(hipMemcpyAsync(st.data(), d.out.p, m, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      if (status)
+        for (size_t i = 0; i < m; i++) status[lo + i] = std::max(status[lo + i], st[i]);
     }
     return BH_OK;
-  };
-  std::lock_guard<std::mutex> g(d->mu);
-  HIPCHK(hipSetDevice(d->id));
-  void *dxy, *dr, *ds, *dm, *dro, *dso, *dmo, *drl, *dsl, *dml, *dver, *dbm, *drs;
-  int rc = 0;
-  if (!rc) rc = up(b->xy, n * 64, &dxy);
-  if (!rc) rc = up(b->r ? b->r + rlo : nullptr, b->r ? rsz : 0, &dr);
-  if (!rc) rc = up(b->s ? b->s + slo : nullptr, b->s ? ssz : 0, &ds);
-  if (!rc) rc = up(b->msg ? b->msg + mlo : nullptr, b->msg ? msz : 0, &dm);
-  if (!rc) rc = up(ro.data(), n * 8, &dro);
-  if (!rc) rc = up(so.data(), n * 8, &dso);
-  if (!rc) rc = up(mo.data(), n * 8, &dmo);
-  if (!rc) rc = up(b->r_len, n * 4, &drl);
-  if (!rc) rc = up(b->s_len, n * 4, &dsl);
-  if (!rc) rc = up(b->msg_len, n * 4, &dml);
-  if (!rc) rc = up(b->version, n * 4, &dver);
-  if (!rc) rc = up(nullptr, round64(n) / 8, &dbm);
-  if (!rc) rc = up(nullptr, n, &drs);
-  if (!rc) {
-    bh_bdls_batch db{(const uint8_t*)dxy, (const uint8_t*)dr, (const uint64_t*)dro,
-                     (const uint32_t*)drl, (const uint8_t*)ds, (const uint64_t*)dso,
-                     (const uint32_t*)dsl, (const uint32_t*)dver, (const uint8_t*)dm,
-                     (const uint64_t*)dmo, (const uint32_t*)dml};
-    rc = run_dev(*d, curve, &db, n, 0u, (uint64_t*)dbm, (uint8_t*)drs, d->stream, nullptr);
-  }
-  if (!rc) {
-    std::vector<uint64_t> words(round64(n) / 64);
-    hipError_t e = hipStreamSynchronize(d->stream);
-    if (e == hipSuccess) e = hipMemcpy(words.data(), dbm, words.size() * 8, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(reason, drs, n, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) rc = fail(BH_E_DEVICE, std::string("hipMemcpy: ") + hipGetErrorString(e));
-    else std::memcpy(bitmap, words.data(), (n + 7) / 8);
-  }
-  cleanup();
-  return rc;
+  });
+}
+
+int bh_keys_clear(int device, int curve) {
+  if (int rc = check_curve(curve)) return rc;
+  return for_devices(device, [&](Dev& d) -> int {
+    const bh::KeyReg& g = d.reg[curve].g;
+    if (g.cap == 0) return BH_OK;
+    if (d.done_recorded) HIPCHK(hipEventSynchronize(d.done));
+    HIPCHK(hipMemsetAsync(g.slot_hash, 0, (size_t)g.hc * 8, d.stream));
+    HIPCHK(hipMemsetAsync(g.count, 0, 4, d.stream));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    return BH_OK;
+  });
+}
+
+int bh_keys_count(int device, int curve, size_t* count) {
+  if (int rc = check_curve(curve)) return rc;
+  if (!count) return fail(BH_E_INVALID, "null count");
+  *count = 0;
+  bool first = true;
+  return for_devices(device, [&](Dev& d) -> int {
+    const bh::KeyReg& g = d.reg[curve].g;
+    size_t c = 0;
+    if (g.cap) {
+      if (d.done_recorded) HIPCHK(hipEventSynchronize(d.done));
+      uint32_t v = 0;
+      HIPCHK(hipMemcpy(&v, g.count, 4, hipMemcpyDeviceToHost));
+      c = std::min<size_t>(v, g.cap);
+    }
+    *count = first ? c : std::min(*count, c);  // -1: keys present on every device
+    first = false;
+    return BH_OK;
+  });
 }
 
 }  // extern "C"
-

@@ -86,11 +86,22 @@ struct Plan {
   uint32_t* rec_slot;   // [ns] slot or kNone
   uint32_t* comb_list;  // [ns] records on the key-comb path
   uint32_t* ladder_list;  // [ns] records on the variable-base ladder path
-  uint32_t* counters;   // [0] n_comb, [1] n_ladder, [2] n_tables
+  uint32_t* counters;   // [0] n_comb, [1] n_ladder, [2] table builds
+  uint32_t* rec_tab;    // [ns] table id of the record's key (kNone: ladder)
   uint32_t* tab_rec;    // [max_tables] record whose Q builds the table
-  uint32_t* tables;     // [max_tables][kKWin][kKEnt][kQPt]
+  uint32_t* tab_dst;    // [max_tables] table id the build writes
+  uint32_t* tables;     // [max_tables][kKWin][kKEnt][kQPt]  per-batch tables
 };
 constexpr uint32_t kNone = 0xffffffffu;
+
+// Per-launch choices made on the host (bdls_hip.cpp run_dev).
+struct LaunchOpts {
+  uint32_t inv_chunk;  // records per batch-inversion lane
+  uint32_t min_uses;   // key-table threshold (uses of one key in the batch)
+  uint32_t min_batch;  // no per-batch tables below this batch size
+  bool keep;           // BH_F_KEEP_KEYS: new tables go to the key registry
+  int wide;            // lanes per record on the key-table path (1, 4, 16)
+};
 
 // G comb table: window w in [0, 33), entry j in [0, 128): (j+1) * 2^(8w) * G,
 // affine, canonical radix-2^30 Montgomery x (limbs 0..8) and y (limbs 9..17),
@@ -119,10 +130,29 @@ BH_HD void st9(uint32_t* base, uint32_t i, uint32_t ns, const uint32_t v[9]) {
 }
 
 // ------------------------------------------------------------------ prep
+// Public key bytes X || Y (32 B big-endian each) -> canonical radix-2^30
+// Montgomery coordinates; false unless 0 <= X, Y < p and Y^2 = X^3 + aX + b
+// (Go pointFromAffine, crypto/ecdsa verifyNISTEC).
+template <class P, class C>
+BH_HD bool key_import(const uint8_t* q, uint32_t qx30[9], uint32_t qy30[9]) {
+  uint32_t qx[8], qy[8], pp[8];
+  load_const8(pp, C::p);
+  be32_to_limbs(qx, q);
+  be32_to_limbs(qy, q + 32);
+  if (geq8(qx, pp) || geq8(qy, pp)) return false;
+  f_from_u256(qx30, qx);
+  f_from_u256(qy30, qy);
+  f_to_mont<P>(qx30, qx30);
+  f_to_mont<P>(qy30, qy30);
+  f_canon<P>(qx30, qx30);
+  f_canon<P>(qy30, qy30);
+  return j_on_curve<P>(qx30, qy30);
+}
+
 template <class P, class N, class C>
 BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
   uint8_t reason = R_OK;
-  uint32_t r[8], s[8], e[8], qx[8], qy[8];
+  uint32_t r[8], s[8], e[8];
   uint32_t qx30[9], qy30[9];
   const uint32_t slen = in.sig_len[i];
   const uint32_t mlen = in.msg_len[i];
@@ -133,10 +163,9 @@ BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
   else if (!fused && mlen == 0) reason = R_EMPTY_DIGEST;
   DerSig ds;
   if (reason == R_OK) reason = der_parse_sig(in.sig + in.sig_off[i], slen, &ds);
-  uint32_t half[8], nn[8], pp[8];
+  uint32_t half[8], nn[8];
   load_const8(half, C::half_n);
   load_const8(nn, C::n);
-  load_const8(pp, C::p);
   if (reason == R_OK) {
     copy8(r, ds.r);
     copy8(s, ds.s);
@@ -144,22 +173,8 @@ BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
     if (!(in.flags & BHF_NO_LOW_S) && (ds.s_big || !geq8(half, s))) reason = R_HIGH_S;
   }
   // ---- inside crypto/ecdsa.Verify (verifyNISTEC): Q first, then r, s ranges
-  const uint8_t* q = in.pub + (size_t)i * 64;
-  be32_to_limbs(qx, q);
-  be32_to_limbs(qy, q + 32);
-  if (reason == R_OK) {
-    if (geq8(qx, pp) || geq8(qy, pp)) {
-      reason = R_BAD_KEY;
-    } else {
-      f_from_u256(qx30, qx);
-      f_from_u256(qy30, qy);
-      f_to_mont<P>(qx30, qx30);
-      f_to_mont<P>(qy30, qy30);
-      f_canon<P>(qx30, qx30);
-      f_canon<P>(qy30, qy30);
-      if (!j_on_curve<P>(qx30, qy30)) reason = R_BAD_KEY;
-    }
-  }
+  if (reason == R_OK && !key_import<P, C>(in.pub + (size_t)i * 64, qx30, qy30))
+    reason = R_BAD_KEY;
   if (reason == R_OK && (ds.r_big || geq8(r, nn))) reason = R_R_RANGE;
   if (reason == R_OK && (ds.s_big || geq8(s, nn))) reason = R_S_RANGE;
   // ---- digest -> e (hashToNat: left-most 32 bytes, reduced mod n)
@@ -250,31 +265,16 @@ BH_HD void setbytes_u256(const uint8_t* b, uint32_t len, uint32_t v[8], bool* bi
 template <class P, class N, class C>
 BH_HD void stage_prep(const BdlsIn& in, const Work& w, uint32_t i) {
   uint8_t reason = R_OK;
-  uint32_t r[8], s[8], e[8], qx[8], qy[8], nn[8], pp[8];
+  uint32_t r[8], s[8], e[8], nn[8];
   uint32_t qx30[9], qy30[9];
   load_const8(nn, C::n);
-  load_const8(pp, C::p);
   bool rbig, rzero, sbig, szero;
   setbytes_u256(in.r + in.r_off[i], in.r_len[i], r, &rbig, &rzero);
   setbytes_u256(in.s + in.s_off[i], in.s_len[i], s, &sbig, &szero);
   if (rzero) reason = R_R_NONPOS;       // ecdsa.Verify: r.Sign() <= 0
   else if (szero) reason = R_S_NONPOS;
   const uint8_t* q = in.xy + (size_t)i * 64;
-  be32_to_limbs(qx, q);
-  be32_to_limbs(qy, q + 32);
-  if (reason == R_OK) {
-    if (geq8(qx, pp) || geq8(qy, pp)) {
-      reason = R_BAD_KEY;
-    } else {
-      f_from_u256(qx30, qx);
-      f_from_u256(qy30, qy);
-      f_to_mont<P>(qx30, qx30);
-      f_to_mont<P>(qy30, qy30);
-      f_canon<P>(qx30, qx30);
-      f_canon<P>(qy30, qy30);
-      if (!j_on_curve<P>(qx30, qy30)) reason = R_BAD_KEY;
-    }
-  }
+  if (reason == R_OK && !key_import<P, C>(q, qx30, qy30)) reason = R_BAD_KEY;
   if (reason == R_OK && (rbig || geq8(r, nn))) reason = R_R_RANGE;
   if (reason == R_OK && (sbig || geq8(s, nn))) reason = R_S_RANGE;
   if (reason == R_OK) {
@@ -782,6 +782,224 @@ BH_HD bool same_key(const Work& w, uint32_t a, uint32_t b) {
     d |= w.qy[(size_t)k * w.ns + a] ^ w.qy[(size_t)k * w.ns + b];
   }
   return d == 0;
+}
+
+
+// ------------------------------------------------------------ key registry
+// Persistent per-device, per-curve store of key tables (include/bdls_hip.h
+// bh_keys_register / BH_F_KEEP_KEYS): an open-addressed fingerprint table ->
+// table index, the canonical Montgomery key per table (full compare on every
+// hit) and the tables themselves (kKTabWords words each, same layout as the
+// per-batch tables). Entries are only added (bh_keys_clear resets), and a
+// fingerprint slot is published only after its table is complete.
+struct KeyReg {
+  uint32_t cap;         // tables (0 = registry not allocated)
+  uint32_t hc;          // fingerprint slots (power of two >= 2 cap)
+  uint64_t* slot_hash;  // [hc] 0 = empty
+  uint32_t* slot_tab;   // [hc]
+  uint32_t* keys;       // [cap][18] qx || qy (canonical radix-2^30 Montgomery)
+  uint32_t* tables;     // [cap][kKTabWords]
+  uint32_t* count;      // [1] tables handed out (may exceed cap; clamp on read)
+};
+
+// Table ids: registry index, or kLocal | per-batch plan index.
+constexpr uint32_t kLocal = 0x80000000u;
+
+BH_HD const uint32_t* tab_ptr(const Plan& pl, const KeyReg& g, uint32_t id) {
+  return (id & kLocal) ? pl.tables + (size_t)(id & ~kLocal) * kKTabWords
+                       : g.tables + (size_t)id * kKTabWords;
+}
+
+BH_HD bool reg_key_eq(const KeyReg& g, uint32_t t, const Work& w, uint32_t i) {
+  const uint32_t* k = g.keys + (size_t)t * 18;
+  uint32_t d = 0;
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    d |= k[q] ^ w.qx[(size_t)q * w.ns + i];
+    d |= k[9 + q] ^ w.qy[(size_t)q * w.ns + i];
+  }
+  return d == 0;
+}
+
+BH_HD void reg_key_store(const KeyReg& g, uint32_t t, const Work& w, uint32_t i) {
+  uint32_t* k = g.keys + (size_t)t * 18;
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    k[q] = w.qx[(size_t)q * w.ns + i];
+    k[9 + q] = w.qy[(size_t)q * w.ns + i];
+  }
+}
+
+// Registry table for record i's key, or kNone.
+BH_HD uint32_t reg_lookup(const KeyReg& g, const Work& w, uint32_t i, uint64_t h) {
+  if (g.cap == 0) return kNone;
+  const uint32_t mask = g.hc - 1;
+  uint32_t p = (uint32_t)h & mask;
+  for (uint32_t probe = 0; probe < g.hc; probe++) {
+    const uint64_t cur = g.slot_hash[p];
+    if (cur == 0) return kNone;
+    if (cur == h) {
+      const uint32_t t = g.slot_tab[p];
+      if (t < g.cap && reg_key_eq(g, t, w, i)) return t;
+    }
+    p = (p + 1) & mask;
+  }
+  return kNone;
+}
+
+// ------------------------------------------------------- wide key comb
+// For batches far smaller than the chip (block validation, one BDLS round),
+// L lanes share one record: lane l of the group adds the key-table windows
+// win = l, l + L, ... and the G-comb windows likewise, then the L partial
+// sums are combined by a butterfly over the group. The signed digits come
+// from one addition instead of a carry scan: with M = sum 8 * 16^w the
+// nibbles of k + M minus 8 are the digits of k in [-8, 7] (and with 128 *
+// 256^w, bytes minus 128 in [-128, 127]), so every lane reads its windows
+// directly. Same point as q_keycomb / g_comb (different digits, same sum).
+
+// v (288-bit, 9 limbs) = k + M, M = pattern in every limb of the low 256 bits
+// plus `top` at bit 256 (the top window's offset).
+BH_HD void recode_offset(uint32_t v[9], const uint32_t k[8], uint32_t pattern, uint32_t top) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    c += (uint64_t)k[q] + pattern;
+    v[q] = (uint32_t)c;
+    c >>= 32;
+  }
+  v[8] = (uint32_t)c + top;
+}
+
+// o = v >> sh (288-bit), 0 <= sh < 128
+BH_HD void shr288(uint32_t o[9], const uint32_t v[9], uint32_t sh) {
+  const uint32_t ws = sh >> 5, bs = sh & 31u;
+  uint32_t t[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    uint32_t x = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 4; d++)
+      if (ws == d) x = (q + (int)d < 9) ? v[q + d] : 0u;
+    t[q] = x;
+  }
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    const uint32_t hi = (q + 1 < 9) ? t[q + 1] : 0u;
+    o[q] = bs ? ((t[q] >> bs) | (hi << (32 - bs))) : t[q];
+  }
+}
+
+// v >>= B (288-bit, compile-time B < 288)
+template <int B>
+BH_HD void shr_const(uint32_t v[9]) {
+  constexpr int ws = B / 32, bs = B % 32;
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    const uint32_t lo = (q + ws < 9) ? v[q + ws] : 0u;
+    const uint32_t hi = (q + ws + 1 < 9) ? v[q + ws + 1] : 0u;
+    v[q] = bs ? ((lo >> bs) | (hi << (32 - bs))) : lo;
+  }
+}
+
+// Acc += T (Jacobian), with infinity flags and the explicit degenerate cases.
+template <class P>
+BH_HD void j_acc(J30& A, bool& a_inf, const J30& T, bool t_inf) {
+  J30 R;
+  bool same;
+  const bool deg = j_add<P>(R, A, T, &same);
+  const bool take = !t_inf;
+  const bool use_t = take && a_inf;
+  const bool use_r = take && !a_inf && !deg;
+  const bool rare = take && !a_inf && deg;
+  j_sel(A, use_r, R, A);
+  j_sel(A, use_t, T, A);
+  if (rare) {
+    if (same) j_dbl<P>(A, T);
+    else a_inf = true;
+  }
+  if (use_t) a_inf = false;
+}
+
+// Acc += (tx, ty) affine (mixed addition).
+template <class P>
+BH_HD void j_acc_aff(J30& A, bool& a_inf, const uint32_t tx[9], const uint32_t ty[9],
+                     const uint32_t one[9], bool t_inf) {
+  J30 R;
+  bool same;
+  const bool deg = j_madd<P>(R, A, tx, ty, &same);
+  const bool take = !t_inf;
+  const bool use_t = take && a_inf;
+  const bool use_r = take && !a_inf && !deg;
+  const bool rare = take && !a_inf && deg;
+  j_sel(A, use_r, R, A);
+  if (use_t) {
+    f_copy(A.X, tx);
+    f_copy(A.Y, ty);
+    f_copy(A.Z, one);
+  }
+  if (rare) {
+    if (same) {
+      J30 T;
+      f_copy(T.X, tx);
+      f_copy(T.Y, ty);
+      f_copy(T.Z, one);
+      j_dbl<P>(A, T);
+    } else {
+      a_inf = true;
+    }
+  }
+  if (use_t) a_inf = false;
+}
+
+// Lane l's partial sum C = sum over its windows of (key-table digit points
+// + G-comb digit points).
+template <class P, int L>
+BH_HD void keycomb_part(J30& C, bool& c_inf, const Work& w, const uint32_t* gtab, uint32_t i,
+                        const uint32_t* tab, uint32_t l) {
+  uint32_t k[8], v[9], sv[9];
+  f_const(C.X, P::r1);
+  f_const(C.Y, P::r1);
+  f_const(C.Z, P::r1);
+  c_inf = true;
+  // u2 Q: 4-bit windows win = l + m L
+  ld8(k, w.r, i, w.ns);
+  recode_offset(v, k, 0x88888888u, 0x8u);
+  shr288(sv, v, 4u * l);
+  for (int m = 0; m * L < kKWin; m++) {
+    const uint32_t win = l + (uint32_t)(m * L);
+    const int d = (int)(sv[0] & 0xfu) - 8;
+    shr_const<4 * L>(sv);
+    if (win < (uint32_t)kKWin) {
+      const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+      J30 T;
+      ktab_load(T, tab, win, mag ? mag - 1 : 0);
+      if (d < 0) f_neg<P, 64>(T.Y, T.Y);
+      j_acc<P>(C, c_inf, T, mag == 0);
+    }
+  }
+  // u1 G: 8-bit windows win = l + m L over the affine G comb
+  ld8(k, w.e, i, w.ns);
+  recode_offset(v, k, 0x80808080u, 0x80u);
+  shr288(sv, v, 8u * l);
+  uint32_t one[9];
+  f_const(one, P::r1);
+  for (int m = 0; m * L < kCombWindows; m++) {
+    const uint32_t win = l + (uint32_t)(m * L);
+    const int d = (int)(sv[0] & 0xffu) - 128;
+    shr_const<8 * L>(sv);
+    if (win < (uint32_t)kCombWindows) {
+      const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+      const uint32_t* te = gtab + ((size_t)win * kCombEntries + (mag ? mag - 1 : 0)) * kGEntry;
+      uint32_t tx[9], ty[9];
+#pragma unroll
+      for (int q = 0; q < 9; q++) {
+        tx[q] = te[q];
+        ty[q] = te[9 + q];
+      }
+      if (d < 0) f_neg<P, 64>(ty, ty);
+      j_acc_aff<P>(C, c_inf, tx, ty, one, mag == 0);
+    }
+  }
 }
 
 }  // namespace bh

@@ -4,13 +4,21 @@
 //   k_prep        1 lane/record   parse / checks / SHA-256 / Montgomery inputs
 //   k_inv         1 lane/chunk    batched s^-1 mod n, u1, u2
 //   k_key_insert / k_key_count / k_key_plan / k_split
-//                 1 lane/record   dedup public keys, pick keys used >= kMinUses
+//                 1 lane/record   registry lookup, dedup of the other keys,
+//                                 per-batch tables for keys used >= min_uses
 //                                 times, route records to the two paths
-//   k_ktab_build  1 lane/key      per-key fixed-base table (65 x 8 points)
+//   k_ktab_ladder 1 lane/key + 1 lane/record
+//                                 key-table builds and, in the same grid, the
+//                                 variable-base ladder for records without a
+//                                 table (independent work: the ladder fills
+//                                 the issue slots the latency-bound builds
+//                                 leave idle)
+//   k_reg_publish 1 lane/build    make new registry tables visible
 //   k_keycomb     1 lane/record   u2 Q by table additions (no doublings) + u1 G
-//   k_ladder      1 lane/record   u2 Q by Booth-5 ladder + u1 G (unique keys)
+//   k_keycomb_wide<L>  L lanes/record, for batches far below chip size
 //   k_bitmap      1 lane/record   validity bitmap from the reason bytes
-// plus k_gtab_build once per device at bh_init (fixed-base comb table for G).
+// plus k_gtab_build once per device at bh_init (fixed-base comb table for G)
+// and k_reg_prep / k_reg_status for bh_keys_register.
 #include "verify.h"
 
 using namespace bh;
@@ -33,15 +41,24 @@ __global__ __launch_bounds__(256) void k_inv(Work w, uint32_t n, uint32_t chunk)
   stage_inv<N>(w, (uint32_t)lo, (uint32_t)hi);
 }
 
-// ---- key dedup / plan ------------------------------------------------------
-__global__ __launch_bounds__(256) void k_key_insert(Work w, Plan pl, uint32_t n) {
+// ---- key lookup / dedup / plan ----------------------------------------------
+// Registry hit -> rec_tab; otherwise insert the fingerprint into the batch's
+// dedup table (smallest record index becomes the slot's representative).
+__global__ __launch_bounds__(256) void k_key_insert(Work w, Plan pl, KeyReg g, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  pl.rec_tab[i] = kNone;
   if ((w.st[i] & 0x7fu) != R_OK) {
     pl.rec_slot[i] = kNone;
     return;
   }
   const uint64_t h = key_hash(w, i);
+  const uint32_t t = reg_lookup(g, w, i, h);
+  if (t != kNone) {
+    pl.rec_tab[i] = t;
+    pl.rec_slot[i] = kNone;
+    return;
+  }
   const uint32_t mask = pl.hc - 1;
   uint32_t p = (uint32_t)h & mask;
   for (uint32_t probe = 0; probe < pl.hc; probe++) {
@@ -72,16 +89,32 @@ __global__ __launch_bounds__(256) void k_key_count(Work w, Plan pl, uint32_t n) 
   }
 }
 
-__global__ __launch_bounds__(256) void k_key_plan(Plan pl, uint32_t n) {
+// One table build per representative whose key is used >= min_uses times (in
+// batches of >= min_batch records). keep: the table goes to the registry
+// while it has room, else to the batch. reg_only: registry or nothing
+// (bh_keys_register).
+__global__ __launch_bounds__(256) void k_key_plan(Work w, Plan pl, KeyReg g, uint32_t n,
+                                                  uint32_t min_uses, uint32_t min_batch,
+                                                  uint32_t keep, uint32_t reg_only) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || n < kKeyTableMinBatch) return;
+  if (i >= n || n < min_batch) return;
   const uint32_t p = pl.rec_slot[i];
-  if (p == kNone || pl.slot_rep[p] != i || pl.slot_cnt[p] < kMinUses) return;
-  const uint32_t t = atomicAdd(&pl.counters[2], 1u);
-  if (t < pl.max_tables) {
-    pl.slot_tab[p] = t;
-    pl.tab_rec[t] = i;
+  if (p == kNone || pl.slot_rep[p] != i || pl.slot_cnt[p] < min_uses) return;
+  uint32_t id = kNone;
+  if (keep && g.cap) {
+    const uint32_t r = atomicAdd(g.count, 1u);
+    if (r < g.cap) {
+      id = r;
+      reg_key_store(g, r, w, i);
+    }
   }
+  if (id == kNone && reg_only) return;
+  const uint32_t job = atomicAdd(&pl.counters[2], 1u);
+  if (job >= pl.max_tables) return;  // registry slot (if any) stays unpublished
+  if (id == kNone) id = kLocal | job;
+  pl.slot_tab[p] = id;
+  pl.tab_rec[job] = i;
+  pl.tab_dst[job] = id;
 }
 
 // Route every record: failed prep -> reason now; key table -> comb list;
@@ -95,38 +128,32 @@ __global__ __launch_bounds__(256) void k_split(Work w, Plan pl, uint32_t n,
     reason[i] = st;
     return;
   }
-  const uint32_t p = pl.rec_slot[i];
-  const uint32_t t = (p == kNone) ? kNone : pl.slot_tab[p];
+  uint32_t t = pl.rec_tab[i];
+  if (t == kNone) {
+    const uint32_t p = pl.rec_slot[i];
+    if (p != kNone) t = pl.slot_tab[p];
+    pl.rec_tab[i] = t;
+  }
   if (t != kNone) pl.comb_list[atomicAdd(&pl.counters[0], 1u)] = i;
   else pl.ladder_list[atomicAdd(&pl.counters[1], 1u)] = i;
 }
 
+// Blocks [0, tab_blocks) build key tables (one lane per table); the rest run
+// the ladder list. Ladder waves past the list length exit whole (the Q-table
+// scratch slot is the list position).
 template <class P>
-__global__ __launch_bounds__(64) void k_ktab_build(Work w, Plan pl) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t nt = min(pl.counters[2], pl.max_tables);
-  if (t >= nt) return;
-  ktab_build<P>(pl.tables + (size_t)t * kKTabWords, w, pl.tab_rec[t]);
-}
-
-template <class P>
-__global__ __launch_bounds__(256) void k_keycomb(Work w, Plan pl, const uint32_t* __restrict__ gtab,
-                                                 uint8_t* __restrict__ reason) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t cnt = pl.counters[0];
-  if (j >= cnt) return;
-  const uint32_t i = pl.comb_list[j];
-  const uint32_t t = pl.slot_tab[pl.rec_slot[i]];
-  const bool ok = stage_keycomb<P>(w, gtab, i, pl.tables + (size_t)t * kKTabWords);
-  reason[i] = ok ? R_OK : R_MATH;
-}
-
-// Variable-base path over the ladder list; the Q-table scratch slot is the
-// list position, so whole waves past the list length exit.
-template <class P>
-__global__ __launch_bounds__(256) void k_ladder(Work w, Plan pl, const uint32_t* __restrict__ gtab,
-                                                uint8_t* __restrict__ reason) {
-  const uint32_t j0 = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
+                                                     const uint32_t* __restrict__ gtab,
+                                                     uint8_t* __restrict__ reason,
+                                                     uint32_t tab_blocks) {
+  if (blockIdx.x < tab_blocks) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nt = min(pl.counters[2], pl.max_tables);
+    if (t >= nt) return;
+    ktab_build<P>(const_cast<uint32_t*>(tab_ptr(pl, g, pl.tab_dst[t])), w, pl.tab_rec[t]);
+    return;
+  }
+  const uint32_t j0 = (blockIdx.x - tab_blocks) * blockDim.x + threadIdx.x;
   const uint32_t cnt = pl.counters[1];
   if ((j0 & ~63u) >= cnt) return;
   const bool active = j0 < cnt;
@@ -134,6 +161,65 @@ __global__ __launch_bounds__(256) void k_ladder(Work w, Plan pl, const uint32_t*
   const uint32_t i = pl.ladder_list[j];
   const bool ok = stage_ladder<P>(w, gtab, i, j0 >> 6, threadIdx.x & 63u);
   if (active) reason[i] = ok ? R_OK : R_MATH;
+}
+
+// Publish registry tables built in this batch (after the builds completed).
+__global__ __launch_bounds__(256) void k_reg_publish(Work w, Plan pl, KeyReg g) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nt = min(pl.counters[2], pl.max_tables);
+  if (t >= nt) return;
+  const uint32_t id = pl.tab_dst[t];
+  if (id & kLocal) return;
+  const uint64_t h = key_hash(w, pl.tab_rec[t]);
+  const uint32_t mask = g.hc - 1;
+  uint32_t p = (uint32_t)h & mask;
+  for (uint32_t probe = 0; probe < g.hc; probe++) {
+    if (atomicCAS((unsigned long long*)&g.slot_hash[p], 0ull, (unsigned long long)h) == 0ull) {
+      g.slot_tab[p] = id;
+      return;
+    }
+    p = (p + 1) & mask;
+  }
+}
+
+template <class P>
+__global__ __launch_bounds__(256) void k_keycomb(Work w, Plan pl, KeyReg g,
+                                                 const uint32_t* __restrict__ gtab,
+                                                 uint8_t* __restrict__ reason) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t cnt = pl.counters[0];
+  if (j >= cnt) return;
+  const uint32_t i = pl.comb_list[j];
+  const bool ok = stage_keycomb<P>(w, gtab, i, tab_ptr(pl, g, pl.rec_tab[i]));
+  reason[i] = ok ? R_OK : R_MATH;
+}
+
+// L lanes per record (a group of L adjacent lanes of one wave): partial sums
+// over interleaved windows, butterfly over the group, lane 0 checks.
+template <class P, int L>
+__global__ __launch_bounds__(256) void k_keycomb_wide(Work w, Plan pl, KeyReg g,
+                                                      const uint32_t* __restrict__ gtab,
+                                                      uint8_t* __restrict__ reason) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j = gid / L, l = gid % L;
+  const uint32_t cnt = pl.counters[0];
+  if (j >= cnt) return;  // whole groups exit together
+  const uint32_t i = pl.comb_list[j];
+  J30 C;
+  bool c_inf;
+  keycomb_part<P, L>(C, c_inf, w, gtab, i, tab_ptr(pl, g, pl.rec_tab[i]), l);
+  for (int off = 1; off < L; off <<= 1) {
+    J30 T;
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+      T.X[q] = __shfl_xor(C.X[q], off, 64);
+      T.Y[q] = __shfl_xor(C.Y[q], off, 64);
+      T.Z[q] = __shfl_xor(C.Z[q], off, 64);
+    }
+    const bool t_inf = __shfl_xor((int)c_inf, off, 64) != 0;
+    j_acc<P>(C, c_inf, T, t_inf);
+  }
+  if (l == 0) reason[i] = finish_check<P>(w, i, C, c_inf, C, true) ? R_OK : R_MATH;
 }
 
 __global__ __launch_bounds__(256) void k_bitmap(const uint8_t* __restrict__ reason, uint32_t n,
@@ -153,6 +239,37 @@ __global__ __launch_bounds__(64) void k_gtab_build(uint32_t* gtab) {
   gtab_entry<P>(t, gtab + (size_t)t * kGEntry);
 }
 
+// bh_keys_register: keys only (X || Y per record) -> Work.qx / qy / st.
+template <class P, class C>
+__global__ __launch_bounds__(256) void k_reg_prep(const uint8_t* __restrict__ pub, Work w,
+                                                  uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t qx[9], qy[9];
+  const bool ok = key_import<P, C>(pub + (size_t)i * 64, qx, qy);
+  if (!ok) {
+    f_const(qx, P::gx_m);
+    f_const(qy, P::gy_m);
+  }
+  st9(w.qx, i, w.ns, qx);
+  st9(w.qy, i, w.ns, qy);
+  w.st[i] = ok ? R_OK : R_BAD_KEY;
+}
+
+// Per key: 0 = in the registry (new or already), R_BAD_KEY, or kRegFull.
+__global__ __launch_bounds__(256) void k_reg_status(Work w, Plan pl, uint32_t n,
+                                                    uint8_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if ((w.st[i] & 0x7fu) != R_OK) {
+    status[i] = R_BAD_KEY;
+    return;
+  }
+  uint32_t t = pl.rec_tab[i];
+  if (t == kNone && pl.rec_slot[i] != kNone) t = pl.slot_tab[pl.rec_slot[i]];
+  status[i] = (t != kNone && !(t & kLocal)) ? 0 : 0xffu;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -169,42 +286,60 @@ hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Full launch sequence. ev (optional, 6 events) brackets: prep | inv | plan
-// (dedup + split) | key tables | key comb | ladder+bitmap.
+static hipError_t plan_reset(const Plan& pl, hipStream_t s) {
+  hipError_t e;
+  if ((e = hipMemsetAsync(pl.slot_hash, 0, (size_t)pl.hc * 8, s))) return e;
+  if ((e = hipMemsetAsync(pl.slot_rep, 0xff, (size_t)pl.hc * 4, s))) return e;
+  if ((e = hipMemsetAsync(pl.slot_cnt, 0, (size_t)pl.hc * 4, s))) return e;
+  if ((e = hipMemsetAsync(pl.slot_tab, 0xff, (size_t)pl.hc * 4, s))) return e;
+  return hipMemsetAsync(pl.counters, 0, 16, s);
+}
+
+// Full launch sequence. ev (optional, 7 events) brackets: prep | inv | plan
+// (lookup + dedup + split) | key tables + ladder | publish | key comb + bitmap.
 template <class P, class N, class C, class IN>
-static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const uint32_t* gtab,
-                      uint32_t n, uint32_t chunk, uint64_t* bitmap, uint8_t* reason, hipStream_t s,
-                      hipEvent_t* ev) {
+static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg& g,
+                      const uint32_t* gtab, uint32_t n, const LaunchOpts& o, uint64_t* bitmap,
+                      uint8_t* reason, hipStream_t s, hipEvent_t* ev) {
   const dim3 blk(256);
   const dim3 grd((n + 255) / 256);
-  const uint32_t nchunks = (n + chunk - 1) / chunk;
+  const uint32_t nchunks = (n + o.inv_chunk - 1) / o.inv_chunk;
   const dim3 grc((nchunks + 255) / 256);
   hipError_t e;
 #define REC(k)                                                 \
   if (ev) {                                                    \
     if ((e = hipEventRecord(ev[k], s)) != hipSuccess) return e; \
   }
-  if ((e = hipMemsetAsync(pl.slot_hash, 0, (size_t)pl.hc * 8, s))) return e;
-  if ((e = hipMemsetAsync(pl.slot_rep, 0xff, (size_t)pl.hc * 4, s))) return e;
-  if ((e = hipMemsetAsync(pl.slot_cnt, 0, (size_t)pl.hc * 4, s))) return e;
-  if ((e = hipMemsetAsync(pl.slot_tab, 0xff, (size_t)pl.hc * 4, s))) return e;
-  if ((e = hipMemsetAsync(pl.counters, 0, 16, s))) return e;
+  if ((e = plan_reset(pl, s))) return e;
   REC(0);
   hipLaunchKernelGGL((k_prep<P, N, C, IN>), grd, blk, 0, s, in, w, n);
   REC(1);
-  hipLaunchKernelGGL((k_inv<N>), grc, blk, 0, s, w, n, chunk);
+  hipLaunchKernelGGL((k_inv<N>), grc, blk, 0, s, w, n, o.inv_chunk);
   REC(2);
-  hipLaunchKernelGGL(k_key_insert, grd, blk, 0, s, w, pl, n);
+  hipLaunchKernelGGL(k_key_insert, grd, blk, 0, s, w, pl, g, n);
   hipLaunchKernelGGL(k_key_count, grd, blk, 0, s, w, pl, n);
-  hipLaunchKernelGGL(k_key_plan, grd, blk, 0, s, pl, n);
+  hipLaunchKernelGGL(k_key_plan, grd, blk, 0, s, w, pl, g, n, o.min_uses, o.min_batch,
+                     o.keep ? 1u : 0u, 0u);
   hipLaunchKernelGGL(k_split, grd, blk, 0, s, w, pl, n, reason);
   REC(3);
-  const uint32_t mt = pl.max_tables ? pl.max_tables : 1;
-  hipLaunchKernelGGL((k_ktab_build<P>), dim3((mt + 63) / 64), dim3(64), 0, s, w, pl);
+  const uint32_t tab_blocks = (pl.max_tables + 255) / 256;
+  hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x), blk, 0, s, w, pl, g, gtab,
+                     reason, tab_blocks);
   REC(4);
-  hipLaunchKernelGGL((k_keycomb<P>), grd, blk, 0, s, w, pl, gtab, reason);
+  if (o.keep) hipLaunchKernelGGL(k_reg_publish, dim3(tab_blocks), blk, 0, s, w, pl, g);
   REC(5);
-  hipLaunchKernelGGL((k_ladder<P>), grd, blk, 0, s, w, pl, gtab, reason);
+  switch (o.wide) {
+    case 4:
+      hipLaunchKernelGGL((k_keycomb_wide<P, 4>), dim3((n * 4 + 255) / 256), blk, 0, s, w, pl, g,
+                         gtab, reason);
+      break;
+    case 16:
+      hipLaunchKernelGGL((k_keycomb_wide<P, 16>), dim3((n * 16 + 255) / 256), blk, 0, s, w, pl,
+                         g, gtab, reason);
+      break;
+    default:
+      hipLaunchKernelGGL((k_keycomb<P>), grd, blk, 0, s, w, pl, g, gtab, reason);
+  }
   hipLaunchKernelGGL(k_bitmap, grd, blk, 0, s, reason, n, bitmap);
   REC(6);
 #undef REC
@@ -212,20 +347,48 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const uint32_
 }
 
 hipError_t launch_verify(int curve, const BatchIn& in, const Work& w, const Plan& pl,
-                         const uint32_t* gtab, uint32_t n, uint32_t chunk, uint64_t* bitmap,
-                         uint8_t* reason, hipStream_t s, hipEvent_t* ev) {
+                         const KeyReg& g, const uint32_t* gtab, uint32_t n, const LaunchOpts& o,
+                         uint64_t* bitmap, uint8_t* reason, hipStream_t s, hipEvent_t* ev) {
   // Fabric / BCCSP records: P-256 only (the low-S table of bccsp/utils covers
   // the NIST curves; secp256k1 never reaches bccsp/sw).
   if (curve != 0) return hipErrorInvalidValue;
-  return seq<F30_p256, Fn_p256, Cv_p256>(in, w, pl, gtab, n, chunk, bitmap, reason, s, ev);
+  return seq<F30_p256, Fn_p256, Cv_p256>(in, w, pl, g, gtab, n, o, bitmap, reason, s, ev);
 }
 
 hipError_t launch_verify_bdls(int curve, const BdlsIn& in, const Work& w, const Plan& pl,
-                              const uint32_t* gtab, uint32_t n, uint32_t chunk, uint64_t* bitmap,
-                              uint8_t* reason, hipStream_t s, hipEvent_t* ev) {
+                              const KeyReg& g, const uint32_t* gtab, uint32_t n,
+                              const LaunchOpts& o, uint64_t* bitmap, uint8_t* reason,
+                              hipStream_t s, hipEvent_t* ev) {
   if (curve == 0)
-    return seq<F30_p256, Fn_p256, Cv_p256>(in, w, pl, gtab, n, chunk, bitmap, reason, s, ev);
-  return seq<F30_k1, Fn_k1, Cv_k1>(in, w, pl, gtab, n, chunk, bitmap, reason, s, ev);
+    return seq<F30_p256, Fn_p256, Cv_p256>(in, w, pl, g, gtab, n, o, bitmap, reason, s, ev);
+  return seq<F30_k1, Fn_k1, Cv_k1>(in, w, pl, g, gtab, n, o, bitmap, reason, s, ev);
+}
+
+// bh_keys_register: import, dedup against the registry and within the call,
+// build a registry table per new key, publish, per-key status.
+template <class P, class C>
+static hipError_t reg_seq(const uint8_t* pub, const Work& w, const Plan& pl, const KeyReg& g,
+                          uint32_t n, uint8_t* status, hipStream_t s) {
+  const dim3 blk(256);
+  const dim3 grd((n + 255) / 256);
+  hipError_t e;
+  if ((e = plan_reset(pl, s))) return e;
+  hipLaunchKernelGGL((k_reg_prep<P, C>), grd, blk, 0, s, pub, w, n);
+  hipLaunchKernelGGL(k_key_insert, grd, blk, 0, s, w, pl, g, n);
+  hipLaunchKernelGGL(k_key_count, grd, blk, 0, s, w, pl, n);
+  hipLaunchKernelGGL(k_key_plan, grd, blk, 0, s, w, pl, g, n, 1u, 0u, 1u, 1u);
+  const uint32_t tab_blocks = (pl.max_tables + 255) / 256;
+  hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, pl, g,
+                     (const uint32_t*)nullptr, (uint8_t*)nullptr, tab_blocks);
+  hipLaunchKernelGGL(k_reg_publish, dim3(tab_blocks), blk, 0, s, w, pl, g);
+  hipLaunchKernelGGL(k_reg_status, grd, blk, 0, s, w, pl, n, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_register(int curve, const uint8_t* pub, const Work& w, const Plan& pl,
+                           const KeyReg& g, uint32_t n, uint8_t* status, hipStream_t s) {
+  if (curve == 0) return reg_seq<F30_p256, Cv_p256>(pub, w, pl, g, n, status, s);
+  return reg_seq<F30_k1, Cv_k1>(pub, w, pl, g, n, status, s);
 }
 
 }  // namespace bh

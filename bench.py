@@ -33,8 +33,18 @@ sys.path.insert(0, ROOT)
 # (16 ops) + 33 mixed adds (11 ops) + ~23 for the final add/x check = 1,426
 # F_p ops per verify, plus 65 x (5 dbl x 8 + 3 add x 16) = 5,720 per key table.
 MAC_PER_FP = 128
-FP_OPS = {"ladder_ms": 3200, "keycomb_ms": 1426, "ktab_ms": 5720}
-MACS_PER_VERIFY = FP_OPS["ladder_ms"] * MAC_PER_FP
+FP_LADDER, FP_KEYCOMB, FP_KTAB = 3200, 1426, 5720
+MACS_PER_VERIFY = FP_LADDER * MAC_PER_FP
+KERNELS = {"build_ladder_ms": "k_ktab_ladder", "keycomb_ms": "k_keycomb"}
+
+
+def kernel_fp_ops(stage: str, routes: dict) -> float:
+    """Algorithmic F_p ops of one launch of the stage's kernel."""
+    if stage == "build_ladder_ms":
+        return routes["ladder"] * FP_LADDER + routes["key_tables"] * FP_KTAB
+    return routes["keycomb"] * FP_KEYCOMB
+
+
 # Algorithmic HBM bytes per verify record (config 2): pub 64 + sig ~71 + msg 256
 # + offsets/lengths 24 + reason 1 + bitmap 1/8.
 def alg_bytes_per_record(msg_len: int) -> float:
@@ -134,29 +144,53 @@ def bench_latency(a, rank, world, local):
     reason = np.zeros(n, np.uint8)
     dwords = DA(local, ((n + 63) // 64) * 8)
     dreason = DA(local, n)
-    for _ in range(max(1, a.warmup)):
-        _lib.check(host_call(bitmap, reason))
-        _lib.check(dev_call(dwords, dreason, None))
-    dist.barrier(world)
-    host_ms, dev_ms = [], []
-    tm = _lib.BhTiming()
-    kern = {k: 0.0 for k in _lib.BhTiming.STAGES}
-    for _ in range(a.steps):
-        t = time.perf_counter()
-        _lib.check(host_call(bitmap, reason))
-        host_ms.append((time.perf_counter() - t) * 1e3)
-    for _ in range(a.steps):
-        t = time.perf_counter()
-        _lib.check(dev_call(dwords, dreason, None))
-        dev_ms.append((time.perf_counter() - t) * 1e3)
-    _lib.check(dev_call(dwords, dreason, ctypes.byref(tm)))
-    kern = {k: round(getattr(tm, k), 4) for k in _lib.BhTiming.STAGES}
-    dist.barrier(world)
-    p50 = dist.max_over_ranks(percentile(host_ms, 50), world)
-    parity_ok = bool((reason == expect).all() and (dreason.to_numpy(np.uint8, n) == expect).all()
-                     and (np.unpackbits(bitmap, bitorder="little")[:n].astype(bool)
-                          == (expect == 0)).all())
-    parity_ok = dist.all_true(parity_ok, world)
+    pubs = np.unique((w.pub if a.config == 3 else r.xy).reshape(-1, 64)[:n], axis=0)
+
+    def measure(tag):
+        for _ in range(max(1, a.warmup)):
+            _lib.check(host_call(bitmap, reason))
+            _lib.check(dev_call(dwords, dreason, None))
+        dist.barrier(world)
+        host_ms, dev_ms = [], []
+        for _ in range(a.steps):
+            t = time.perf_counter()
+            _lib.check(host_call(bitmap, reason))
+            host_ms.append((time.perf_counter() - t) * 1e3)
+        for _ in range(a.steps):
+            t = time.perf_counter()
+            _lib.check(dev_call(dwords, dreason, None))
+            dev_ms.append((time.perf_counter() - t) * 1e3)
+        tm = _lib.BhTiming()
+        _lib.check(dev_call(dwords, dreason, ctypes.byref(tm)))
+        ok = bool((reason == expect).all() and (dreason.to_numpy(np.uint8, n) == expect).all()
+                  and (np.unpackbits(bitmap, bitorder="little")[:n].astype(bool)
+                       == (expect == 0)).all())
+        return {
+            "host_p50": round(percentile(host_ms, 50), 4),
+            "host_p99": round(percentile(host_ms, 99), 4),
+            "device_resident_p50": round(percentile(dev_ms, 50), 4),
+            "device_resident_p99": round(percentile(dev_ms, 99), 4),
+            "kernel_ms": {k: round(getattr(tm, k), 4) for k in _lib.BhTiming.STAGES},
+            "routes": {"keycomb": tm.n_keycomb, "ladder": tm.n_ladder,
+                       "key_tables": tm.n_keytables, "wide": tm.wide},
+            "parity": ok,
+        }
+
+    # cold: no key known to the device (per-batch tables are off at this size,
+    # every record takes the ladder)
+    _lib.check(L.bh_keys_clear(-1, curve))
+    cold = measure("cold")
+    # warm: the batch's public keys registered once beforehand (the Fabric
+    # MSP identity cache / the BDLS participant set); registration timed alone
+    t = time.perf_counter()
+    st = np.zeros(len(pubs), np.uint8)
+    _lib.check(L.bh_keys_register(-1, curve, np.ascontiguousarray(pubs).ctypes.data, len(pubs),
+                                  st.ctypes.data))
+    reg_ms = (time.perf_counter() - t) * 1e3
+    warm = measure("warm")
+    _lib.check(L.bh_keys_clear(-1, curve))
+    p50 = dist.max_over_ranks(warm["host_p50"], world)
+    parity_ok = dist.all_true(cold["parity"] and warm["parity"], world)
     out = {
         "metric": ("block-validate latency (ms, one block's signatures, host C ABI)"
                    if a.config == 3 else "BDLS round verify latency (ms, host C ABI)"),
@@ -164,14 +198,12 @@ def bench_latency(a, rank, world, local):
         "warmup": a.warmup, "ms_per_step": round(p50, 4), "higher_is_better": False,
         "scaling": "replicas", "vs_baseline": None,
         "dtype": "u32", "data": "synthetic (seeded keys/signatures, workload/gen.c)",
-        "config": {"workload": workload_desc, "records": n},
+        "config": {"workload": workload_desc, "records": n, "distinct_keys": len(pubs),
+                   "value_is": "warm host_p50: keys registered before timing "
+                               "(bh_keys_register); cold = no key known"},
         "parity": parity_ok,
-        "latency_ms": {"host_p50": round(percentile(host_ms, 50), 4),
-                       "host_p99": round(percentile(host_ms, 99), 4),
-                       "device_resident_p50": round(percentile(dev_ms, 50), 4),
-                       "device_resident_p99": round(percentile(dev_ms, 99), 4)},
-        "kernel_ms": kern,
-        "routes": {"keycomb": tm.n_keycomb, "ladder": tm.n_ladder, "key_tables": tm.n_keytables},
+        "latency_ms": {"warm": warm, "cold": cold,
+                       "register_keys_ms": round(reg_ms, 3)},
     }
     if rank == 0 and a.cpu_baseline:
         from oracle import orc
@@ -269,11 +301,10 @@ def main():
     ms_per_step = elapsed * 1e3 / a.steps
     peak, peak_src = (a.mac_peak, "--mac-peak") if a.mac_peak else mac_peak_default()
     # dominant kernel of the step and its algorithmic work per launch
-    dom = max(("ladder_ms", "keycomb_ms", "ktab_ms"), key=lambda k: kern[k])
-    units = {"ladder_ms": routes["ladder"], "keycomb_ms": routes["keycomb"],
-             "ktab_ms": routes["key_tables"]}[dom]
+    dom = max(KERNELS, key=lambda k: kern[k])
     dom_avg_s = kern[dom] * 1e-3 / a.steps
-    achieved = units * FP_OPS[dom] * MAC_PER_FP / dom_avg_s if dom_avg_s > 0 else 0.0
+    fp_ops = kernel_fp_ops(dom, routes)
+    achieved = fp_ops * MAC_PER_FP / dom_avg_s if dom_avg_s > 0 else 0.0
 
     out = {
         "metric": "P-256 ECDSA verifies/sec (fused SHA-256, bit-exact vs Go crypto/ecdsa + Fabric low-S)",
@@ -299,14 +330,17 @@ def main():
         "routes": routes,
         "roofline": {
             "bound": "valu",
-            "kernel": {"ladder_ms": "k_ladder", "keycomb_ms": "k_keycomb", "ktab_ms": "k_ktab_build"}[dom],
+            "kernel": KERNELS[dom],
             "achieved": achieved / 1e12,
             "peak": peak / 1e12,
             "unit": "TMAC/s (u32 x u32 -> u64)",
             "frac": achieved / peak if peak else None,
-            "work_per_unit": f"{FP_OPS[dom]} F_p mul/sqr x {MAC_PER_FP} u32 MACs per "
-                             f"{'key table' if dom == 'ktab_ms' else 'verify'} (SURVEY 8(d) units)",
-            "units_per_launch": units,
+            "work_per_launch": (f"{routes['ladder']} ladder verifies x {FP_LADDER} + "
+                                f"{routes['key_tables']} key tables x {FP_KTAB}"
+                                if dom == "build_ladder_ms" else
+                                f"{routes['keycomb']} key-table verifies x {FP_KEYCOMB}")
+                               + f" F_p mul/sqr x {MAC_PER_FP} u32 MACs (SURVEY 8(d) units)",
+            "fp_ops_per_launch": fp_ops,
             "peak_source": peak_src,
             "traffic": None,
             "alg_bytes_per_record": alg_bytes_per_record(a.msg_len),
@@ -316,7 +350,12 @@ def main():
     prof = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(prof):
         with open(prof) as f:
-            out["roofline"]["traffic"] = json.load(f).get("ladder_bytes_per_launch")
+            tr = json.load(f).get("kernels", {})
+        # the profile's per-launch bytes for this kernel, when it was taken on
+        # this same workload (bench default: config 2)
+        hit = [v for k, v in tr.items() if k.startswith(KERNELS[dom] + "<")]
+        if hit and a.config == 2 and n == 1 << 20:
+            out["roofline"]["traffic"] = hit[0]["bytes_per_launch"]
 
     if rank == 0 and world == 1 and a.cpu_baseline:
         from oracle import orc

@@ -55,6 +55,8 @@ extern "C" {
 /* ---- flags ---- */
 #define BH_F_HASH_SHA256 1u /* msg[i] is a message; digest = SHA-256(msg[i]) (identity.Verify) */
 #define BH_F_NO_LOW_S 2u    /* do not apply Fabric's low-S rule (plain crypto/ecdsa.Verify) */
+#define BH_F_KEEP_KEYS 4u   /* keys used >= 2 times in the batch get a table in the device's
+                               key registry (kept across calls, see bh_keys_register) */
 
 #define BH_CURVE_P256 0
 #define BH_CURVE_SECP256K1 1
@@ -74,16 +76,17 @@ typedef struct bh_batch {
 /* Per-call stage timing (milliseconds, HIP events on the launch stream) and
  * routing counts. */
 typedef struct bh_timing {
-  float prep_ms;       /* parse + checks + SHA-256 + Montgomery inputs */
+  float prep_ms;       /* parse + checks + SHA-256 / BLAKE2b + Montgomery inputs */
   float inv_ms;        /* batched s^-1 mod n, u1, u2 */
-  float plan_ms;       /* public-key dedup + routing */
-  float ktab_ms;       /* per-key fixed-base tables (keys used >= 4 times) */
-  float keycomb_ms;    /* u2 Q from key tables + u1 G + x check */
-  float ladder_ms;     /* u2 Q by variable-base ladder + u1 G + x check, bitmap */
+  float plan_ms;       /* registry lookup + public-key dedup + routing */
+  float build_ladder_ms; /* one grid: per-key fixed-base table builds and the
+                            variable-base ladder for records without a table */
+  float publish_ms;    /* registry publication of new tables (BH_F_KEEP_KEYS) */
+  float keycomb_ms;    /* u2 Q from key tables + u1 G + x check, bitmap */
   uint32_t n_keycomb;  /* records verified on the key-table path */
   uint32_t n_ladder;   /* records verified on the ladder path */
-  uint32_t n_keytables;
-  uint32_t reserved;
+  uint32_t n_keytables; /* tables built in this call */
+  uint32_t wide;       /* lanes per record on the key-table path */
 } bh_timing;
 
 /* Initialise the devices in device_mask (bit d = HIP device d; 0 = all
@@ -168,6 +171,26 @@ int bh_dev_free(int device, void *ptr);
 int bh_memcpy_h2d(int device, void *dst, const void *src, size_t bytes);
 int bh_memcpy_d2h(int device, void *dst, const void *src, size_t bytes);
 int bh_sync(int device); /* wait for all work queued on the device's library stream */
+
+/* ---- key registry ---------------------------------------------------------
+ * Per device and curve, a persistent store of per-key fixed-base tables
+ * (65 x 8 multiples of Q, 56 KiB per key in HBM). A record whose public key
+ * is registered skips every doubling: u2 Q is 65 table additions. This is the
+ * device-side counterpart of the reference's long-lived identities -- the
+ * MSP identity cache (msp/cache/cache.go) for Fabric, the fixed participant
+ * set (consensus.go:456-466, Config.Participants) for BDLS. Verification
+ * results never depend on the registry (same bitmap and reasons with or
+ * without it); only the route and the time do.
+ * capacity: tables per (device, curve); bh_keys_register / BH_F_KEEP_KEYS
+ * reserve 65536 on first use when not reserved before. Entries persist until
+ * bh_keys_clear; once full, new keys take the per-batch path. */
+int bh_keys_reserve(int device, int curve, size_t capacity);
+/* Import and register n keys (host pointer, n * 64 bytes X || Y). status
+ * (optional, n bytes): 0 registered (or already present), BH_R_BAD_KEY not a
+ * valid curve point, 255 registry full. Synchronous. */
+int bh_keys_register(int device, int curve, const uint8_t *pub, size_t n, uint8_t *status);
+int bh_keys_clear(int device, int curve);
+int bh_keys_count(int device, int curve, size_t *count);
 
 #ifdef __cplusplus
 }

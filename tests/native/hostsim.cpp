@@ -24,6 +24,43 @@ static const uint32_t* gtab_for() {
   return g.data();
 }
 
+// Lanes per record on the key-table path (verify_kernels.hip k_keycomb_wide);
+// 1 = k_keycomb.
+static int g_wide = 1;
+extern "C" void hs_set_wide(int L) { g_wide = L; }
+
+template <class P, int L>
+static bool wide_keycomb(const Work& w, const uint32_t* gtab, uint32_t i, const uint32_t* tab) {
+  J30 C[L];
+  bool inf[L];
+  for (int l = 0; l < L; l++) keycomb_part<P, L>(C[l], inf[l], w, gtab, i, tab, (uint32_t)l);
+  for (int off = 1; off < L; off <<= 1) {  // the kernel's __shfl_xor butterfly
+    J30 D[L];
+    bool dinf[L];
+    for (int l = 0; l < L; l++) {
+      j_copy(D[l], C[l]);
+      dinf[l] = inf[l];
+      j_acc<P>(D[l], dinf[l], C[l ^ off], inf[l ^ off]);
+    }
+    for (int l = 0; l < L; l++) {
+      j_copy(C[l], D[l]);
+      inf[l] = dinf[l];
+    }
+  }
+  return finish_check<P>(w, i, C[0], inf[0], C[0], true);
+}
+
+template <class P>
+static bool keycomb_any(const Work& w, const uint32_t* gtab, uint32_t i, const uint32_t* tab) {
+  switch (g_wide) {
+    case 2: return wide_keycomb<P, 2>(w, gtab, i, tab);
+    case 4: return wide_keycomb<P, 4>(w, gtab, i, tab);
+    case 8: return wide_keycomb<P, 8>(w, gtab, i, tab);
+    case 16: return wide_keycomb<P, 16>(w, gtab, i, tab);
+    default: return stage_keycomb<P>(w, gtab, i, tab);
+  }
+}
+
 // Sequential restatement of the device launch sequence (verify_kernels.hip
 // seq()): prep, inv, key dedup / plan / split, key tables, both verify paths.
 // min_uses overrides kMinUses (and the batch-size gate) so tests can force
@@ -82,7 +119,7 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
         tables.emplace_back(kKTabWords);
         ktab_build<P>(tables.back().data(), w, r);
       }
-      ok = stage_keycomb<P>(w, gtab, i, tables[tab_of[r]].data());
+      ok = keycomb_any<P>(w, gtab, i, tables[tab_of[r]].data());
       combs++;
     } else {
       ok = stage_ladder<P>(w, gtab, i, i / 64, i % 64);

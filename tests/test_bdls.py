@@ -114,8 +114,8 @@ def _k1_edge_records():
     return recs
 
 
-@pytest.mark.parametrize("min_uses", [1, 1000])
-def test_k1_curve_edges_hostsim(hs, min_uses):
+@pytest.mark.parametrize("min_uses,wide", [(1, 1), (1000, 1), (1, 16), (1, 4)])
+def test_k1_curve_edges_hostsim(hs, min_uses, wide):
     recs = _k1_edge_records()
     pub = np.frombuffer(b"".join(qx.to_bytes(32, "big") + qy.to_bytes(32, "big")
                                  for _, qx, qy, _, _, _ in recs), np.uint8)
@@ -128,9 +128,13 @@ def test_k1_curve_edges_hostsim(hs, min_uses):
     sig = np.frombuffer(b"".join(sigs), np.uint8)
     dg = np.frombuffer(b"".join(dgs), np.uint8)
     out = np.zeros(len(recs), np.uint8)
-    hs.hs_verify_k1_digest(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
-                           dg.ctypes.data, do.ctypes.data, dl.ctypes.data, len(recs), min_uses,
-                           out.ctypes.data)
+    hs.hs_set_wide(wide)
+    try:
+        hs.hs_verify_k1_digest(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
+                               dg.ctypes.data, do.ctypes.data, dl.ctypes.data, len(recs),
+                               min_uses, out.ctypes.data)
+    finally:
+        hs.hs_set_wide(1)
     bad = [(t[0], int(o), t[5]) for t, o in zip(recs, out) if o != t[5]]
     assert not bad
     assert any(t[0] == "k1_xwrap_accept" and t[5] == 0 for t in recs)

@@ -79,7 +79,7 @@ def test_unique_keys(csp):
 def test_device_api(csp):
     """bh_verify_dev on HBM-resident buffers (library-owned device memory)."""
     from bdls_amd import workload
-    w = workload.generate(5000, 100, 256, 8, seed=9)
+    w = workload.generate(10_000, 100, 256, 8, seed=9)
     DA = _lib.DeviceArray
     t = [DA.from_numpy(0, x) for x in w.arrays()]
     words = DA(0, ((w.n + 63) // 64) * 8)
@@ -92,8 +92,8 @@ def test_device_api(csp):
     bits = np.unpackbits(words.to_numpy(np.uint64, (w.n + 63) // 64).view(np.uint8),
                          bitorder="little")[:w.n]
     assert (bits.astype(bool) == w.expected_valid).all()
-    assert tm.prep_ms > 0 and tm.keycomb_ms + tm.ladder_ms > 0
-    # 100 keys over 5000 records: the key-table path is taken
+    assert tm.prep_ms > 0 and tm.keycomb_ms + tm.build_ladder_ms > 0
+    # 100 keys over 10000 records: the key-table path is taken
     assert tm.n_keytables > 0 and tm.n_keycomb > 0
     # async form + explicit sync gives the same answer
     _lib.check(_lib.lib().bh_verify_dev(0, 0, ctypes.byref(b), w.n, _lib.BH_F_HASH_SHA256,

@@ -70,6 +70,23 @@ def test_hostsim_golden_keycomb_path(hs, golden, fused):
     assert not bad
 
 
+@pytest.mark.parametrize("wide", [4, 16])
+@pytest.mark.parametrize("fused", [False, True])
+def test_hostsim_golden_wide_keycomb(hs, golden, fused, wide):
+    """The L-lanes-per-record key-table path (k_keycomb_wide): interleaved
+    windows, offset recoding, butterfly combine -- bit-exact on every golden
+    record, including the crafted infinity / u1 G == u2 Q / x-wrap cases."""
+    recs = [r for r in golden if (not fused) or "msg" in r]
+    hs.hs_set_wide(wide)
+    try:
+        out, ncomb = run2(hs, pack(recs, fused), fused, 1)
+    finally:
+        hs.hs_set_wide(1)
+    assert ncomb > 0
+    bad = [(r["tag"], int(o), r["reason"]) for r, o in zip(recs, out) if o != r["reason"]]
+    assert not bad
+
+
 def test_hostsim_workload_mixed_paths(hs):
     from bdls_amd import workload
     w = workload.generate(900, 60, 256, 4, seed=13, nthreads=4)

@@ -1,0 +1,155 @@
+"""Device key registry (bh_keys_*, BH_F_KEEP_KEYS) and the wide key-table path.
+
+The registry only changes the route a record takes (per-key comb instead of
+the ladder) and the time; every result must stay bit-exact with the golden
+expectations and the by-construction workload reasons.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from bdls_amd import _lib
+from tests.conftest import pack
+
+pytestmark = pytest.mark.gpu
+CURVE_P256, CURVE_K1 = 0, 1
+
+
+@pytest.fixture
+def dev():
+    _lib.ensure_init()
+    L = _lib.lib()
+    for c in (CURVE_P256, CURVE_K1):
+        _lib.check(L.bh_keys_clear(-1, c))
+    yield L
+    for c in (CURVE_P256, CURVE_K1):
+        _lib.check(L.bh_keys_clear(-1, c))
+
+
+def count(L, curve, device=0):
+    c = ctypes.c_size_t()
+    _lib.check(L.bh_keys_count(device, curve, ctypes.byref(c)))
+    return c.value
+
+
+def register(L, curve, pubs: np.ndarray, device=-1):
+    pubs = np.ascontiguousarray(pubs, np.uint8)
+    n = len(pubs) // 64
+    st = np.full(n, 77, np.uint8)
+    _lib.check(L.bh_keys_register(device, curve, pubs.ctypes.data, n, st.ctypes.data))
+    return st
+
+
+def run_dev(L, arrs, n, flags):
+    DA = _lib.DeviceArray
+    t = [DA.from_numpy(0, x) for x in arrs]
+    words = DA(0, ((n + 63) // 64) * 8)
+    reason = DA(0, max(n, 1))
+    b = _lib.BhBatch(*[x.ptr for x in t])
+    tm = _lib.BhTiming()
+    _lib.check(L.bh_verify_dev(0, 0, ctypes.byref(b), n, flags, words.ptr, reason.ptr, None, 1,
+                               ctypes.byref(tm)))
+    bits = np.unpackbits(words.to_numpy(np.uint64, (n + 63) // 64).view(np.uint8),
+                         bitorder="little")[:n].astype(bool)
+    return reason.to_numpy(np.uint8, n), bits, tm
+
+
+def test_register_status_and_count(dev):
+    from bdls_amd import workload
+    w = workload.generate(300, 40, 32, 0, seed=21)
+    keys = np.unique(w.pub.reshape(-1, 64), axis=0)
+    bad = keys[:2].copy()
+    bad[0, 63] ^= 1                      # off the curve
+    bad[1, :32] = 0xff                   # X >= p
+    pubs = np.concatenate([keys, keys[:5], bad]).reshape(-1)
+    st = register(dev, CURVE_P256, pubs)
+    assert (st[:len(keys) + 5] == 0).all()
+    assert list(st[-2:]) == [7, 7]
+    assert count(dev, CURVE_P256) == len(keys)
+    st2 = register(dev, CURVE_P256, keys.reshape(-1))  # idempotent
+    assert (st2 == 0).all() and count(dev, CURVE_P256) == len(keys)
+    _lib.check(dev.bh_keys_clear(-1, CURVE_P256))
+    assert count(dev, CURVE_P256) == 0
+
+
+def test_registry_full(dev):
+    from bdls_amd import workload
+    _lib.check(dev.bh_keys_reserve(0, CURVE_P256, 8))
+    try:
+        w = workload.generate(200, 30, 32, 0, seed=22)
+        keys = np.unique(w.pub.reshape(-1, 64), axis=0)
+        st = register(dev, CURVE_P256, keys.reshape(-1), device=0)
+        assert (st == 0).sum() == 8 and (st == _lib.KEY_FULL).sum() == len(keys) - 8
+        assert count(dev, CURVE_P256) == 8
+        # records of registered and unregistered keys verify identically
+        r, bits, tm = run_dev(dev, w.arrays(), w.n, _lib.BH_F_HASH_SHA256)
+        assert (r == w.reason).all() and (bits == w.expected_valid).all()
+        assert tm.n_keycomb > 0 and tm.n_ladder > 0
+    finally:
+        _lib.check(dev.bh_keys_reserve(0, CURVE_P256, 1 << 16))
+
+
+@pytest.mark.parametrize("n,wide", [(3000, 16), (20_000, 4), (40_000, 1)])
+def test_registered_keys_route_and_parity(dev, n, wide):
+    from bdls_amd import workload
+    w = workload.generate(n, 50, 200, 8, seed=n)
+    r0, b0, tm0 = run_dev(dev, w.arrays(), w.n, _lib.BH_F_HASH_SHA256)
+    assert (r0 == w.reason).all()
+    register(dev, CURVE_P256, np.unique(w.pub.reshape(-1, 64), axis=0).reshape(-1))
+    r1, b1, tm1 = run_dev(dev, w.arrays(), w.n, _lib.BH_F_HASH_SHA256)
+    assert (r1 == w.reason).all() and (b1 == w.expected_valid).all()
+    assert tm1.n_keytables == 0 and tm1.n_ladder == 0 and tm1.n_keycomb > 0
+    assert tm1.wide == wide
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_golden_through_registry_wide(dev, golden, fused):
+    """Every golden record (crafted edge cases included) through registered
+    keys on the 16-lane path."""
+    recs = [r for r in golden if (not fused) or "msg" in r]
+    arrs = pack(recs, fused)
+    register(dev, CURVE_P256, arrs[0])  # invalid keys come back as status 7
+    flags = _lib.BH_F_HASH_SHA256 if fused else 0
+    r, bits, tm = run_dev(dev, arrs, len(recs), flags)
+    bad = [(x["tag"], int(o), x["reason"]) for x, o in zip(recs, r) if o != x["reason"]]
+    assert not bad
+    assert [bool(v) for v in bits] == [x["valid"] for x in recs]
+    assert tm.n_keycomb > 0 and tm.wide == 16
+
+
+def test_keep_keys_flag(dev):
+    from bdls_amd import workload
+    w = workload.generate(4000, 30, 100, 8, seed=31)
+    f = _lib.BH_F_HASH_SHA256 | _lib.BH_F_KEEP_KEYS
+    r1, b1, tm1 = run_dev(dev, w.arrays(), w.n, f)
+    assert (r1 == w.reason).all() and tm1.n_keytables > 0
+    assert count(dev, CURVE_P256) == tm1.n_keytables
+    w2 = workload.generate(4000, 30, 100, 8, seed=31)  # same keys, same records
+    r2, b2, tm2 = run_dev(dev, w2.arrays(), w2.n, f)
+    assert (r2 == w2.reason).all() and (b2 == b1).all()
+    assert tm2.n_keytables == 0 and tm2.n_keycomb >= tm1.n_keycomb
+
+
+def test_bdls_round_registered_validators(dev):
+    from bdls_amd.workload import generate_bdls_round
+    b = generate_bdls_round(nval=100, curve=CURVE_K1, seed=12)
+    register(dev, CURVE_K1, np.unique(b.xy.reshape(-1, 64)[:b.n], axis=0).reshape(-1))
+    assert count(dev, CURVE_K1) == 100
+    DA = _lib.DeviceArray
+    t = [DA.from_numpy(0, x) for x in b.arrays()]
+    db = _lib.BhBdlsBatch(*[x.ptr for x in t])
+    words = DA(0, ((b.n + 63) // 64) * 8)
+    reason = DA(0, b.n)
+    tm = _lib.BhTiming()
+    _lib.check(dev.bh_verify_bdls_dev(0, CURVE_K1, ctypes.byref(db), b.n, words.ptr, reason.ptr,
+                                      None, 1, ctypes.byref(tm)))
+    assert not reason.to_numpy(np.uint8, b.n).any()
+    assert tm.n_keycomb == b.n and tm.n_ladder == 0
+    # host API, same registry (every device)
+    bitmap = np.zeros((b.n + 7) // 8, np.uint8)
+    rs = np.full(b.n, 255, np.uint8)
+    hb = _lib.BhBdlsBatch(*[x.ctypes.data for x in b.arrays()])
+    _lib.check(dev.bh_verify_bdls(CURVE_K1, ctypes.byref(hb), b.n, bitmap.ctypes.data,
+                                  rs.ctypes.data))
+    assert not rs.any() and np.unpackbits(bitmap, bitorder="little")[:b.n].all()

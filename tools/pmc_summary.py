@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Per-kernel summary of rocprofv3 --pmc passes (tools/gpu_check.sh step pmc).
+
+usage: python tools/pmc_summary.py <dir with pmc_*/ subdirs or csvs> <out.json> [--traffic]
+
+For each kernel (short name) and counter: mean value per dispatch. With
+--traffic, also writes profiles/traffic.json: HBM bytes per launch from
+FETCH_SIZE (KB, doubled: gfx950 reports half of 16-B/lane reads, see
+/opt/skills/guides/MI355X_MICROARCH.md "HBM") + WRITE_SIZE (KB).
+"""
+from __future__ import annotations
+
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    m = re.search(r"::(k_\w+)", name)
+    base = m.group(1) if m else name.split("(")[0]
+    t = re.search(r"<(.*)>\(", name)
+    return f"{base}<{t.group(1)}>" if t else base
+
+
+def load(root: str):
+    acc = defaultdict(lambda: defaultdict(list))
+    meta = {}
+    for path in glob.glob(os.path.join(root, "**", "*counter_collection*.csv"), recursive=True) + \
+            glob.glob(os.path.join(root, "**", "pmc_*.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                k = short(row["Kernel_Name"])
+                acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                meta[k] = {"grid": int(row["Grid_Size"]), "wg": int(row["Workgroup_Size"]),
+                           "vgpr": int(row["VGPR_Count"]), "sgpr": int(row["SGPR_Count"]),
+                           "scratch": int(row["Scratch_Size"]), "lds": int(row["LDS_Block_Size"])}
+    out = {}
+    for k, cs in acc.items():
+        out[k] = {"meta": meta[k], "counters": {c: sum(v) / len(v) for c, v in cs.items()},
+                  "dispatches": max(len(v) for v in cs.values())}
+    return out
+
+
+def main():
+    root, dst = sys.argv[1], sys.argv[2]
+    s = load(root)
+    with open(dst, "w") as f:
+        json.dump(s, f, indent=1, sort_keys=True)
+    if "--traffic" in sys.argv:
+        tr = {"source": f"{root} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
+              "correction": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half "
+                            "of 16-B/lane read bytes); WRITE_SIZE as reported",
+              "kernels": {}}
+        for k, v in s.items():
+            c = v["counters"]
+            if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                tr["kernels"][k] = {"fetch_bytes": 2 * c["FETCH_SIZE"] * 1024,
+                                    "write_bytes": c["WRITE_SIZE"] * 1024,
+                                    "bytes_per_launch": (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024}
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "profiles", "traffic.json")
+        with open(path, "w") as f:
+            json.dump(tr, f, indent=1, sort_keys=True)
+    for k, v in sorted(s.items()):
+        print(k, v["meta"], {c: round(x, 1) for c, x in v["counters"].items()})
+
+
+if __name__ == "__main__":
+    main()
