@@ -25,7 +25,7 @@ EXPORTS = (
     "bh_workspace_bytes", "bh_verify", "bh_verify_dev", "bh_csp_verify_p256",
     "bh_parse_der_sig", "bh_dev_alloc", "bh_dev_free", "bh_memcpy_h2d", "bh_memcpy_d2h",
     "bh_sync", "bh_verify_bdls", "bh_verify_bdls_dev", "bh_keys_reserve", "bh_keys_register",
-    "bh_keys_clear", "bh_keys_count",
+    "bh_keys_clear", "bh_keys_count", "bh_timing_begin", "bh_timing_end",
 )
 KEY_FULL = 255  # bh_keys_register status: registry full
 
@@ -108,6 +108,10 @@ def lib() -> ctypes.CDLL:
         L.bh_memcpy_d2h.restype = i32
         L.bh_sync.argtypes = [i32]
         L.bh_sync.restype = i32
+        L.bh_timing_begin.argtypes = [i32]
+        L.bh_timing_begin.restype = i32
+        L.bh_timing_end.argtypes = [i32, vp]
+        L.bh_timing_end.restype = i32
         L.bh_keys_reserve.argtypes = [i32, i32, sz]
         L.bh_keys_reserve.restype = i32
         L.bh_keys_register.argtypes = [i32, i32, vp, sz, vp]

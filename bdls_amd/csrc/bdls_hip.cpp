@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -100,6 +101,12 @@ struct Dev {
   hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipEvent_t done = nullptr;  // end of the last pass (orders passes across streams)
   bool done_recorded = false;
+  // deferred timing (bh_timing_begin/_end): one event set per pass, read at end
+  bool defer = false;
+  std::vector<std::vector<hipEvent_t>> ev_pool;
+  size_t ev_used = 0;
+  const uint32_t* last_counters = nullptr;  // plan counters of the last pass
+  uint32_t last_max_tables = 0, last_wide = 0;
   std::mutex mu;
 };
 
@@ -230,6 +237,9 @@ void dev_free(Dev& d) {
   for (auto& e : d.ev)
     if (e) (void)hipEventDestroy(e);
   if (d.done) (void)hipEventDestroy(d.done);
+  for (auto& set : d.ev_pool)
+    for (auto e : set) (void)hipEventDestroy(e);
+  d.ev_pool.clear();
   if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
@@ -247,7 +257,15 @@ std::vector<Dev*> all_devs() {
 
 bh::LaunchOpts launch_opts(size_t m, uint32_t flags) {
   bh::LaunchOpts o;
-  o.inv_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(16, m / 65536));
+  // records per inversion lane: enough lanes for ~4 waves per SIMD (safegcd
+  // makes the per-lane inversion cheap, so occupancy matters more than
+  // amortisation); BH_INV_CHUNK overrides for tuning
+  static const long env_chunk = [] {
+    const char* e = getenv("BH_INV_CHUNK");
+    return e ? atol(e) : 0L;
+  }();
+  o.inv_chunk = env_chunk > 0 ? (uint32_t)std::min<long>(env_chunk, 64)
+                              : (uint32_t)std::max<size_t>(1, std::min<size_t>(16, m / 262144));
   o.keep = (flags & BH_F_KEEP_KEYS) != 0;
   // kept tables pay off over later calls, so a second use in the batch is
   // enough; per-batch tables must pay off inside this batch
@@ -299,8 +317,19 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
     int rc = carve_work(d, m, &w, &pl);
     if (rc) return rc;
     const bh::LaunchOpts o = launch_opts(m, flags);
+    hipEvent_t* ev = t ? d.ev : nullptr;
+    if (!t && d.defer) {
+      if (d.ev_used == d.ev_pool.size()) {
+        d.ev_pool.emplace_back(7, nullptr);
+        for (auto& e : d.ev_pool.back()) HIPCHK(hipEventCreate(&e));
+      }
+      ev = d.ev_pool[d.ev_used++].data();
+    }
     HIPCHK(launch(curve, slice(b, base, flags), w, pl, d.reg[curve].g, d.gtab[curve],
-                  (uint32_t)m, o, bitmap + base / 64, reason + base, s, t ? d.ev : nullptr));
+                  (uint32_t)m, o, bitmap + base / 64, reason + base, s, ev));
+    d.last_counters = pl.counters;
+    d.last_max_tables = pl.max_tables;
+    d.last_wide = (uint32_t)o.wide;
     if (t) {
       HIPCHK(hipEventSynchronize(d.ev[6]));
       float ms[6];
@@ -660,6 +689,46 @@ int bh_sync(int device) {
   HIPCHK(hipSetDevice(d->id));
   if (d->done_recorded) HIPCHK(hipEventSynchronize(d->done));
   HIPCHK(hipStreamSynchronize(d->stream));
+  return BH_OK;
+}
+
+int bh_timing_begin(int device) {
+  Dev* d = get_dev(device);
+  if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
+  std::lock_guard<std::mutex> g(d->mu);
+  d->defer = true;
+  d->ev_used = 0;
+  return BH_OK;
+}
+
+int bh_timing_end(int device, bh_timing* t) {
+  if (!t) return fail(BH_E_INVALID, "null timing");
+  Dev* d = get_dev(device);
+  if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
+  std::lock_guard<std::mutex> g(d->mu);
+  HIPCHK(hipSetDevice(d->id));
+  *t = bh_timing{};
+  d->defer = false;
+  float* acc[6] = {&t->prep_ms, &t->inv_ms, &t->plan_ms, &t->build_ladder_ms, &t->publish_ms,
+                   &t->keycomb_ms};
+  for (size_t p = 0; p < d->ev_used; p++) {
+    const std::vector<hipEvent_t>& ev = d->ev_pool[p];
+    HIPCHK(hipEventSynchronize(ev[6]));
+    for (int k = 0; k < 6; k++) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+      *acc[k] += ms;
+    }
+  }
+  if (d->ev_used && d->last_counters) {
+    uint32_t cnt[4];
+    HIPCHK(hipMemcpy(cnt, d->last_counters, 16, hipMemcpyDeviceToHost));
+    t->n_keycomb = cnt[0];
+    t->n_ladder = cnt[1];
+    t->n_keytables = std::min<uint32_t>(cnt[2], d->last_max_tables);
+    t->wide = d->last_wide;
+  }
+  d->ev_used = 0;
   return BH_OK;
 }
 

@@ -173,6 +173,160 @@ BH_HDNI void mont_inv(uint32_t r[8], const uint32_t a[8]) {
   copy8(r, acc);
 }
 
+// ------------------------------------------- safegcd (divsteps) inversion
+// Bernstein-Yang constant-iteration modular inversion (the "safegcd" divstep
+// recurrence, "Fast constant-time gcd computation and modular inversion",
+// 2019) on signed radix-2^30 limbs: 20 batches of 30 branch-free divsteps
+// (600 >= 590, the iteration bound for 256-bit moduli), each batch applied to
+// (f, g) and (d, e) as a 2x2 matrix of 31-bit integers. About 14k simple VALU
+// instructions per inversion against ~77k for the Fermat ladder above, with
+// no data-dependent branch (every lane of a wave runs the same schedule).
+// The inputs are public (signature scalars), so no side-channel rule applies;
+// constant iteration is chosen for SIMT uniformity.
+struct Div2x2 {
+  int32_t u, v, q, r;
+};
+
+// 30 divsteps on the low words of f (odd) and g; returns the new zeta
+// (= -(delta + 1/2)). Matrix entries stay within [-2^30, 2^30].
+BH_HD int32_t divsteps30(int32_t zeta, uint32_t f, uint32_t g, Div2x2& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+#pragma unroll
+  for (int i = 0; i < 30; i++) {
+    uint32_t m1 = (uint32_t)(zeta >> 31);  // zeta < 0
+    const uint32_t m2 = 0u - (g & 1u);     // g odd
+    const uint32_t x = (f ^ m1) - m1, y = (u ^ m1) - m1, z = (v ^ m1) - m1;
+    g += x & m2;
+    q += y & m2;
+    r += z & m2;
+    m1 &= m2;
+    zeta = (zeta ^ (int32_t)m1) - 1;
+    f += g & m1;
+    u += q & m1;
+    v += r & m1;
+    g >>= 1;
+    u <<= 1;
+    v <<= 1;
+  }
+  t.u = (int32_t)u;
+  t.v = (int32_t)v;
+  t.q = (int32_t)q;
+  t.r = (int32_t)r;
+  return zeta;
+}
+
+constexpr int32_t kS30Mask = 0x3fffffff;
+
+// [d, e] <- (t [d, e] + m [md, me]) / 2^30 with md, me chosen so the division
+// is exact; keeps d, e in (-2m, m).
+template <class M>
+BH_HD void divsteps_update_de(int32_t d[9], int32_t e[9], const Div2x2& t) {
+  const int32_t sd = d[8] >> 31, se = e[8] >> 31;
+  int32_t md = (t.u & sd) + (t.v & se);
+  int32_t me = (t.q & sd) + (t.r & se);
+  int64_t cd = (int64_t)t.u * d[0] + (int64_t)t.v * e[0];
+  int64_t ce = (int64_t)t.q * d[0] + (int64_t)t.r * e[0];
+  md -= (int32_t)((M::inv30 * (uint32_t)cd + (uint32_t)md) & (uint32_t)kS30Mask);
+  me -= (int32_t)((M::inv30 * (uint32_t)ce + (uint32_t)me) & (uint32_t)kS30Mask);
+  cd += (int64_t)M::s30[0] * md;
+  ce += (int64_t)M::s30[0] * me;
+  cd >>= 30;
+  ce >>= 30;
+#pragma unroll
+  for (int i = 1; i < 9; i++) {
+    const int32_t di = d[i], ei = e[i];
+    cd += (int64_t)t.u * di + (int64_t)t.v * ei + (int64_t)M::s30[i] * md;
+    ce += (int64_t)t.q * di + (int64_t)t.r * ei + (int64_t)M::s30[i] * me;
+    d[i - 1] = (int32_t)cd & kS30Mask;
+    e[i - 1] = (int32_t)ce & kS30Mask;
+    cd >>= 30;
+    ce >>= 30;
+  }
+  d[8] = (int32_t)cd;
+  e[8] = (int32_t)ce;
+}
+
+// [f, g] <- t [f, g] / 2^30 (exact by construction of the divsteps).
+BH_HD void divsteps_update_fg(int32_t f[9], int32_t g[9], const Div2x2& t) {
+  int64_t cf = (int64_t)t.u * f[0] + (int64_t)t.v * g[0];
+  int64_t cg = (int64_t)t.q * f[0] + (int64_t)t.r * g[0];
+  cf >>= 30;
+  cg >>= 30;
+#pragma unroll
+  for (int i = 1; i < 9; i++) {
+    const int32_t fi = f[i], gi = g[i];
+    cf += (int64_t)t.u * fi + (int64_t)t.v * gi;
+    cg += (int64_t)t.q * fi + (int64_t)t.r * gi;
+    f[i - 1] = (int32_t)cf & kS30Mask;
+    g[i - 1] = (int32_t)cg & kS30Mask;
+    cf >>= 30;
+    cg >>= 30;
+  }
+  f[8] = (int32_t)cf;
+  g[8] = (int32_t)cg;
+}
+
+// d <- d + (c ? m : 0), then (neg ? -d : d), carries propagated (limbs 0..7
+// in [0, 2^30), limb 8 signed).
+template <class M>
+BH_HD void s30_addm_neg(int32_t d[9], bool c, bool neg) {
+  int64_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    int64_t v = (int64_t)d[i] + (c ? M::s30[i] : 0);
+    cy += neg ? -v : v;
+    if (i < 8) {
+      d[i] = (int32_t)cy & kS30Mask;
+      cy >>= 30;
+    } else {
+      d[8] = (int32_t)cy;
+    }
+  }
+}
+
+// r = a^-1 mod m for plain canonical a in [1, m) (32-bit limbs in and out).
+template <class M>
+BH_HD void mod_inv_sg(uint32_t r[8], const uint32_t a[8]) {
+  int32_t d[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int32_t e[9] = {1, 0, 0, 0, 0, 0, 0, 0, 0};
+  int32_t f[9], g[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    f[i] = M::s30[i];
+    const int b = 30 * i, w = b >> 5, s = b & 31;
+    uint64_t x = a[w];
+    if (w + 1 < 8) x |= (uint64_t)a[w + 1] << 32;
+    g[i] = (int32_t)((x >> s) & (i < 8 ? (uint64_t)kS30Mask : 0xffffffffull));
+  }
+  int32_t zeta = -1;
+  for (int it = 0; it < 20; it++) {
+    Div2x2 t;
+    zeta = divsteps30(zeta, (uint32_t)f[0], (uint32_t)g[0], t);
+    divsteps_update_de<M>(d, e, t);
+    divsteps_update_fg(f, g, t);
+  }
+  // g == 0, f == +-1, d == +-a^-1 in (-2m, m): bring to [0, m)
+  s30_addm_neg<M>(d, d[8] < 0, f[8] < 0);
+  s30_addm_neg<M>(d, d[8] < 0, false);
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    const int b = 32 * w, i = b / 30, s = b % 30;
+    uint64_t x = (uint64_t)(uint32_t)d[i] >> s;
+    if (i + 1 < 9) x |= (uint64_t)(uint32_t)d[i + 1] << (30 - s);  // 60 - s >= 32 bits
+    r[w] = (uint32_t)x;
+  }
+}
+
+// Montgomery-domain inverse by safegcd: input aR, output a^-1 R
+// ((aR)^-1 * R^3 * R^-1).
+template <class M>
+BH_HD void mont_inv_sg(uint32_t r[8], const uint32_t a[8]) {
+  uint32_t t[8], r3[8];
+  mod_inv_sg<M>(t, a);
+  load_const8(r3, M::r3);
+  mont_mul<M>(r, t, r3);
+}
+
 // 32 big-endian bytes -> limbs
 BH_HD void be32_to_limbs(uint32_t r[8], const uint8_t* b) {
 #pragma unroll

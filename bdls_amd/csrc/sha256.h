@@ -86,16 +86,12 @@ BH_HD void sha256_msg(uint32_t out[8], const uint8_t* m, uint64_t len) {
   uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                    0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
   const uint64_t total = ((len + 9 + 63) / 64) * 64;
-  const bool aligned = (((uintptr_t)m) & 3u) == 0;
   for (uint64_t blk = 0; blk < total; blk += 64) {
     uint32_t w[16];
-    if (aligned && blk + 64 <= len) {
-      const uint32_t* m32 = (const uint32_t*)(m + blk);
+    if (blk + 64 <= len) {  // full message block, any alignment
+      load_le_words<16>(w, m + blk);
 #pragma unroll
-      for (int i = 0; i < 16; i++) {
-        uint32_t x = m32[i];
-        w[i] = (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
-      }
+      for (int i = 0; i < 16; i++) w[i] = bswap32(w[i]);
     } else {
 #pragma unroll
       for (int i = 0; i < 16; i++) w[i] = sha256_word(m, len, total, blk + 4 * i);

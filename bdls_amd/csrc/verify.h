@@ -3,7 +3,7 @@
 //   stage_prep   : CSP.Verify arg checks, Go-exact DER parse, low-S, key and r
 //                  range / on-curve checks, digest (fused SHA-256 or given),
 //                  e = hashToNat, Montgomery conversions.        (1 lane/record)
-//   stage_inv    : w = s^-1 mod n by Montgomery's batch trick over a chunk of
+//   stage_inv    : w = s^-1 mod n by Montgomery's batch trick over a set of
 //                  records, u1 = e w, u2 = r w.               (1 lane/chunk)
 //   stage_ladder : Q table, signed-window (Booth w=5) ladder for u2 Q, fixed-base
 //                  comb (8-bit signed windows) for u1 G, final add, projective
@@ -319,20 +319,25 @@ BH_HD void stage_prep(const BdlsIn& in, const Work& w, uint32_t i) {
 }
 
 // ------------------------------------------------------------ batch inverse
-// Records [lo, hi) of one lane. Montgomery's trick: one Fermat inversion per
-// chunk, 3 multiplications per record.
+// One lane's records (strided). Montgomery's trick: one safegcd inversion per
+// lane, 3 multiplications per record.
 template <class N>
-BH_HD void stage_inv(const Work& w, uint32_t lo, uint32_t hi) {
+BH_HD void stage_inv(const Work& w, uint32_t c, uint32_t stride, uint32_t n) {
+  // lane c owns records c, c + stride, c + 2 stride, ... (< n): consecutive
+  // lanes touch consecutive records, so every limb access is coalesced
   uint32_t acc[8], x[8];
   load_const8(acc, N::r1);
-  for (uint32_t i = lo; i < hi; i++) {
-    st8(w.pre, i, w.ns, acc);  // prefix of records < i
+  uint32_t last = c;
+  for (uint32_t i = c; i < n; i += stride) {
+    st8(w.pre, i, w.ns, acc);  // prefix of this lane's earlier records
     ld8(x, w.sm, i, w.ns);
     mont_mul<N>(acc, acc, x);
+    last = i;
   }
+  if (c >= n) return;
   uint32_t inv[8];
-  mont_inv<N>(inv, acc);  // (prod s_i)^-1 * R
-  for (uint32_t i = hi; i-- > lo;) {
+  mont_inv_sg<N>(inv, acc);  // (prod s_i)^-1 * R
+  for (uint32_t i = last;; i -= stride) {
     uint32_t pre[8], wi[8], t[8];
     ld8(pre, w.pre, i, w.ns);
     mont_mul<N>(wi, inv, pre);  // s_i^-1 * R
@@ -344,6 +349,7 @@ BH_HD void stage_inv(const Work& w, uint32_t lo, uint32_t hi) {
     ld8(t, w.r, i, w.ns);
     mont_mul<N>(t, t, wi);      // u2 = r * w (plain)
     st8(w.r, i, w.ns, t);
+    if (i < c + stride) break;
   }
 }
 

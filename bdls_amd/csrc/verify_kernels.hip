@@ -2,7 +2,7 @@
 //
 // Launch structure per batch (one stream; see seq() below and bdls_hip.cpp):
 //   k_prep        1 lane/record   parse / checks / SHA-256 / Montgomery inputs
-//   k_inv         1 lane/chunk    batched s^-1 mod n, u1, u2
+//   k_inv         1 lane/chunk    batched s^-1 mod n (safegcd), u1, u2
 //   k_key_insert / k_key_count / k_key_plan / k_split
 //                 1 lane/record   registry lookup, dedup of the other keys,
 //                                 per-batch tables for keys used >= min_uses
@@ -33,12 +33,10 @@ __global__ __launch_bounds__(256) void k_prep(IN in, Work w, uint32_t n) {
 }
 
 template <class N>
-__global__ __launch_bounds__(256) void k_inv(Work w, uint32_t n, uint32_t chunk) {
+__global__ __launch_bounds__(256) void k_inv(Work w, uint32_t n, uint32_t lanes) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t lo = (uint64_t)c * chunk;
-  if (lo >= n) return;
-  const uint64_t hi = lo + chunk < n ? lo + chunk : n;
-  stage_inv<N>(w, (uint32_t)lo, (uint32_t)hi);
+  if (c >= lanes) return;
+  stage_inv<N>(w, c, lanes, n);
 }
 
 // ---- key lookup / dedup / plan ----------------------------------------------
@@ -303,8 +301,8 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
                       uint8_t* reason, hipStream_t s, hipEvent_t* ev) {
   const dim3 blk(256);
   const dim3 grd((n + 255) / 256);
-  const uint32_t nchunks = (n + o.inv_chunk - 1) / o.inv_chunk;
-  const dim3 grc((nchunks + 255) / 256);
+  const uint32_t nlanes = (n + o.inv_chunk - 1) / o.inv_chunk;  // records per lane ~ inv_chunk
+  const dim3 grc((nlanes + 255) / 256);
   hipError_t e;
 #define REC(k)                                                 \
   if (ev) {                                                    \
@@ -314,7 +312,7 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   REC(0);
   hipLaunchKernelGGL((k_prep<P, N, C, IN>), grd, blk, 0, s, in, w, n);
   REC(1);
-  hipLaunchKernelGGL((k_inv<N>), grc, blk, 0, s, w, n, o.inv_chunk);
+  hipLaunchKernelGGL((k_inv<N>), grc, blk, 0, s, w, n, nlanes);
   REC(2);
   hipLaunchKernelGGL(k_key_insert, grd, blk, 0, s, w, pl, g, n);
   hipLaunchKernelGGL(k_key_count, grd, blk, 0, s, w, pl, n);

@@ -4,7 +4,8 @@
  *   config 2: n records, `nkeys` distinct P-256 keys, `msg_len`-byte random
  *             messages (fused SHA-256), 1/`corrupt_den` of the records
  *             corrupted over the eleven classes below, seeded.
- *   config 5: nkeys == n (one distinct key per record).
+ *   config 5: nkeys >= n: record i signs with key i (one distinct key per
+ *             record, no reuse anywhere in the batch).
  * Signing follows bccsp/sw/ecdsa.go:27-39 (signECDSA: ecdsa.Sign, ToLowS, DER)
  * with a seeded nonce so every batch is reproducible. OpenSSL libcrypto
  * provides k*G / d*G on the host; this is data preparation, outside every
@@ -102,7 +103,8 @@ static void *gen_worker(void *arg) {
   for (size_t i = j->lo; i < j->hi; i++) {
     uint64_t st = j->seed * 0x100000001b3ull + i * 0x9e3779b97f4a7c15ull + 17;
     splitmix(&st);
-    const int key = (int)(splitmix(&st) % (uint64_t)j->nkeys);
+    const uint64_t kr = splitmix(&st);
+    const int key = (size_t)j->nkeys >= j->n ? (int)i : (int)(kr % (uint64_t)j->nkeys);
     int cls = C_NONE;
     if (j->corrupt_den > 0 && splitmix(&st) % (uint64_t)j->corrupt_den == 0)
       cls = 1 + (int)(splitmix(&st) % (C_NUM - 1));

@@ -172,6 +172,14 @@ int bh_memcpy_h2d(int device, void *dst, const void *src, size_t bytes);
 int bh_memcpy_d2h(int device, void *dst, const void *src, size_t bytes);
 int bh_sync(int device); /* wait for all work queued on the device's library stream */
 
+/* Deferred stage timing for pipelined callers: after bh_timing_begin, every
+ * pass on `device` that is given no bh_timing records HIP events around its
+ * stages on its launch stream WITHOUT synchronising; bh_timing_end waits for
+ * those events and returns the stage times summed over the passes since
+ * begin (routing counts and lanes of the last pass). */
+int bh_timing_begin(int device);
+int bh_timing_end(int device, bh_timing *timing);
+
 /* ---- key registry ---------------------------------------------------------
  * Per device and curve, a persistent store of per-key fixed-base tables
  * (65 x 8 multiples of Q, 56 KiB per key in HBM). A record whose public key

@@ -87,7 +87,8 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
   w.qtab = p;
   w.st = st.data();
   for (uint32_t i = 0; i < n; i++) stage_prep<P, N, C>(in, w, i);
-  for (uint32_t lo = 0; lo < n; lo += chunk) stage_inv<N>(w, lo, lo + chunk < n ? lo + chunk : n);
+  const uint32_t lanes = (n + chunk - 1) / chunk;
+  for (uint32_t c = 0; c < lanes; c++) stage_inv<N>(w, c, lanes, n);
   // dedup: representative = first record with an equal key
   std::vector<uint32_t> rep(n, kNone), cnt(n, 0);
   std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;
@@ -183,4 +184,17 @@ extern "C" void hs_f_sqr(const uint32_t* a, uint32_t* r) { f_sqr<F30_p256>(r, a)
 extern "C" void hs_bdls_hash(uint32_t version, const uint8_t* x32, const uint8_t* y32,
                              const uint8_t* msg, uint32_t mlen, uint8_t* out) {
   bdls_signed_proto_hash(out, version, x32, y32, msg, mlen);
+}
+
+// ---- scalar-field inversion probes (tests/test_field30.py) ----
+extern "C" void hs_n_inv(int curve, const uint32_t* a, uint32_t* r) {
+  if (curve == 0) mod_inv_sg<Fn_p256>(r, a);
+  else mod_inv_sg<Fn_k1>(r, a);
+}
+extern "C" void hs_n_mont_inv(int curve, const uint32_t* a, uint32_t* r) {
+  if (curve == 0) mont_inv_sg<Fn_p256>(r, a);
+  else mont_inv_sg<Fn_k1>(r, a);
+}
+extern "C" void hs_sha256(const uint8_t* msg, uint32_t len, uint32_t* out) {
+  sha256_msg(out, msg, len);
 }

@@ -1,0 +1,60 @@
+"""CPU: the device hash code (bdls_amd/csrc/sha256.h, blake2b.h -- dword loads
+with funnel shifts at any byte alignment) compiled for the host by the
+test-only harness, against hashlib on every length across the block edges,
+large messages, and all four pointer alignments."""
+import ctypes
+import hashlib
+import os
+import random
+import struct
+
+import pytest
+
+from tests.conftest import ROOT
+
+LIB = os.path.join(ROOT, "tests", "native", "build", "libhostsim.so")
+LENS = list(range(0, 300)) + [511, 512, 513, 1023, 1024, 1025, 4096, 4097, 13_337]
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not os.path.exists(LIB):
+        pytest.skip("hostsim not built")
+    return ctypes.CDLL(LIB)
+
+
+def placed(msg, align):
+    """msg copied at byte offset `align` of a fresh buffer (end of allocation
+    right after the message, so over-reads would be visible to ASan builds)."""
+    buf = ctypes.create_string_buffer(b"\xee" * align + msg, align + len(msg))
+    return buf, ctypes.cast(ctypes.addressof(buf) + align, ctypes.c_void_p)
+
+
+@pytest.mark.parametrize("align", [0, 1, 2, 3])
+def test_sha256(L, align):
+    rng = random.Random(align)
+    out = (ctypes.c_uint32 * 8)()
+    for n in LENS:
+        m = rng.randbytes(n)
+        buf, p = placed(m, align)
+        L.hs_sha256(p, n, out)
+        got = b"".join(struct.pack(">I", out[i]) for i in range(8))
+        assert got == hashlib.sha256(m).digest(), n
+
+
+@pytest.mark.parametrize("align", [0, 1, 2, 3])
+def test_bdls_blake2b(L, align):
+    # vendor/github.com/BDLS-bft/bdls/message.go:97-138 SignedProto.Hash framing
+    rng = random.Random(10 + align)
+    out = ctypes.create_string_buffer(32)
+    for n in LENS:
+        m = rng.randbytes(n)
+        x, y = rng.randbytes(32), rng.randbytes(32)
+        ver = rng.randrange(2**32)
+        buf, p = placed(m, align)
+        xb, xp = placed(x + y, align)
+        L.hs_bdls_hash(ctypes.c_uint32(ver), xp, ctypes.c_void_p(xp.value + 32), p,
+                       ctypes.c_uint32(n), out)
+        want = hashlib.blake2b(b"BDLS_CONSENSUS_SIGNATURE" + struct.pack("<I", ver) + x + y
+                               + struct.pack("<I", n) + m, digest_size=32).digest()
+        assert out.raw == want, n
