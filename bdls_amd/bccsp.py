@@ -25,7 +25,7 @@ from typing import Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import BH_F_HASH_SHA256, BH_F_NO_LOW_S, BhBatch
+from ._lib import BH_F_HASH_SHA256, BH_F_HASH_SHA3_256, BH_F_NO_LOW_S, BhBatch
 
 # reason codes (include/bdls_hip.h)
 R_OK, R_EMPTY_SIG, R_EMPTY_DIGEST, R_DER, R_R_NONPOS, R_S_NONPOS, R_HIGH_S = range(7)
@@ -82,6 +82,20 @@ class SHA256Opts:
     """bccsp/hashopts.go SHA256Opts."""
 
 
+class SHA3_256Opts:
+    """bccsp/hashopts.go SHA3_256Opts."""
+
+
+# msp/identities.go:219-227 getHashOpt: MSP SignatureHashFamily -> device hash flag
+_FAMILY_FLAG = {"SHA2": BH_F_HASH_SHA256, "SHA3": BH_F_HASH_SHA3_256}
+
+
+def family_flag(family: str) -> int:
+    if family not in _FAMILY_FLAG:
+        raise BCCSPError(-1, f"hash family not recognized [{family}]")
+    return _FAMILY_FLAG[family]
+
+
 def _arr(a: np.ndarray) -> int:
     return a.ctypes.data if a.size else 0
 
@@ -126,6 +140,8 @@ class HipCSP:
     # -- BCCSP.Hash (bccsp/sw/hash.go:29-33). Single-message hashing stays on the
     # host like sw; batched hashing is fused into BatchIdentityVerify on device.
     def hash(self, msg: bytes, opts=None) -> bytes:
+        if isinstance(opts, SHA3_256Opts):
+            return hashlib.sha3_256(msg).digest()
         return hashlib.sha256(msg).digest()
 
     def key_import(self, raw, opts) -> ECDSAPublicKey:
@@ -159,14 +175,15 @@ class HipCSP:
         return verify_packed(*pack_records(keys, signatures, digests), flags=self._flags)
 
     def batch_identity_verify(self, keys: Sequence[ECDSAPublicKey], messages: Sequence[bytes],
-                              signatures: Sequence[bytes]):
-        """msp/identities.go:170-199 for a whole batch with SHA-256 fused on device."""
+                              signatures: Sequence[bytes], family: str = "SHA2"):
+        """msp/identities.go:170-199 for a whole batch with the MSP's hash family
+        (SHA2 -> SHA-256, SHA3 -> SHA3-256) fused on device."""
         return verify_packed(*pack_records(keys, signatures, messages),
-                             flags=self._flags | BH_F_HASH_SHA256)
+                             flags=self._flags | family_flag(family))
 
-    def identity_verify(self, k, msg: bytes, sig: bytes) -> None:
+    def identity_verify(self, k, msg: bytes, sig: bytes, family: str = "SHA2") -> None:
         """identity.Verify: raises on error or invalid signature (returns None if valid)."""
-        valid, reason = self.batch_identity_verify([k], [msg], [sig])
+        valid, reason = self.batch_identity_verify([k], [msg], [sig], family)
         r = int(reason[0])
         if r in ERROR_REASONS:
             raise BCCSPError(r, "could not determine the validity of the signature: " +

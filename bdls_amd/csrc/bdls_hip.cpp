@@ -512,6 +512,14 @@ int check_curve(int curve) {
   return BH_OK;
 }
 
+int check_flags(uint32_t flags) {
+  constexpr uint32_t known = BH_F_HASH_SHA256 | BH_F_NO_LOW_S | BH_F_KEEP_KEYS | BH_F_HASH_SHA3_256;
+  if (flags & ~known) return fail(BH_E_INVALID, "unknown flag");
+  if ((flags & BH_F_HASH_SHA256) && (flags & BH_F_HASH_SHA3_256))
+    return fail(BH_E_INVALID, "BH_F_HASH_SHA256 and BH_F_HASH_SHA3_256 are exclusive");
+  return BH_OK;
+}
+
 // device >= 0: that device; -1: every initialised device.
 int for_devices(int device, const std::function<int(Dev&)>& fn) {
   std::vector<Dev*> ds;
@@ -587,6 +595,7 @@ int bh_verify_dev(int device, int curve, const bh_batch* b, size_t n, uint32_t f
                    !b->msg_off || !b->msg_len || !bitmap_words || !reason)))
     return fail(BH_E_INVALID, "null pointer in batch");
   if (curve != BH_CURVE_P256) return fail(BH_E_INVALID, "curve not supported by bh_verify_dev");
+  if (int rc = check_flags(flags)) return rc;
   if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
   Dev* d = get_dev(device);
   if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
@@ -606,6 +615,7 @@ int bh_verify(int curve, const bh_batch* b, size_t n, uint32_t flags, uint8_t* b
                    !bitmap || !reason)))
     return fail(BH_E_INVALID, "null pointer in batch");
   if (curve != BH_CURVE_P256) return fail(BH_E_INVALID, "curve not supported by bh_verify");
+  if (int rc = check_flags(flags)) return rc;
   if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
   return host_verify(curve, b, n, flags, bitmap, reason);
 }

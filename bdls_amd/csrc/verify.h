@@ -21,13 +21,18 @@
 #include "ec.h"
 #include "ec30.h"
 #include "sha256.h"
+#include "sha3.h"
 
 namespace bh {
 
 enum : uint32_t {
-  BHF_HASH_SHA256 = 1u,  // msg is a message: digest = SHA-256(msg) (identity.Verify)
-  BHF_NO_LOW_S = 2u,     // skip Fabric's low-S rule (plain Go ecdsa.Verify semantics)
+  BHF_HASH_SHA256 = 1u,    // msg is a message: digest = SHA-256(msg) (identity.Verify)
+  BHF_NO_LOW_S = 2u,       // skip Fabric's low-S rule (plain Go ecdsa.Verify semantics)
+  BHF_HASH_SHA3_256 = 8u,  // msg is a message: digest = SHA3-256(msg) (SHA3 hash family)
 };
+
+// Digest source of a verify record (compile-time, one k_prep instantiation each).
+enum : int { HK_GIVEN_OR_SHA256 = 0, HK_SHA3_256 = 1 };
 
 // Status byte kept per record between stages: low 7 bits = reason, bit 7 = r+n < p.
 enum : uint8_t { ST_R2OK = 0x80u };
@@ -149,14 +154,16 @@ BH_HD bool key_import(const uint8_t* q, uint32_t qx30[9], uint32_t qy30[9]) {
   return j_on_curve<P>(qx30, qy30);
 }
 
-template <class P, class N, class C>
+// HK: HK_GIVEN_OR_SHA256 (msg is the digest, or with BHF_HASH_SHA256 the
+// message) or HK_SHA3_256 (msg is the message, SHA3-256 digest).
+template <class P, class N, class C, int HK = HK_GIVEN_OR_SHA256>
 BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
   uint8_t reason = R_OK;
   uint32_t r[8], s[8], e[8];
   uint32_t qx30[9], qy30[9];
   const uint32_t slen = in.sig_len[i];
   const uint32_t mlen = in.msg_len[i];
-  const bool fused = (in.flags & BHF_HASH_SHA256) != 0;
+  const bool fused = HK == HK_SHA3_256 || (in.flags & BHF_HASH_SHA256) != 0;
   // impl.go:249-257: empty signature, then empty digest (a fused message always
   // has a 32-byte digest).
   if (slen == 0) reason = R_EMPTY_SIG;
@@ -180,7 +187,11 @@ BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
   // ---- digest -> e (hashToNat: left-most 32 bytes, reduced mod n)
   if (reason == R_OK) {
     const uint8_t* m = in.msg + in.msg_off[i];
-    if (fused) {
+    if constexpr (HK == HK_SHA3_256) {
+      uint8_t hb[32];
+      sha3_256_msg(hb, m, mlen);
+      be32_to_limbs(e, hb);  // hashToNat: the 32-byte digest, big-endian
+    } else if (fused) {
       uint32_t h[8];
       sha256_msg(h, m, mlen);
 #pragma unroll

@@ -19,17 +19,35 @@
 //   k_bitmap      1 lane/record   validity bitmap from the reason bytes
 // plus k_gtab_build once per device at bh_init (fixed-base comb table for G)
 // and k_reg_prep / k_reg_status for bh_keys_register.
+#include <type_traits>
+
 #include "verify.h"
 
 using namespace bh;
 
 namespace {
 
-template <class P, class N, class C, class IN>
+template <class P, class N, class C, class IN, int HK>
 __global__ __launch_bounds__(256) void k_prep(IN in, Work w, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  stage_prep<P, N, C>(in, w, i);
+  if constexpr (std::is_same_v<IN, BatchIn>) stage_prep<P, N, C, HK>(in, w, i);
+  else stage_prep<P, N, C>(in, w, i);
+}
+
+// Fabric records pick the digest source per batch (SHA3 family or not); BDLS
+// records always hash with BLAKE2b.
+template <class P, class N, class C>
+void launch_prep(const BatchIn& in, const Work& w, uint32_t n, dim3 grd, dim3 blk,
+                 hipStream_t s) {
+  if (in.flags & BHF_HASH_SHA3_256)
+    hipLaunchKernelGGL((k_prep<P, N, C, BatchIn, HK_SHA3_256>), grd, blk, 0, s, in, w, n);
+  else
+    hipLaunchKernelGGL((k_prep<P, N, C, BatchIn, HK_GIVEN_OR_SHA256>), grd, blk, 0, s, in, w, n);
+}
+template <class P, class N, class C>
+void launch_prep(const BdlsIn& in, const Work& w, uint32_t n, dim3 grd, dim3 blk, hipStream_t s) {
+  hipLaunchKernelGGL((k_prep<P, N, C, BdlsIn, 0>), grd, blk, 0, s, in, w, n);
 }
 
 template <class N>
@@ -310,7 +328,7 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   }
   if ((e = plan_reset(pl, s))) return e;
   REC(0);
-  hipLaunchKernelGGL((k_prep<P, N, C, IN>), grd, blk, 0, s, in, w, n);
+  launch_prep<P, N, C>(in, w, n, grd, blk, s);
   REC(1);
   hipLaunchKernelGGL((k_inv<N>), grc, blk, 0, s, w, n, nlanes);
   REC(2);

@@ -41,14 +41,17 @@ class Workload:
 
 
 def generate(n: int, nkeys: int, msg_len: int = 256, corrupt_den: int = 16, seed: int = 2,
-             nthreads: int | None = None) -> Workload:
+             nthreads: int | None = None, family: str = "SHA2") -> Workload:
+    """Records signed over Hash(msg) with the MSP hash family (SHA2: SHA-256,
+    SHA3: SHA3-256; msp/identities.go:219-227)."""
     if not os.path.exists(_LIB):
         raise RuntimeError(f"{_LIB} not built (run `make`)")
     L = ctypes.CDLL(_LIB)
     vp = ctypes.c_void_p
-    L.gen_p256.argtypes = [ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                           ctypes.c_uint64, ctypes.c_int] + [vp] * 9
-    L.gen_p256.restype = ctypes.c_int
+    L.gen_p256_family.argtypes = [ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_uint64, ctypes.c_int, ctypes.c_int] + [vp] * 9
+    L.gen_p256_family.restype = ctypes.c_int
+    fam = {"SHA2": 0, "SHA3": 1}[family]
     if nthreads is None:
         nthreads = min(16, os.cpu_count() or 1)
     w = Workload(
@@ -56,7 +59,7 @@ def generate(n: int, nkeys: int, msg_len: int = 256, corrupt_den: int = 16, seed
         msg_off=np.empty(n, np.uint64), msg_len=np.empty(n, np.uint32),
         sig=np.zeros(n * SIG_STRIDE, np.uint8), sig_off=np.empty(n, np.uint64),
         sig_len=np.empty(n, np.uint32), reason=np.empty(n, np.uint8), cls=np.empty(n, np.uint8))
-    rc = L.gen_p256(n, nkeys, msg_len, corrupt_den, seed, nthreads, w.pub.ctypes.data,
+    rc = L.gen_p256_family(n, nkeys, msg_len, corrupt_den, seed, nthreads, fam, w.pub.ctypes.data,
                     w.msg.ctypes.data, w.msg_off.ctypes.data, w.msg_len.ctypes.data,
                     w.sig.ctypes.data, w.sig_off.ctypes.data, w.sig_len.ctypes.data,
                     w.reason.ctypes.data, w.cls.ctypes.data)

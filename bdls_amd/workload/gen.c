@@ -17,6 +17,7 @@
 #include <openssl/bn.h>
 #include <openssl/ec.h>
 #include <openssl/obj_mac.h>
+#include <openssl/evp.h>
 #include <openssl/sha.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -86,6 +87,7 @@ typedef struct {
   uint8_t *pub, *msg, *sig, *reason, *cls;
   uint64_t *moff, *soff;
   uint32_t *mlen, *slen;
+  int family; /* 0 SHA2 (SHA-256), 1 SHA3 (SHA3-256): msp/identities.go:219-227 */
 } gjob;
 
 static void *gen_worker(void *arg) {
@@ -112,7 +114,8 @@ static void *gen_worker(void *arg) {
     rand_bytes(&st, m, j->msg_len);
     j->moff[i] = (uint64_t)i * j->msg_len;
     j->mlen[i] = (uint32_t)j->msg_len;
-    SHA256(m, j->msg_len, dg);
+    if (j->family == 1) EVP_Digest(m, j->msg_len, dg, NULL, EVP_sha3_256(), NULL);
+    else SHA256(m, j->msg_len, dg);
     /* sign: r = x(kG) mod n, s = k^-1 (e + r d) mod n, low-S */
     BN_bin2bn(j->keypriv + 32 * key, 32, d);
     BN_bin2bn(dg, 32, e);
@@ -207,9 +210,11 @@ static void *key_worker(void *arg) {
 
 /* Caller allocates: pub n*64, msg n*msg_len, sig n*80, moff/soff n u64,
  * mlen/slen n u32, reason/cls n u8. */
-int gen_p256(size_t n, int nkeys, int msg_len, int corrupt_den, uint64_t seed, int nthreads,
-             uint8_t *pub, uint8_t *msg, uint64_t *moff, uint32_t *mlen, uint8_t *sig,
-             uint64_t *soff, uint32_t *slen, uint8_t *reason, uint8_t *cls) {
+int gen_p256_family(size_t n, int nkeys, int msg_len, int corrupt_den, uint64_t seed,
+                    int nthreads, int family, uint8_t *pub, uint8_t *msg, uint64_t *moff,
+                    uint32_t *mlen, uint8_t *sig, uint64_t *soff, uint32_t *slen,
+                    uint8_t *reason, uint8_t *cls) {
+  if (family != 0 && family != 1) return -3;
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 128) nthreads = 128;
   if (nkeys < 1 || msg_len < 1) return -1;
@@ -233,7 +238,7 @@ int gen_p256(size_t n, int nkeys, int msg_len, int corrupt_den, uint64_t seed, i
     size_t lo = t * gper, hi = lo + gper > n ? n : lo + gper;
     if (lo >= hi) break;
     gj[t] = (gjob){lo, hi, n, seed, nkeys, msg_len, corrupt_den, kpub, kpriv,
-                   pub, msg, sig, reason, cls, moff, soff, mlen, slen};
+                   pub, msg, sig, reason, cls, moff, soff, mlen, slen, family};
     pthread_create(&th[t], NULL, gen_worker, &gj[t]);
     used++;
   }
@@ -241,6 +246,13 @@ int gen_p256(size_t n, int nkeys, int msg_len, int corrupt_den, uint64_t seed, i
   free(kpub);
   free(kpriv);
   return 0;
+}
+
+int gen_p256(size_t n, int nkeys, int msg_len, int corrupt_den, uint64_t seed, int nthreads,
+             uint8_t *pub, uint8_t *msg, uint64_t *moff, uint32_t *mlen, uint8_t *sig,
+             uint64_t *soff, uint32_t *slen, uint8_t *reason, uint8_t *cls) {
+  return gen_p256_family(n, nkeys, msg_len, corrupt_den, seed, nthreads, 0, pub, msg, moff, mlen,
+                         sig, soff, slen, reason, cls);
 }
 
 /* ---------------------------------------------------------------------------

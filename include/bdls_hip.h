@@ -57,6 +57,9 @@ extern "C" {
 #define BH_F_NO_LOW_S 2u    /* do not apply Fabric's low-S rule (plain crypto/ecdsa.Verify) */
 #define BH_F_KEEP_KEYS 4u   /* keys used >= 2 times in the batch get a table in the device's
                                key registry (kept across calls, see bh_keys_register) */
+#define BH_F_HASH_SHA3_256 8u /* msg[i] is a message; digest = SHA3-256(msg[i]): identity.Verify
+                                 of an MSP with SignatureHashFamily SHA3 (msp/identities.go:
+                                 219-227, bccsp/sw/new.go:72). Exclusive with BH_F_HASH_SHA256. */
 
 #define BH_CURVE_P256 0
 #define BH_CURVE_SECP256K1 1

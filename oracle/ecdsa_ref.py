@@ -431,9 +431,20 @@ def csp_verify(c: Curve, qx: int, qy: int, sig: bytes, digest: bytes):
     return reason == R_OK, reason
 
 
-def identity_verify(c: Curve, qx: int, qy: int, msg: bytes, sig: bytes):
-    """msp/identities.go:170-199: digest = SHA-256(msg) (SHA2 family), then Verify."""
-    return csp_verify(c, qx, qy, sig, hashlib.sha256(msg).digest())
+def identity_verify(c: Curve, qx: int, qy: int, msg: bytes, sig: bytes, family: str = "SHA2"):
+    """msp/identities.go:170-199: digest = Hash(msg) with the MSP's hash family
+    (getHashOpt :219-227: SHA2 -> SHA-256, SHA3 -> SHA3-256, the sha3.New256 of
+    bccsp/sw/new.go:72), then Verify."""
+    return csp_verify(c, qx, qy, sig, family_digest(family, msg))
+
+
+def family_digest(family: str, msg: bytes) -> bytes:
+    """bccsp/sw/new.go:70-72 hashers for identity.getHashOpt (identities.go:219-227)."""
+    if family == "SHA2":
+        return hashlib.sha256(msg).digest()
+    if family == "SHA3":
+        return hashlib.sha3_256(msg).digest()
+    raise ValueError(f"hash family not recognized [{family}]")
 
 
 # ----------------------------------------------------------------------------

@@ -24,6 +24,7 @@
 #include <openssl/bn.h>
 #include <openssl/ec.h>
 #include <openssl/ecdsa.h>
+#include <openssl/evp.h>
 #include <openssl/obj_mac.h>
 #include <openssl/sha.h>
 #include <pthread.h>
@@ -280,7 +281,10 @@ static void *worker(void *arg) {
     const uint8_t *m = j->msg + j->moff[i];
     size_t ml = j->mlen[i];
     if (j->fused) { /* msp/identities.go:179 Hash then :190 Verify */
-      SHA256(m, ml, dg);
+      if (j->fused == 2) /* SHA3 family: sha3.New256, bccsp/sw/new.go:72 */
+        EVP_Digest(m, ml, dg, NULL, EVP_sha3_256(), NULL);
+      else
+        SHA256(m, ml, dg);
       m = dg;
       ml = 32;
     }
@@ -290,8 +294,9 @@ static void *worker(void *arg) {
   return NULL;
 }
 
-/* Batch: fused != 0 -> msg is hashed with SHA-256 first (identity.Verify);
- * fused == 0 -> msg is the digest (CSP.Verify). reason[i] == 0 <=> valid. */
+/* Batch: fused == 1 -> msg is hashed with SHA-256 first (identity.Verify,
+ * SHA2 family); fused == 2 -> with SHA3-256 (SHA3 family); fused == 0 -> msg
+ * is the digest (CSP.Verify). reason[i] == 0 <=> valid. */
 int orc_batch_verify(int curve, int fused, size_t n, const uint8_t *q, const uint8_t *msg,
                      const uint64_t *moff, const uint32_t *mlen, const uint8_t *sig,
                      const uint64_t *soff, const uint32_t *slen, uint8_t *reason, int nthreads) {

@@ -62,9 +62,10 @@ def unmarshal(sig: bytes):
 
 
 def batch_verify(q: np.ndarray, msg: np.ndarray, moff: np.ndarray, mlen: np.ndarray,
-                 sig: np.ndarray, soff: np.ndarray, slen: np.ndarray, fused: bool = True,
+                 sig: np.ndarray, soff: np.ndarray, slen: np.ndarray, fused=True,
                  nthreads: int = 1, curve: int = P256) -> np.ndarray:
-    """Returns the reason code per record (0 = valid)."""
+    """Returns the reason code per record (0 = valid). fused: False (msg is the
+    digest), True / "SHA2" (SHA-256 of msg), "SHA3" (SHA3-256 of msg)."""
     n = len(mlen)
     reason = np.zeros(n, dtype=np.uint8)
     q = np.ascontiguousarray(q, dtype=np.uint8)
@@ -74,7 +75,8 @@ def batch_verify(q: np.ndarray, msg: np.ndarray, moff: np.ndarray, mlen: np.ndar
     sig = np.ascontiguousarray(sig, dtype=np.uint8)
     soff = np.ascontiguousarray(soff, dtype=np.uint64)
     slen = np.ascontiguousarray(slen, dtype=np.uint32)
-    lib().orc_batch_verify(curve, 1 if fused else 0, n, q.ctypes.data, msg.ctypes.data,
+    mode = {False: 0, True: 1, "SHA2": 1, "SHA3": 2}[fused]
+    lib().orc_batch_verify(curve, mode, n, q.ctypes.data, msg.ctypes.data,
                            moff.ctypes.data, mlen.ctypes.data, sig.ctypes.data,
                            soff.ctypes.data, slen.ctypes.data, reason.ctypes.data, nthreads)
     return reason

@@ -4,6 +4,7 @@
 // no GPU. Never linked into libbdlship.so; the product path has no CPU fallback.
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -86,7 +87,14 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
   p += 9 * ns;
   w.qtab = p;
   w.st = st.data();
-  for (uint32_t i = 0; i < n; i++) stage_prep<P, N, C>(in, w, i);
+  for (uint32_t i = 0; i < n; i++) {
+    if constexpr (std::is_same_v<IN, BatchIn>) {
+      if (in.flags & BHF_HASH_SHA3_256) stage_prep<P, N, C, HK_SHA3_256>(in, w, i);
+      else stage_prep<P, N, C>(in, w, i);
+    } else {
+      stage_prep<P, N, C>(in, w, i);
+    }
+  }
   const uint32_t lanes = (n + chunk - 1) / chunk;
   for (uint32_t c = 0; c < lanes; c++) stage_inv<N>(w, c, lanes, n);
   // dedup: representative = first record with an equal key
@@ -197,4 +205,7 @@ extern "C" void hs_n_mont_inv(int curve, const uint32_t* a, uint32_t* r) {
 }
 extern "C" void hs_sha256(const uint8_t* msg, uint32_t len, uint32_t* out) {
   sha256_msg(out, msg, len);
+}
+extern "C" void hs_sha3_256(const uint8_t* msg, uint32_t len, uint8_t* out) {
+  sha3_256_msg(out, msg, len);
 }

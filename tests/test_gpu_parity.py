@@ -76,6 +76,37 @@ def test_unique_keys(csp):
     assert (reason == w.reason).all()
 
 
+def test_sha3_family(csp):
+    """SHA3 hash family (msp/identities.go:219-227 -> sha3.New256): fused
+    SHA3-256 on device, every corruption class, message lengths across the
+    136-byte rate; also through identity_verify(family="SHA3")."""
+    from bdls_amd import workload
+    from oracle import orc
+    for L in (135, 136, 137, 300):
+        w = workload.generate(3000, 200, L, 8, seed=30 + L, family="SHA3")
+        valid, reason = verify_packed(*w.arrays(), flags=_lib.BH_F_HASH_SHA3_256)
+        assert (reason == w.reason).all(), L
+        assert (valid == w.expected_valid).all(), L
+        got = orc.batch_verify(w.pub.reshape(-1, 64), w.msg, w.msg_off, w.msg_len, w.sig,
+                               w.sig_off, w.sig_len, fused="SHA3", nthreads=4)
+        assert (got == reason).all(), L
+    i = int(np.flatnonzero(w.reason == 0)[0])
+    k = ECDSAPublicKey(int.from_bytes(bytes(w.pub[64 * i:64 * i + 32]), "big"),
+                       int.from_bytes(bytes(w.pub[64 * i + 32:64 * i + 64]), "big"))
+    m = bytes(w.msg[w.msg_off[i]:w.msg_off[i] + w.msg_len[i]])
+    sg = bytes(w.sig[w.sig_off[i]:w.sig_off[i] + w.sig_len[i]])
+    csp.identity_verify(k, m, sg, family="SHA3")
+    with pytest.raises(BCCSPError):
+        csp.identity_verify(k, m, sg, family="SHA2")
+
+
+def test_hash_flags_exclusive(csp):
+    with pytest.raises(_lib.EngineError):
+        verify_packed(*pack([], False), flags=_lib.BH_F_HASH_SHA256 | _lib.BH_F_HASH_SHA3_256)
+    with pytest.raises(_lib.EngineError):
+        verify_packed(*pack([], False), flags=0x100)
+
+
 def test_device_api(csp):
     """bh_verify_dev on HBM-resident buffers (library-owned device memory)."""
     from bdls_amd import workload

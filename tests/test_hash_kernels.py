@@ -58,3 +58,16 @@ def test_bdls_blake2b(L, align):
         want = hashlib.blake2b(b"BDLS_CONSENSUS_SIGNATURE" + struct.pack("<I", ver) + x + y
                                + struct.pack("<I", n) + m, digest_size=32).digest()
         assert out.raw == want, n
+
+
+@pytest.mark.parametrize("align", [0, 1, 2, 3])
+def test_sha3_256(L, align):
+    # bccsp/sw/new.go:72 sha3.New256 (SHA3 family, msp/identities.go:219-227);
+    # lengths straddle the 136-byte rate: 135/136/137, 271/272/273, ...
+    rng = random.Random(20 + align)
+    out = ctypes.create_string_buffer(32)
+    for n in LENS + [135, 136, 137, 271, 272, 273, 407, 408, 409]:
+        m = rng.randbytes(n)
+        buf, p = placed(m, align)
+        L.hs_sha3_256(p, ctypes.c_uint32(n), out)
+        assert out.raw == hashlib.sha3_256(m).digest(), n

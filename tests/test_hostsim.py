@@ -93,3 +93,19 @@ def test_hostsim_workload_mixed_paths(hs):
     out, ncomb = run2(hs, w.arrays(), True, 4)
     assert 0 < ncomb < w.n
     assert (out == w.reason).all()
+
+
+def test_hostsim_workload_sha3(hs):
+    """SHA3 hash family (msp/identities.go:219-227): records signed over
+    SHA3-256(msg); the SHA-256 flag must reject the valid ones."""
+    from bdls_amd import workload
+    from bdls_amd._lib import BH_F_HASH_SHA3_256
+    w = workload.generate(300, 40, 300, 4, seed=13, nthreads=4, family="SHA3")
+    pub, sig, so, sl, msg, mo, ml = w.arrays()
+    out = np.zeros(w.n, np.uint8)
+    hs.hs_verify(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
+                 msg.ctypes.data, mo.ctypes.data, ml.ctypes.data, w.n, BH_F_HASH_SHA3_256, 8,
+                 out.ctypes.data)
+    assert (out == w.reason).all()
+    out2 = run(hs, w.arrays(), True, 8)
+    assert (out2[w.reason == 0] != 0).all()
