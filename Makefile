@@ -19,7 +19,11 @@ $(LIB)/bdls_hip.o: $(CSRC)/bdls_hip.cpp $(HDRS)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB)/libbdlship.so: $(LIB)/verify_kernels.o $(LIB)/bdls_hip.o
+$(LIB)/bdls_msg.o: $(CSRC)/bdls_msg.cpp include/bdls_hip.h
+	@mkdir -p $(LIB)
+	g++ -O2 -std=c++17 -fPIC -Wall -c $< -o $@
+
+$(LIB)/libbdlship.so: $(LIB)/verify_kernels.o $(LIB)/bdls_hip.o $(LIB)/bdls_msg.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
 $(LIB)/libbdlsgen.so: bdls_amd/workload/gen.c

@@ -59,6 +59,14 @@ class BhTiming(ctypes.Structure):
     STAGES = ("prep_ms", "inv_ms", "plan_ms", "build_ladder_ms", "publish_ms", "keycomb_ms")
 
 
+class BhBdlsMsgResult(ctypes.Structure):
+    """include/bdls_hip.h bh_bdls_msg_result."""
+    _fields_ = [("status", ctypes.c_int32), ("bad_sp", ctypes.c_int32),
+                ("type", ctypes.c_uint32), ("distinct_signers", ctypes.c_uint32),
+                ("height", ctypes.c_uint64), ("round", ctypes.c_uint64),
+                ("sp_first", ctypes.c_uint32), ("sp_count", ctypes.c_uint32)]
+
+
 class EngineError(RuntimeError):
     """The HIP engine itself failed (no device, HIP error, bad arguments)."""
 
@@ -121,6 +129,9 @@ def lib() -> ctypes.CDLL:
         L.bh_keys_clear.restype = i32
         L.bh_keys_count.argtypes = [i32, i32, ctypes.POINTER(sz)]
         L.bh_keys_count.restype = i32
+        L.bh_bdls_preverify.argtypes = [i32, vp, vp, vp, sz, vp, sz, u32, vp, vp, sz,
+                                        ctypes.POINTER(sz)]
+        L.bh_bdls_preverify.restype = i32
         _lib = L
     return _lib
 

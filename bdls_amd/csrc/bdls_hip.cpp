@@ -44,6 +44,14 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+}  // namespace
+
+namespace bh {
+int host_fail(int code, const char* msg) { return fail(code, msg); }
+}  // namespace bh
+
+namespace {
+
 #define HIPCHK(expr)                                                                      \
   do {                                                                                    \
     hipError_t e_ = (expr);                                                               \

@@ -166,6 +166,82 @@ int bh_verify_bdls_dev(int device, int curve, const bh_bdls_batch *b, size_t n,
                        uint64_t *bitmap_words, uint8_t *reason, void *stream, int sync,
                        bh_timing *timing);
 
+/* ---- BDLS drained-batch pre-verification ------------------------------------
+ * Replaces the per-message signature work of agent-tcp/tcp_peer.go:176-192
+ * (inputConsensusMessage drains the queued raw messages and calls
+ * Consensus.ReceiveMessage one by one) with ONE device batch: every
+ * SignedProto reachable from the drained messages -- the outer one, each
+ * Message.Proof of a <lock>/<select>/<decide>, Message.LockRelease and the
+ * proofs of the <lock> it embeds, and (recursively, depth <= 8) the proofs a
+ * <resync> pushes to the loopback -- is decoded (gogo/protobuf wire format,
+ * message.pb.go Unmarshal semantics), gated on the participant set
+ * (consensus.go:449-470) and verified with SignedProto.Verify semantics.
+ *
+ * results[i].status is the first failure among the checks that depend only on
+ * the message bytes and the participant list, in the order Go runs them
+ * (receiveMessage :1209-1226, verifyMessage :449-493, verifyLockMessage
+ * :520-600, verifySelectMessage :628-728, verifyDecideMessage :829-902,
+ * verifyLockReleaseMessage :604-623). Checks that need consensus state or
+ * callbacks (height/round against the current round, StateValidate,
+ * StateCompare, MessageValidator, the lock-release stage) are left to the
+ * caller: status != BH_BDLS_OK means Go rejects the message for certain;
+ * BH_BDLS_OK means the signature layer and proof structure pass. The quorum
+ * checks (2t+1 proofs to the proposed state, <select> proposal counts) use
+ * the default Config.StateHash (BLAKE2b-256 of the state, consensus.go:41);
+ * pass BH_BDLS_F_NO_QUORUM with a custom StateHash.
+ *
+ * sp_reason (optional unless BH_BDLS_F_GIVEN_REASONS): one byte per decoded
+ * SignedProto, message by message in the order [outer, proofs..., LockRelease,
+ * its proofs..., resync sub-messages...] (results[i].sp_first / sp_count):
+ * BH_R_OK, a BH_R_* reject, or BH_SP_NOT_VERIFIED (signer not a participant,
+ * or the outer version is wrong). These feed a verified-signature cache that
+ * the unchanged ReceiveMessage then consults.
+ * *sp_total (required) receives the number of decoded SignedProtos; with
+ * sp_reason != NULL and sp_cap < *sp_total the call fails with BH_E_INVALID
+ * before any device work (call again with a larger buffer). */
+#define BH_BDLS_F_GIVEN_REASONS 1u /* sp_reason is INPUT (e.g. cache hits): no device work */
+#define BH_BDLS_F_NO_QUORUM 2u     /* skip the StateHash-based quorum checks */
+#define BH_SP_NOT_VERIFIED 255
+
+#define BH_BDLS_OK 0
+#define BH_BDLS_DECODE 1                    /* proto.Unmarshal(SignedProto) failed, :1212 */
+#define BH_BDLS_VERSION 2                   /* ErrMessageVersion, :1218 */
+#define BH_BDLS_UNKNOWN_PARTICIPANT 3       /* ErrMessageUnknownParticipant, :469 */
+#define BH_BDLS_BAD_SIGNATURE 4             /* ErrMessageSignature, :486 */
+#define BH_BDLS_MSG_DECODE 5                /* proto.Unmarshal(Message) failed, :490 */
+#define BH_BDLS_UNKNOWN_TYPE 6              /* ErrMessageUnknownMessageType */
+#define BH_BDLS_EMPTY_STATE 7               /* Err{Lock,Decide}EmptyState */
+#define BH_BDLS_NOT_LEADER 8                /* Err{Lock,Select,Decide}NotSignedByLeader */
+#define BH_BDLS_PROOF_UNKNOWN_PARTICIPANT 9 /* Err*ProofUnknownParticipant */
+#define BH_BDLS_PROOF_BAD_SIGNATURE 10      /* ErrMessageSignature from a proof */
+#define BH_BDLS_PROOF_DECODE 11             /* a proof's Message does not decode */
+#define BH_BDLS_PROOF_TYPE_MISMATCH 12      /* Err*ProofTypeMismatch */
+#define BH_BDLS_PROOF_HEIGHT_MISMATCH 13    /* Err*ProofHeightMismatch */
+#define BH_BDLS_PROOF_ROUND_MISMATCH 14     /* Err*ProofRoundMismatch */
+#define BH_BDLS_PROOF_INSUFFICIENT 15       /* Err{Lock,Select,Decide}ProofInsufficient */
+#define BH_BDLS_SELECT_STATE_MISMATCH 16    /* ErrSelectStateMismatch */
+#define BH_BDLS_SELECT_PROOF_EXCEEDED 17    /* ErrSelectProofExceeded */
+#define BH_BDLS_LOCKRELEASE_EMPTY 18        /* ErrMessageIsEmpty (nil LockRelease) */
+
+typedef struct bh_bdls_msg_result {
+  int32_t status;            /* BH_BDLS_* */
+  int32_t bad_sp;            /* SignedProto (relative to sp_first) that failed, or -1 */
+  uint32_t type;             /* Message.Type (valid from status >= BH_BDLS_UNKNOWN_TYPE or OK) */
+  uint32_t distinct_signers; /* distinct participants among the checked proofs */
+  uint64_t height;           /* Message.Height */
+  uint64_t round;            /* Message.Round */
+  uint32_t sp_first;         /* first SignedProto of this message in sp_reason */
+  uint32_t sp_count;
+} bh_bdls_msg_result;
+
+/* msgs/msg_off/msg_len: n raw SignedProto encodings (host). participants:
+ * n_participants * 64 bytes, Identity = X || Y (Config.Participants order,
+ * which defines roundLeader). curve: BH_CURVE_SECP256K1 or BH_CURVE_P256. */
+int bh_bdls_preverify(int curve, const uint8_t *msgs, const uint64_t *msg_off,
+                      const uint32_t *msg_len, size_t n, const uint8_t *participants,
+                      size_t n_participants, uint32_t flags, bh_bdls_msg_result *results,
+                      uint8_t *sp_reason, size_t sp_cap, size_t *sp_total);
+
 /* ---- device buffers on an initialised device (callers that keep batches
  * resident in HBM, e.g. bench.py; the library owns the HIP runtime so callers
  * never mix runtimes). Copies are synchronous on the device's stream. ---- */
