@@ -26,7 +26,7 @@ EXPORTS = (
     "bh_workspace_bytes", "bh_verify", "bh_verify_dev", "bh_csp_verify_p256",
     "bh_parse_der_sig", "bh_dev_alloc", "bh_dev_free", "bh_memcpy_h2d", "bh_memcpy_d2h",
     "bh_sync", "bh_verify_bdls", "bh_verify_bdls_dev", "bh_keys_reserve", "bh_keys_register",
-    "bh_keys_clear", "bh_keys_count", "bh_timing_begin", "bh_timing_end",
+    "bh_keys_clear", "bh_keys_count", "bh_timing_begin", "bh_timing_end", "bh_bdls_preverify",
 )
 KEY_FULL = 255  # bh_keys_register status: registry full
 
