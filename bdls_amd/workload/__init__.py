@@ -153,3 +153,31 @@ def generate_block(ntx: int = 500, endorsements: int = 3, norgs: int = 4, nclien
     creators = generate(ntx, nclients, creator_len, corrupt_den, seed=seed * 7 + 1)
     endorse = generate(ntx * endorsements, norgs, endorse_len, corrupt_den, seed=seed * 7 + 2)
     return concat([creators, endorse])
+
+
+def generate_bdls_wire_round(nval: int = 100, curve: int = 1, seed: int = 4):
+    """One BDLS round as raw wire messages (SignedProto encodings) for
+    bh_bdls_preverify: nval <roundchange>, the leader's <lock> with 2t+1
+    proofs, nval <commit>, the leader's <decide> with 2t+1 proofs, all valid.
+    Returns (participants: list of 64-byte X||Y, messages: list of bytes)."""
+    if not os.path.exists(_LIB):
+        raise RuntimeError(f"{_LIB} not built (run `make`)")
+    L = ctypes.CDLL(_LIB)
+    vp = ctypes.c_void_p
+    L.gen_bdls_wire_round.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                      vp, vp, ctypes.c_uint64, vp, vp]
+    L.gen_bdls_wire_round.restype = ctypes.c_int
+    t2p1 = 2 * ((nval - 1) // 3) + 1
+    cnt = 2 * nval + 2
+    parts = np.zeros(nval * 64, np.uint8)
+    cap = cnt * 512 + 2 * t2p1 * 512
+    out = np.zeros(cap, np.uint8)
+    off = np.zeros(cnt, np.uint64)
+    ln = np.zeros(cnt, np.uint32)
+    rc = L.gen_bdls_wire_round(curve, nval, t2p1, seed, parts.ctypes.data, out.ctypes.data, cap,
+                               off.ctypes.data, ln.ctypes.data)
+    if rc != cnt:
+        raise RuntimeError(f"gen_bdls_wire_round failed: {rc}")
+    pb = parts.tobytes()
+    return ([pb[64 * i:64 * i + 64] for i in range(nval)],
+            [out[int(o):int(o) + int(l)].tobytes() for o, l in zip(off, ln)])

@@ -472,3 +472,114 @@ int gen_bdls_round(int curve, int nval, int t2p1, int small_len, uint64_t seed, 
   EC_GROUP_free(g);
   return rc;
 }
+
+/* ---------------------------------------------------------------------------
+ * BDLS round as raw wire messages (input of bh_bdls_preverify): SignedProto
+ * encodings (message.pb.go MarshalToSizedBuffer :300-356) of signed Messages
+ * (:358-): nval <roundchange> (Type 1) + the leader's <lock> (Type 2) with
+ * t2p1 roundchange proofs + nval <commit> (Type 4) + the leader's <decide>
+ * (Type 6) with t2p1 commit proofs. Height 1, round 0, so the leader is
+ * participant 0 (consensus.go roundLeader :1148-1154). All valid.
+ * ------------------------------------------------------------------------- */
+static size_t pb_varint(uint8_t *o, uint64_t v) {
+  size_t k = 0;
+  while (v >= 0x80) { o[k++] = (uint8_t)(v | 0x80); v >>= 7; }
+  o[k++] = (uint8_t)v;
+  return k;
+}
+
+static size_t pb_bytes(uint8_t *o, uint8_t tag, const uint8_t *b, size_t n) {
+  size_t k = 0;
+  o[k++] = tag;
+  k += pb_varint(o + k, n);
+  memcpy(o + k, b, n);
+  return k + n;
+}
+
+static size_t pb_signed(uint8_t *o, const sproto *s) { /* worst case 16 + ml + 2*34 + 2*35 */
+  size_t k = 0;
+  if (s->ver) { o[k++] = 0x08; k += pb_varint(o + k, s->ver); }
+  if (s->ml) k += pb_bytes(o + k, 0x12, s->msg, s->ml);
+  k += pb_bytes(o + k, 0x1a, s->x, 32);
+  k += pb_bytes(o + k, 0x22, s->y, 32);
+  if (s->rl) k += pb_bytes(o + k, 0x2a, s->r, s->rl);
+  if (s->sl) k += pb_bytes(o + k, 0x32, s->s, s->sl);
+  return k;
+}
+
+static size_t pb_message(uint8_t *o, uint32_t type, uint64_t h, uint64_t r, const uint8_t *st,
+                         size_t stl, const sproto *proofs, int np) {
+  size_t k = 0;
+  if (type) { o[k++] = 0x08; k += pb_varint(o + k, type); }
+  if (h) { o[k++] = 0x10; k += pb_varint(o + k, h); }
+  if (r) { o[k++] = 0x18; k += pb_varint(o + k, r); }
+  if (stl) k += pb_bytes(o + k, 0x22, st, stl);
+  for (int p = 0; p < np; p++) {
+    uint8_t tmp[1024];
+    size_t l = pb_signed(tmp, &proofs[p]);
+    k += pb_bytes(o + k, 0x2a, tmp, l);
+  }
+  return k;
+}
+
+/* parts: nval*64 (X || Y); out: cap bytes of raw messages; off/len: 2*nval+2.
+ * Returns the message count, or < 0. */
+int gen_bdls_wire_round(int curve, int nval, int t2p1, uint64_t seed, uint8_t *parts,
+                        uint8_t *out, uint64_t cap, uint64_t *off, uint32_t *len) {
+  if (nval < 1 || t2p1 > nval) return -1;
+  EC_GROUP *g = EC_GROUP_new_by_curve_name(curve == 0 ? NID_X9_62_prime256v1 : NID_secp256k1);
+  BN_CTX *ctx = BN_CTX_new();
+  BIGNUM *n = BN_new(), *px = BN_new(), *py = BN_new();
+  EC_GROUP_get_order(g, n, ctx);
+  EC_POINT *Q = EC_POINT_new(g);
+  BIGNUM **d = malloc(sizeof(BIGNUM *) * nval);
+  uint64_t st = seed * 0x9e3779b97f4a7c15ull + 0x3172ull;
+  for (int v = 0; v < nval; v++) {
+    d[v] = BN_new();
+    rand_scalar(&st, d[v], n, ctx);
+    EC_POINT_mul(g, Q, d[v], NULL, NULL, ctx);
+    EC_POINT_get_affine_coordinates(g, Q, px, py, ctx);
+    BN_bn2binpad(px, parts + 64 * (size_t)v, 32);
+    BN_bn2binpad(py, parts + 64 * (size_t)v + 32, 32);
+  }
+  uint8_t state[64];
+  rand_bytes(&st, state, sizeof state);
+  sproto *rc = calloc((size_t)nval, sizeof(sproto)), *cm = calloc((size_t)nval, sizeof(sproto));
+  uint8_t mb[256];
+  for (int v = 0; v < nval; v++) {
+    size_t ml = pb_message(mb, 1, 1, 0, state, sizeof state, NULL, 0);
+    sp_sign(&rc[v], g, ctx, d[v], parts + 64 * (size_t)v, parts + 64 * (size_t)v + 32, mb,
+            (uint32_t)ml, &st);
+    ml = pb_message(mb, 4, 1, 0, state, sizeof state, NULL, 0);
+    sp_sign(&cm[v], g, ctx, d[v], parts + 64 * (size_t)v, parts + 64 * (size_t)v + 32, mb,
+            (uint32_t)ml, &st);
+  }
+  const size_t big = 256 + (size_t)t2p1 * 512;
+  uint8_t *lm = malloc(big), *dm = malloc(big);
+  sproto lock, dec;
+  size_t ll = pb_message(lm, 2, 1, 0, state, sizeof state, rc, t2p1);
+  size_t dl = pb_message(dm, 6, 1, 0, state, sizeof state, cm, t2p1);
+  sp_sign(&lock, g, ctx, d[0], parts, parts + 32, lm, (uint32_t)ll, &st);
+  sp_sign(&dec, g, ctx, d[0], parts, parts + 32, dm, (uint32_t)dl, &st);
+  uint64_t pos = 0;
+  int k = 0, rc_ = 0;
+  const sproto *seq[4] = {rc, &lock, cm, &dec};
+  const int cnt[4] = {nval, 1, nval, 1};
+  for (int q = 0; q < 4 && rc_ == 0; q++)
+    for (int v = 0; v < cnt[q]; v++) {
+      const size_t need = 96 + seq[q][v].ml + 80;
+      if (pos + need > cap) { rc_ = -2; break; }
+      const size_t l = pb_signed(out + pos, &seq[q][v]);
+      off[k] = pos;
+      len[k] = (uint32_t)l;
+      pos += l;
+      k++;
+    }
+  for (int v = 0; v < nval; v++) { free(rc[v].msg); free(cm[v].msg); BN_free(d[v]); }
+  free(lock.msg); free(dec.msg); free(lm); free(dm); free(rc); free(cm); free(d);
+  EC_POINT_free(Q);
+  BN_free(n); BN_free(px); BN_free(py);
+  BN_CTX_free(ctx);
+  EC_GROUP_free(g);
+  return rc_ ? rc_ : k;
+}

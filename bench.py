@@ -188,6 +188,7 @@ def bench_latency(a, rank, world, local):
                                   st.ctypes.data))
     reg_ms = (time.perf_counter() - t) * 1e3
     warm = measure("warm")
+    wire = measure_wire(a, L, curve, rank) if a.config == 4 else None
     _lib.check(L.bh_keys_clear(-1, curve))
     p50 = dist.max_over_ranks(warm["host_p50"], world)
     parity_ok = dist.all_true(cold["parity"] and warm["parity"], world)
@@ -205,6 +206,9 @@ def bench_latency(a, rank, world, local):
         "latency_ms": {"warm": warm, "cold": cold,
                        "register_keys_ms": round(reg_ms, 3)},
     }
+    if wire is not None:
+        out["latency_ms"]["wire_preverify"] = wire
+        out["parity"] = parity_ok = dist.all_true(parity_ok and wire["parity"], world)
     if rank == 0 and a.cpu_baseline:
         from oracle import orc
         cpu = []
@@ -231,6 +235,43 @@ def bench_latency(a, rank, world, local):
         print(json.dumps(out), flush=True)
     dist.finalize(world)
     return 0 if parity_ok else 3
+
+
+def measure_wire(a, L, curve, rank):
+    """Config 4 through bh_bdls_preverify: the round as raw wire messages
+    (what agent-tcp's inputConsensusMessage drains), decoded, gated and
+    structurally checked on the host, every SignedProto verified in one device
+    batch (participants' keys registered, as for "warm")."""
+    from bdls_amd import _lib, workload
+    ids, raws = workload.generate_bdls_wire_round(a.validators, curve, seed=a.seed + 1000 * rank)
+    n = len(raws)
+    ln = np.array([len(m) for m in raws], np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(raws), np.uint8)
+    parts = np.frombuffer(b"".join(ids), np.uint8)
+    res = (_lib.BhBdlsMsgResult * n)()
+    cap = n + len(buf) // 2 + 1
+    rs = np.zeros(cap, np.uint8)
+    total = ctypes.c_size_t()
+
+    def call():
+        return L.bh_bdls_preverify(curve, buf.ctypes.data, off.ctypes.data, ln.ctypes.data, n,
+                                   parts.ctypes.data, len(ids), 0, res, rs.ctypes.data, cap,
+                                   ctypes.byref(total))
+    for _ in range(max(1, a.warmup)):
+        _lib.check(call())
+    ms = []
+    for _ in range(a.steps):
+        t = time.perf_counter()
+        _lib.check(call())
+        ms.append((time.perf_counter() - t) * 1e3)
+    t2p1 = 2 * ((a.validators - 1) // 3) + 1
+    ok = (total.value == 2 * a.validators + 2 * (1 + t2p1)
+          and all(res[i].status == 0 for i in range(n)) and not rs[:total.value].any())
+    return {"p50": round(percentile(ms, 50), 4), "p99": round(percentile(ms, 99), 4),
+            "messages": n, "wire_bytes": int(len(buf)), "signed_protos": int(total.value),
+            "parity": bool(ok)}
 
 
 def main():

@@ -189,3 +189,19 @@ def test_gpu_round_100_validators(curve):
     assert all(r["status"] == 0 for r in res)
     for r, o in zip(res, ores):
         assert {f: r[f] for f in FIELDS} == {f: getattr(o, f) for f in FIELDS}
+
+
+@pytest.mark.parametrize("curve,cname", [(1, "secp256k1"), (0, "P-256")])
+def test_wire_round_generator(curve, cname):
+    """workload/gen.c wire rounds (bench config 4) decode and verify as
+    all-valid under the oracle, and the native logic agrees."""
+    _lib_or_skip()
+    from bdls_amd import consensus, workload
+    ids, raws = workload.generate_bdls_wire_round(10, curve, seed=9)
+    res, rs = M.Preverifier(ids, CURVES[cname]).run(raws)
+    assert all(r.status == 0 for r in res) and set(rs) == {0}
+    t2p1 = 2 * 3 + 1
+    assert len(rs) == 2 * 10 + 2 * (1 + t2p1)
+    assert [r.distinct_signers for r in res if r.type in (2, 6)] == [t2p1, t2p1]
+    nres, nrs = consensus.preverify(cname, raws, ids, given_reasons=np.array(rs, np.uint8))
+    assert all(r["status"] == 0 for r in nres)
