@@ -108,11 +108,20 @@ struct LaunchOpts {
   int wide;            // lanes per record on the key-table path (1, 4, 16)
 };
 
-// G comb table: window w in [0, 33), entry j in [0, 128): (j+1) * 2^(8w) * G,
-// affine, canonical radix-2^30 Montgomery x (limbs 0..8) and y (limbs 9..17),
-// padded to kGEntry words.
-constexpr int kCombWindows = 33;
-constexpr int kCombEntries = 128;
+// G comb table: kGW-bit signed windows. Window w in [0, kCombWindows), entry
+// j in [0, kCombEntries): (j+1) * 2^(kGW w) * G, affine, canonical radix-2^30
+// Montgomery x (limbs 0..8) and y (limbs 9..17), padded to kGEntry words.
+// kGW = 10: 26 windows x 512 entries x 72 B = 958 KB per curve (L2-resident).
+#ifndef BH_GCOMB_BITS
+#define BH_GCOMB_BITS 10
+#endif
+constexpr int kGW = BH_GCOMB_BITS;
+static_assert(kGW >= 8 && kGW <= 12, "G comb window width");
+// digits of k + M (M = sum 2^(kGW-1) 2^(kGW w)) minus 2^(kGW-1) are k's signed
+// digits in [-2^(kGW-1), 2^(kGW-1)); k < 2^256 needs kGW * windows >= 257.
+constexpr int kCombWindows = (257 + kGW - 1) / kGW;
+constexpr int kCombEntries = 1 << (kGW - 1);
+static_assert(kCombWindows * kGW <= 288, "recoded scalar fits 9 limbs");
 constexpr int kGEntry = 18;
 constexpr int kQTab = 16;
 constexpr int kQPt = 28;  // words per Jacobian point in the Q table (27 + pad)
@@ -429,8 +438,8 @@ BH_HD void gtab_entry(uint32_t t, uint32_t* out) {
   f_const(B.X, P::gx_m);
   f_const(B.Y, P::gy_m);
   f_const(B.Z, P::r1);
-  for (uint32_t d = 0; d < 8 * win; d++) j_dbl<P>(B, B);
-  // (j+1) B by left-to-right double-and-add over the bits of j+1 (<= 128)
+  for (uint32_t d = 0; d < (uint32_t)kGW * win; d++) j_dbl<P>(B, B);
+  // (j+1) B by left-to-right double-and-add over the bits of j+1 (<= kCombEntries)
   const uint32_t k = j + 1;
   int top = 31;
   while (!((k >> top) & 1u)) top--;
@@ -441,7 +450,7 @@ BH_HD void gtab_entry(uint32_t t, uint32_t* out) {
     if ((k >> b) & 1u) {
       bool same;
       J30 R;
-      j_add<P>(R, A, B, &same);  // A = m B with 2 <= m < 128: never degenerate
+      j_add<P>(R, A, B, &same);  // A = m B with 2 <= m < kCombEntries: never degenerate
       j_copy(A, R);
     }
   }
@@ -460,6 +469,43 @@ BH_HD void gtab_entry(uint32_t t, uint32_t* out) {
   }
 }
 
+// v >>= B (288-bit, compile-time B < 288)
+template <int B>
+BH_HD void shr_const(uint32_t v[9]) {
+  constexpr int ws = B / 32, bs = B % 32;
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    const uint32_t lo = (q + ws < 9) ? v[q + ws] : 0u;
+    const uint32_t hi = (q + ws + 1 < 9) ? v[q + ws + 1] : 0u;
+    v[q] = bs ? ((lo >> bs) | (hi << (32 - bs))) : lo;
+  }
+}
+
+struct GOff {
+  uint32_t v[9];
+};
+constexpr GOff make_goff() {
+  GOff o{};
+  for (int w = 0; w < kCombWindows; w++) {
+    const int b = w * kGW + kGW - 1;
+    o.v[b / 32] |= 1u << (b % 32);
+  }
+  return o;
+}
+constexpr GOff kGOff = make_goff();
+
+// v (288-bit) = k + M for the G comb's signed-digit recoding (see kGW)
+BH_HD void recode_goff(uint32_t v[9], const uint32_t k[8]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    c += (uint64_t)k[q] + kGOff.v[q];
+    v[q] = (uint32_t)c;
+    c >>= 32;
+  }
+  v[8] = (uint32_t)c + kGOff.v[8];
+}
+
 // ---- shared tail: u1 G by the fixed-base comb, then A + B and the x check
 // u1 G: 8-bit signed windows over the L2-resident affine table (33 mixed adds).
 template <class P>
@@ -470,25 +516,13 @@ BH_HD void g_comb(J30& B, bool& b_inf, const uint32_t* gtab, const uint32_t u1[8
   f_copy(B.X, one);
   f_copy(B.Y, one);
   f_copy(B.Z, one);
-  uint32_t k1[8];
-  copy8(k1, u1);
-  uint32_t carry = 0;
+  uint32_t v[9];
+  recode_goff(v, u1);
   for (int win = 0; win < kCombWindows; win++) {
-    uint32_t v = (k1[0] & 0xffu) + carry;
-#pragma unroll
-    for (int k = 0; k < 7; k++) k1[k] = (k1[k] >> 8) | (k1[k + 1] << 24);
-    k1[7] >>= 8;
-    uint32_t mag;
-    bool neg;
-    if (v > 128u) {
-      mag = 256u - v;
-      neg = true;
-      carry = 1;
-    } else {
-      mag = v;
-      neg = false;
-      carry = 0;
-    }
+    const int d = (int)(v[0] & (2u * kCombEntries - 1u)) - kCombEntries;
+    shr_const<kGW>(v);
+    const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+    const bool neg = d < 0;
     const uint32_t* te = gtab + ((size_t)win * kCombEntries + (mag ? mag - 1 : 0)) * kGEntry;
     uint32_t tx[9], ty[9];
 #pragma unroll
@@ -870,9 +904,9 @@ BH_HD uint32_t reg_lookup(const KeyReg& g, const Work& w, uint32_t i, uint64_t h
 // win = l, l + L, ... and the G-comb windows likewise, then the L partial
 // sums are combined by a butterfly over the group. The signed digits come
 // from one addition instead of a carry scan: with M = sum 8 * 16^w the
-// nibbles of k + M minus 8 are the digits of k in [-8, 7] (and with 128 *
-// 256^w, bytes minus 128 in [-128, 127]), so every lane reads its windows
-// directly. Same point as q_keycomb / g_comb (different digits, same sum).
+// nibbles of k + M minus 8 are the digits of k in [-8, 7] (and the G comb's
+// kGW-bit digits come from recode_goff the same way), so every lane reads its
+// windows directly. Same point as q_keycomb (different digits, same sum).
 
 // v (288-bit, 9 limbs) = k + M, M = pattern in every limb of the low 256 bits
 // plus `top` at bit 256 (the top window's offset).
@@ -887,7 +921,7 @@ BH_HD void recode_offset(uint32_t v[9], const uint32_t k[8], uint32_t pattern, u
   v[8] = (uint32_t)c + top;
 }
 
-// o = v >> sh (288-bit), 0 <= sh < 128
+// o = v >> sh (288-bit), 0 <= sh < 192
 BH_HD void shr288(uint32_t o[9], const uint32_t v[9], uint32_t sh) {
   const uint32_t ws = sh >> 5, bs = sh & 31u;
   uint32_t t[9];
@@ -895,7 +929,7 @@ BH_HD void shr288(uint32_t o[9], const uint32_t v[9], uint32_t sh) {
   for (int q = 0; q < 9; q++) {
     uint32_t x = 0;
 #pragma unroll
-    for (uint32_t d = 0; d < 4; d++)
+    for (uint32_t d = 0; d < 6; d++)
       if (ws == d) x = (q + (int)d < 9) ? v[q + d] : 0u;
     t[q] = x;
   }
@@ -903,18 +937,6 @@ BH_HD void shr288(uint32_t o[9], const uint32_t v[9], uint32_t sh) {
   for (int q = 0; q < 9; q++) {
     const uint32_t hi = (q + 1 < 9) ? t[q + 1] : 0u;
     o[q] = bs ? ((t[q] >> bs) | (hi << (32 - bs))) : t[q];
-  }
-}
-
-// v >>= B (288-bit, compile-time B < 288)
-template <int B>
-BH_HD void shr_const(uint32_t v[9]) {
-  constexpr int ws = B / 32, bs = B % 32;
-#pragma unroll
-  for (int q = 0; q < 9; q++) {
-    const uint32_t lo = (q + ws < 9) ? v[q + ws] : 0u;
-    const uint32_t hi = (q + ws + 1 < 9) ? v[q + ws + 1] : 0u;
-    v[q] = bs ? ((lo >> bs) | (hi << (32 - bs))) : lo;
   }
 }
 
@@ -994,16 +1016,16 @@ BH_HD void keycomb_part(J30& C, bool& c_inf, const Work& w, const uint32_t* gtab
       j_acc<P>(C, c_inf, T, mag == 0);
     }
   }
-  // u1 G: 8-bit windows win = l + m L over the affine G comb
+  // u1 G: kGW-bit windows win = l + m L over the affine G comb
   ld8(k, w.e, i, w.ns);
-  recode_offset(v, k, 0x80808080u, 0x80u);
-  shr288(sv, v, 8u * l);
+  recode_goff(v, k);
+  shr288(sv, v, (uint32_t)kGW * l);
   uint32_t one[9];
   f_const(one, P::r1);
   for (int m = 0; m * L < kCombWindows; m++) {
     const uint32_t win = l + (uint32_t)(m * L);
-    const int d = (int)(sv[0] & 0xffu) - 128;
-    shr_const<8 * L>(sv);
+    const int d = (int)(sv[0] & (2u * kCombEntries - 1u)) - kCombEntries;
+    shr_const<kGW * L>(sv);
     if (win < (uint32_t)kCombWindows) {
       const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
       const uint32_t* te = gtab + ((size_t)win * kCombEntries + (mag ? mag - 1 : 0)) * kGEntry;

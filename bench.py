@@ -30,10 +30,13 @@ sys.path.insert(0, ROOT)
 # Algorithmic work per verify in SURVEY.md 8(d) units: F_p mul/sqr x 128 u32
 # MACs (64 product + 64 reduction). The variable-base ladder is schedule S0
 # (3.2e3 F_p ops = 4.1e5 MACs). The per-key comb path does 65 Jacobian adds
-# (16 ops) + 33 mixed adds (11 ops) + ~23 for the final add/x check = 1,426
-# F_p ops per verify, plus 65 x (5 dbl x 8 + 3 add x 16) = 5,720 per key table.
+# (16 ops) + G_WINDOWS mixed adds (11 ops) + ~23 for the final add/x check
+# (= 1,349 F_p ops per verify with the 10-bit G comb: BH_GCOMB_BITS in
+# verify.h), plus 65 x (5 dbl x 8 + 3 add x 16) = 5,720 per key table.
 MAC_PER_FP = 128
-FP_LADDER, FP_KEYCOMB, FP_KTAB = 3200, 1426, 5720
+G_COMB_BITS = 10
+G_WINDOWS = (257 + G_COMB_BITS - 1) // G_COMB_BITS
+FP_LADDER, FP_KEYCOMB, FP_KTAB = 3200, 65 * 16 + G_WINDOWS * 11 + 23, 5720
 MACS_PER_VERIFY = FP_LADDER * MAC_PER_FP
 KERNELS = {"build_ladder_ms": "k_ktab_ladder", "keycomb_ms": "k_keycomb"}
 
