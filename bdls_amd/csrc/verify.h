@@ -276,6 +276,21 @@ BH_HD void setbytes_u256(const uint8_t* b, uint32_t len, uint32_t v[8], bool* bi
   }
 }
 
+// e = SignedProto.Hash() (message.go:97-138) as hashToInt: 32 bytes, then mod n,
+// stored to w.e for stage_prep. One lane per record; the device runs the
+// 4-lanes-per-record k_bdls_hash (verify_kernels.hip) with the same result.
+template <class C>
+BH_HD void stage_bdls_hash(const BdlsIn& in, const Work& w, uint32_t i) {
+  uint8_t hsh[32];
+  uint32_t e[8], nn[8], t[8];
+  const uint8_t* q = in.xy + (size_t)i * 64;
+  bdls_signed_proto_hash(hsh, in.version[i], q, q + 32, in.msg + in.msg_off[i], in.msg_len[i]);
+  be32_to_limbs(e, hsh);
+  load_const8(nn, C::n);
+  if (!sub8(t, e, nn)) copy8(e, t);
+  st8(w.e, i, w.ns, e);
+}
+
 // SignedProto.Verify (message.go:170-184): hash = SignedProto.Hash(), then Go
 // crypto/ecdsa.Verify(pub{curve, X, Y}, hash, R, S) with R, S from SetBytes.
 // secp256k1 takes verifyLegacy; P-256 takes verifyNISTEC. No low-S rule.
@@ -297,13 +312,7 @@ BH_HD void stage_prep(const BdlsIn& in, const Work& w, uint32_t i) {
   if (reason == R_OK && !key_import<P, C>(q, qx30, qy30)) reason = R_BAD_KEY;
   if (reason == R_OK && (rbig || geq8(r, nn))) reason = R_R_RANGE;
   if (reason == R_OK && (sbig || geq8(s, nn))) reason = R_S_RANGE;
-  if (reason == R_OK) {
-    uint8_t hsh[32];
-    bdls_signed_proto_hash(hsh, in.version[i], q, q + 32, in.msg + in.msg_off[i], in.msg_len[i]);
-    be32_to_limbs(e, hsh);  // hashToInt / hashToNat: 32 bytes, then mod n
-    uint32_t t[8];
-    if (!sub8(t, e, nn)) copy8(e, t);
-  }
+  if (reason == R_OK) ld8(e, w.e, i, w.ns);  // stage_bdls_hash (or k_bdls_hash) ran first
   uint8_t st = reason;
   if (reason == R_OK) {
     uint32_t pmn[8], rn[8], rm[9], r2m[9];

@@ -45,8 +45,150 @@ void launch_prep(const BatchIn& in, const Work& w, uint32_t n, dim3 grd, dim3 bl
   else
     hipLaunchKernelGGL((k_prep<P, N, C, BatchIn, HK_GIVEN_OR_SHA256>), grd, blk, 0, s, in, w, n);
 }
+// ---- BDLS SignedProto.Hash, 4 lanes per record -----------------------------
+// A BLAKE2b round is 4 independent column G's, then 4 independent diagonal
+// G's. Lane c of a quad runs column c and diagonal c, holding v[c], v[4+c],
+// v[8+c], v[12+c]; between the halves rows 1..3 rotate across the quad by DPP
+// quad_perm (full-rate VALU moves, no LDS traffic). The 128-byte block is
+// staged in LDS (lane c writes words 8c..8c+7) and each lane reads the four
+// message words its G's take per round. Same digest as bdls_signed_proto_hash
+// (blake2b.h), ~3x shorter per-record critical path: the serial chain of a
+// lock/decide message (67 embedded proofs, ~100 blocks) dominated a round.
+struct B2Quad {
+  uint32_t k[4][12];  // lane c, round r: sigma[r][2c], [2c+1], [8+2c], [9+2c]
+};
+constexpr B2Quad make_b2quad() {
+  B2Quad q{};
+  for (int c = 0; c < 4; c++)
+    for (int r = 0; r < 12; r++)
+      q.k[c][r] = (uint32_t)B2Sigma::s[r][2 * c] | ((uint32_t)B2Sigma::s[r][2 * c + 1] << 8) |
+                  ((uint32_t)B2Sigma::s[r][8 + 2 * c] << 16) |
+                  ((uint32_t)B2Sigma::s[r][9 + 2 * c] << 24);
+  return q;
+}
+constexpr B2Quad kB2Quad = make_b2quad();
+constexpr int kQRot1 = 0x39;  // quad_perm [1,2,3,0]: lane c reads lane c+1
+constexpr int kQRot2 = 0x4E;  // [2,3,0,1]
+constexpr int kQRot3 = 0x93;  // [3,0,1,2]
+
+template <int CTRL>
+__device__ __forceinline__ uint64_t qperm(uint64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xf, 0xf, false);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, 0xf, 0xf, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ void b2_gq(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d,
+                                      uint64_t x, uint64_t y) {
+  a = a + b + x;
+  d = rotr64(d ^ a, 32);
+  c = c + d;
+  b = rotr64(b ^ c, 24);
+  a = a + b + y;
+  d = rotr64(d ^ a, 16);
+  c = c + d;
+  b = rotr64(b ^ c, 63);
+}
+
+template <class C>
+__global__ __launch_bounds__(256) void k_bdls_hash(BdlsIn in, Work w, uint32_t n) {
+  __shared__ uint64_t lds_blk[64][16];  // one 128-byte block per quad
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = gid >> 2, c = gid & 3u;
+  if (i >= n) return;  // whole quads exit together
+  uint64_t* B = lds_blk[threadIdx.x >> 2];
+  const uint8_t* xy = in.xy + (size_t)i * 64;
+  const uint8_t* msg = in.msg + in.msg_off[i];
+  const uint32_t mlen = in.msg_len[i];
+  uint32_t sidx[12];
+#pragma unroll
+  for (int r = 0; r < 12; r++)
+    sidx[r] = c == 0 ? kB2Quad.k[0][r]
+              : c == 1 ? kB2Quad.k[1][r]
+              : c == 2 ? kB2Quad.k[2][r]
+                       : kB2Quad.k[3][r];
+  const uint64_t iv_a = kB2IV[c], iv_b = kB2IV[4 + c];
+  uint64_t h_a = iv_a ^ (c == 0 ? 0x01010000ull ^ 32ull : 0ull), h_b = iv_b;  // h[c], h[4+c]
+  const uint64_t total = kBdlsHeader + (uint64_t)mlen;
+  for (uint64_t pos = 0;; pos += 128) {
+    const bool last = total - pos <= 128;
+    uint32_t wv[8];  // stream words pos/4 + 8c .. + 7
+    if (pos == 0 && c < 3) {
+      uint32_t hx[8], hy[8];
+      load_le_words<8>(hx, xy);
+      load_le_words<8>(hy, xy + 32);
+      if (c == 0) {
+        wv[0] = 0x534c4442u;  // "BDLS_CONSENSUS_SIGNATURE", little-endian words
+        wv[1] = 0x4e4f435fu;
+        wv[2] = 0x534e4553u;
+        wv[3] = 0x535f5355u;
+        wv[4] = 0x414e4749u;
+        wv[5] = 0x45525554u;
+        wv[6] = in.version[i];
+        wv[7] = hx[0];
+      } else if (c == 1) {
+#pragma unroll
+        for (int k = 0; k < 7; k++) wv[k] = hx[k + 1];
+        wv[7] = hy[0];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 7; k++) wv[k] = hy[k + 1];
+        wv[7] = mlen;
+      }
+    } else {
+      const uint32_t q = (uint32_t)(pos + 32u * c - kBdlsHeader);  // message byte offset
+      if (!last) {
+        load_le_words<8>(wv, msg + q);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) wv[k] = b2_tail_word(msg, mlen, q + 4u * k);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; k++) B[4 * c + k] = (uint64_t)wv[2 * k] | ((uint64_t)wv[2 * k + 1] << 32);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    uint64_t a = h_a, b = h_b, cc = iv_a, d = iv_b;
+    if (c == 0) d ^= last ? total : pos + 128;  // v[12] ^= t
+    if (c == 2 && last) d = ~d;                  // v[14] = ~v[14]
+#pragma unroll
+    for (int r = 0; r < 12; r++) {
+      const uint32_t sx = sidx[r];
+      b2_gq(a, b, cc, d, B[sx & 0xffu], B[(sx >> 8) & 0xffu]);
+      b = qperm<kQRot1>(b);
+      cc = qperm<kQRot2>(cc);
+      d = qperm<kQRot3>(d);
+      b2_gq(a, b, cc, d, B[(sx >> 16) & 0xffu], B[sx >> 24]);
+      b = qperm<kQRot3>(b);
+      cc = qperm<kQRot2>(cc);
+      d = qperm<kQRot1>(d);
+    }
+    h_a ^= a ^ cc;
+    h_b ^= b ^ d;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (last) break;
+  }
+  // digest = h[0..3] little-endian; e = big-endian integer (limb 7 = bytes 0..3)
+  const uint64_t h1 = qperm<kQRot1>(h_a), h2 = qperm<kQRot2>(h_a), h3 = qperm<kQRot3>(h_a);
+  if (c != 0) return;
+  const uint64_t hh[4] = {h_a, h1, h2, h3};
+  uint32_t e[8], nn[8], t[8];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    e[7 - 2 * k] = bswap32((uint32_t)hh[k]);
+    e[6 - 2 * k] = bswap32((uint32_t)(hh[k] >> 32));
+  }
+  load_const8(nn, C::n);
+  if (!sub8(t, e, nn)) copy8(e, t);
+  st8(w.e, i, w.ns, e);
+}
+
 template <class P, class N, class C>
 void launch_prep(const BdlsIn& in, const Work& w, uint32_t n, dim3 grd, dim3 blk, hipStream_t s) {
+  hipLaunchKernelGGL((k_bdls_hash<C>), dim3((n * 4 + 255) / 256), blk, 0, s, in, w, n);
   hipLaunchKernelGGL((k_prep<P, N, C, BdlsIn, 0>), grd, blk, 0, s, in, w, n);
 }
 

@@ -92,6 +92,7 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
       if (in.flags & BHF_HASH_SHA3_256) stage_prep<P, N, C, HK_SHA3_256>(in, w, i);
       else stage_prep<P, N, C>(in, w, i);
     } else {
+      stage_bdls_hash<C>(in, w, i);
       stage_prep<P, N, C>(in, w, i);
     }
   }
