@@ -6,7 +6,7 @@
 //   stage_inv    : w = s^-1 mod n by Montgomery's batch trick over a set of
 //                  records, u1 = e w, u2 = r w.               (1 lane/chunk)
 //   stage_ladder : Q table, signed-window (Booth w=5) ladder for u2 Q, fixed-base
-//                  comb (8-bit signed windows) for u1 G, final add, projective
+//                  comb (kGW-bit signed windows) for u1 G, final add, projective
 //                  x == r (or r + n) check.                   (1 lane/record)
 //
 // Reference semantics restated (see DESIGN.md for the full contract):
@@ -736,15 +736,26 @@ BH_HD void ktab_load(J30& P, const uint32_t* tab, uint32_t win, uint32_t j) {
   }
 }
 
-// Build one key table from the canonical Montgomery (qx, qy) of record `rec`.
+// Build one key table from the canonical Montgomery (qx, qy) of record `rec`,
+// by one lane (parts = 1) or two (parts = 2: part 0 = windows [0, kKSplit),
+// part 1 = windows [kKSplit, 65) after 4 kKSplit doublings of Q). kKSplit
+// balances the two serial chains (88 F_p ops per window vs 8 per doubling:
+// 3,520 vs 3,480 instead of 5,720). Two lanes only pay when a few tables are
+// built (key registration: latency-bound); with tens of thousands of tables
+// the +18% work costs more than the shorter chain saves (measured at config
+// 2: 3.34 -> 4.64 ms), so verify batches use one lane per table.
+constexpr uint32_t kKSplit = 40;
 template <class P>
-BH_HD void ktab_build(uint32_t* tab, const Work& w, uint32_t rec) {
+BH_HD void ktab_build(uint32_t* tab, const Work& w, uint32_t rec, uint32_t part, uint32_t parts) {
   J30 B, E2, E3, E4, T;
   ld9(B.X, w.qx, rec, w.ns);
   ld9(B.Y, w.qy, rec, w.ns);
   f_const(B.Z, P::r1);
   bool same;
-  for (uint32_t win = 0; win < (uint32_t)kKWin; win++) {
+  const uint32_t w0 = part ? kKSplit : 0u;
+  const uint32_t w1 = (part || parts == 1) ? (uint32_t)kKWin : kKSplit;
+  for (uint32_t d = 0; d < 4u * w0; d++) j_dbl<P>(B, B);
+  for (uint32_t win = w0; win < w1; win++) {
     ktab_store(tab, win, 0, B);                 // 1 B
     j_dbl<P>(E2, B);
     ktab_store(tab, win, 1, E2);                // 2 B

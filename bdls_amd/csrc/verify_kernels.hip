@@ -7,7 +7,7 @@
 //                 1 lane/record   registry lookup, dedup of the other keys,
 //                                 per-batch tables for keys used >= min_uses
 //                                 times, route records to the two paths
-//   k_ktab_ladder 1 lane/key + 1 lane/record
+//   k_ktab_ladder 1-2 lanes/key + 1 lane/record
 //                                 key-table builds and, in the same grid, the
 //                                 variable-base ladder for records without a
 //                                 table (independent work: the ladder fills
@@ -150,17 +150,27 @@ __global__ __launch_bounds__(256) void k_bdls_hash(BdlsIn in, Work w, uint32_t n
     for (int k = 0; k < 4; k++) B[4 * c + k] = (uint64_t)wv[2 * k] | ((uint64_t)wv[2 * k + 1] << 32);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    // all 48 message words this lane's G's take, issued back to back (one LDS
+    // latency per block instead of one per half-round)
+    uint64_t mx[12][4];
+#pragma unroll
+    for (int r = 0; r < 12; r++) {
+      const uint32_t sx = sidx[r];
+      mx[r][0] = B[sx & 0xffu];
+      mx[r][1] = B[(sx >> 8) & 0xffu];
+      mx[r][2] = B[(sx >> 16) & 0xffu];
+      mx[r][3] = B[sx >> 24];
+    }
     uint64_t a = h_a, b = h_b, cc = iv_a, d = iv_b;
     if (c == 0) d ^= last ? total : pos + 128;  // v[12] ^= t
     if (c == 2 && last) d = ~d;                  // v[14] = ~v[14]
 #pragma unroll
     for (int r = 0; r < 12; r++) {
-      const uint32_t sx = sidx[r];
-      b2_gq(a, b, cc, d, B[sx & 0xffu], B[(sx >> 8) & 0xffu]);
+      b2_gq(a, b, cc, d, mx[r][0], mx[r][1]);
       b = qperm<kQRot1>(b);
       cc = qperm<kQRot2>(cc);
       d = qperm<kQRot3>(d);
-      b2_gq(a, b, cc, d, B[(sx >> 16) & 0xffu], B[sx >> 24]);
+      b2_gq(a, b, cc, d, mx[r][2], mx[r][3]);
       b = qperm<kQRot3>(b);
       cc = qperm<kQRot2>(cc);
       d = qperm<kQRot1>(d);
@@ -296,19 +306,21 @@ __global__ __launch_bounds__(256) void k_split(Work w, Plan pl, uint32_t n,
   else pl.ladder_list[atomicAdd(&pl.counters[1], 1u)] = i;
 }
 
-// Blocks [0, tab_blocks) build key tables (one lane per table); the rest run
+// Blocks [0, tab_blocks) build key tables (`parts` lanes per table); the rest run
 // the ladder list. Ladder waves past the list length exit whole (the Q-table
 // scratch slot is the list position).
 template <class P>
 __global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
                                                      const uint32_t* __restrict__ gtab,
                                                      uint8_t* __restrict__ reason,
-                                                     uint32_t tab_blocks) {
+                                                     uint32_t tab_blocks, uint32_t parts) {
   if (blockIdx.x < tab_blocks) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t t2 = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t t = t2 / parts;
     const uint32_t nt = min(pl.counters[2], pl.max_tables);
     if (t >= nt) return;
-    ktab_build<P>(const_cast<uint32_t*>(tab_ptr(pl, g, pl.tab_dst[t])), w, pl.tab_rec[t]);
+    ktab_build<P>(const_cast<uint32_t*>(tab_ptr(pl, g, pl.tab_dst[t])), w, pl.tab_rec[t],
+                  t2 % parts, parts);
     return;
   }
   const uint32_t j0 = (blockIdx.x - tab_blocks) * blockDim.x + threadIdx.x;
@@ -453,6 +465,10 @@ static hipError_t plan_reset(const Plan& pl, hipStream_t s) {
   return hipMemsetAsync(pl.counters, 0, 16, s);
 }
 
+// Table builds run two lanes per table when at most this many can be built
+// (far below one wave per SIMD: latency-bound), else one (see ktab_build).
+constexpr uint32_t kSplitBuildMax = 8192;
+
 // Full launch sequence. ev (optional, 7 events) brackets: prep | inv | plan
 // (lookup + dedup + split) | key tables + ladder | publish | key comb + bitmap.
 template <class P, class N, class C, class IN>
@@ -480,9 +496,10 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
                      o.keep ? 1u : 0u, 0u);
   hipLaunchKernelGGL(k_split, grd, blk, 0, s, w, pl, n, reason);
   REC(3);
-  const uint32_t tab_blocks = (pl.max_tables + 255) / 256;
+  const uint32_t parts = pl.max_tables <= kSplitBuildMax ? 2u : 1u;
+  const uint32_t tab_blocks = (parts * pl.max_tables + 255) / 256;
   hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x), blk, 0, s, w, pl, g, gtab,
-                     reason, tab_blocks);
+                     reason, tab_blocks, parts);
   REC(4);
   if (o.keep) hipLaunchKernelGGL(k_reg_publish, dim3(tab_blocks), blk, 0, s, w, pl, g);
   REC(5);
@@ -535,9 +552,10 @@ static hipError_t reg_seq(const uint8_t* pub, const Work& w, const Plan& pl, con
   hipLaunchKernelGGL(k_key_insert, grd, blk, 0, s, w, pl, g, n);
   hipLaunchKernelGGL(k_key_count, grd, blk, 0, s, w, pl, n);
   hipLaunchKernelGGL(k_key_plan, grd, blk, 0, s, w, pl, g, n, 1u, 0u, 1u, 1u);
-  const uint32_t tab_blocks = (pl.max_tables + 255) / 256;
+  const uint32_t parts = pl.max_tables <= kSplitBuildMax ? 2u : 1u;
+  const uint32_t tab_blocks = (parts * pl.max_tables + 255) / 256;
   hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, pl, g,
-                     (const uint32_t*)nullptr, (uint8_t*)nullptr, tab_blocks);
+                     (const uint32_t*)nullptr, (uint8_t*)nullptr, tab_blocks, parts);
   hipLaunchKernelGGL(k_reg_publish, dim3(tab_blocks), blk, 0, s, w, pl, g);
   hipLaunchKernelGGL(k_reg_status, grd, blk, 0, s, w, pl, n, status);
   return hipGetLastError();

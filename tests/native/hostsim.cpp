@@ -127,7 +127,12 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
       if (tab_of[r] == kNone) {
         tab_of[r] = (uint32_t)tables.size();
         tables.emplace_back(kKTabWords);
-        ktab_build<P>(tables.back().data(), w, r);
+        if (r & 1) {  // both build shapes (the device picks per launch)
+          ktab_build<P>(tables.back().data(), w, r, 0, 2);
+          ktab_build<P>(tables.back().data(), w, r, 1, 2);
+        } else {
+          ktab_build<P>(tables.back().data(), w, r, 0, 1);
+        }
       }
       ok = keycomb_any<P>(w, gtab, i, tables[tab_of[r]].data());
       combs++;
