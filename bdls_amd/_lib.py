@@ -10,7 +10,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libbdlship.so")
+# BDLS_HIP_LIB overrides the library path (A/B runs of build variants).
+LIB_PATH = os.environ.get("BDLS_HIP_LIB") or os.path.join(_HERE, "lib", "libbdlship.so")
 
 BH_OK = 0
 BH_F_HASH_SHA256 = 1

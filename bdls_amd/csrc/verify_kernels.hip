@@ -352,8 +352,15 @@ __global__ __launch_bounds__(256) void k_reg_publish(Work w, Plan pl, KeyReg g) 
   }
 }
 
+// BH_KEYCOMB_WAVES: optional occupancy target for k_keycomb (waves per SIMD;
+// the register budget follows from it). Unset = the compiler's choice.
+#ifdef BH_KEYCOMB_WAVES
+#define BH_KEYCOMB_ATTR __attribute__((amdgpu_waves_per_eu(BH_KEYCOMB_WAVES, BH_KEYCOMB_WAVES)))
+#else
+#define BH_KEYCOMB_ATTR
+#endif
 template <class P>
-__global__ __launch_bounds__(256) void k_keycomb(Work w, Plan pl, KeyReg g,
+__global__ __launch_bounds__(256) BH_KEYCOMB_ATTR void k_keycomb(Work w, Plan pl, KeyReg g,
                                                  const uint32_t* __restrict__ gtab,
                                                  uint8_t* __restrict__ reason) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
