@@ -32,7 +32,10 @@ def load(root: str):
     for path in glob.glob(os.path.join(root, "**", "*counter_collection*.csv"), recursive=True) + \
             glob.glob(os.path.join(root, "**", "pmc_*.csv"), recursive=True):
         with open(path) as f:
-            for row in csv.DictReader(f):
+            rd = csv.DictReader(f)
+            if "Counter_Name" not in (rd.fieldnames or []):
+                continue  # kernel-trace / agent-info csvs of the same -o prefix
+            for row in rd:
                 k = short(row["Kernel_Name"])
                 acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
                 meta[k] = {"grid": int(row["Grid_Size"]), "wg": int(row["Workgroup_Size"]),
