@@ -28,6 +28,7 @@ EXPORTS = (
     "bh_parse_der_sig", "bh_dev_alloc", "bh_dev_free", "bh_memcpy_h2d", "bh_memcpy_d2h",
     "bh_sync", "bh_verify_bdls", "bh_verify_bdls_dev", "bh_keys_reserve", "bh_keys_register",
     "bh_keys_clear", "bh_keys_count", "bh_timing_begin", "bh_timing_end", "bh_bdls_preverify",
+    "bh_verify_submit", "bh_verify_wait", "bh_host_alloc", "bh_host_free",
 )
 KEY_FULL = 255  # bh_keys_register status: registry full
 
@@ -95,6 +96,15 @@ def lib() -> ctypes.CDLL:
         L.bh_workspace_bytes.restype = sz
         L.bh_verify.argtypes = [i32, ctypes.POINTER(BhBatch), sz, u32, vp, vp]
         L.bh_verify.restype = i32
+        L.bh_verify_submit.argtypes = [i32, ctypes.POINTER(BhBatch), sz, u32, vp, vp,
+                                       ctypes.POINTER(vp)]
+        L.bh_verify_submit.restype = i32
+        L.bh_verify_wait.argtypes = [vp]
+        L.bh_verify_wait.restype = i32
+        L.bh_host_alloc.argtypes = [sz, ctypes.POINTER(vp)]
+        L.bh_host_alloc.restype = i32
+        L.bh_host_free.argtypes = [vp]
+        L.bh_host_free.restype = i32
         L.bh_verify_dev.argtypes = [i32, i32, ctypes.POINTER(BhBatch), sz, u32, vp, vp, vp, i32,
                                     ctypes.POINTER(BhTiming)]
         L.bh_verify_dev.restype = i32
@@ -153,6 +163,40 @@ def ensure_init(device_mask: int = 0) -> None:
 
 def last_error() -> str:
     return lib().bh_last_error().decode(errors="replace")
+
+
+class HostArray:
+    """Page-locked host memory from libbdlship.so (bh_host_alloc) viewed as a
+    numpy array: the host-API batch layout that lets uploads overlap kernels."""
+
+    def __init__(self, nbytes: int):
+        import numpy as np
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(lib().bh_host_alloc(max(1, self.nbytes), ctypes.byref(p)))
+        self.ptr = p.value
+        buf = (ctypes.c_uint8 * max(1, self.nbytes)).from_address(self.ptr)
+        self.u8 = np.frombuffer(buf, np.uint8)[:self.nbytes]
+
+    @classmethod
+    def from_numpy(cls, a):
+        import numpy as np
+        a = np.ascontiguousarray(a)
+        h = cls(a.nbytes)
+        h.u8[:] = a.view(np.uint8).reshape(-1)
+        return h, h.u8.view(a.dtype)
+
+    def free(self):
+        if self.ptr:
+            self.u8 = None
+            lib().bh_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # noqa: BLE001 (interpreter shutdown)
+            pass
 
 
 class DeviceArray:

@@ -66,6 +66,15 @@ constexpr size_t kDefaultRegCap = size_t(1) << 16;
 size_t round64(size_t n) { return (n + 63) & ~size_t(63); }
 size_t round256(size_t n) { return (n + 255) & ~size_t(255); }
 
+// Records per kernel pass. BH_MAX_CHUNK (test-only; rounded up to a multiple
+// of 64 so bitmap words of consecutive passes concatenate) forces the
+// multi-pass loop on small batches.
+size_t max_chunk() {
+  const char* e = getenv("BH_MAX_CHUNK");  // read per call: tests switch it
+  const long x = e ? atol(e) : 0L;
+  return x > 0 ? std::min(kMaxChunk, round64((size_t)x)) : kMaxChunk;
+}
+
 size_t pow2_at_least(size_t v) {
   size_t p = 1;
   while (p < v) p <<= 1;
@@ -98,13 +107,53 @@ struct Registry {
   bh::KeyReg g{};  // cap == 0: not allocated
 };
 
+// Page-locked host memory (hipHostMalloc, portable: DMA-able by every device).
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return BH_OK;
+    release();
+    const size_t want = std::max<size_t>(bytes, 4096);
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocPortable);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return fail(BH_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    }
+    cap = want;
+    return BH_OK;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// One of the double-buffered host-API pipeline slots of a device: its own
+// device staging for the inputs, device and pinned-host buffers for the
+// outputs, and the events that order upload -> verify -> download. While the
+// compute stream verifies slot k's batch, the copy stream uploads slot k^1's.
+struct Slot {
+  DevBuf stage;     // inputs (H2D on the copy stream)
+  DevBuf out;       // bitmap words + reasons (device)
+  HostBuf host_out; // bitmap words + reasons (pinned, D2H on the compute stream)
+  hipEvent_t uploaded = nullptr, done = nullptr;
+  bh_job* owner = nullptr;  // job whose results are in flight / sit in host_out
+  size_t owner_part = 0;
+};
+constexpr int kSlots = 2;
+
 struct Dev {
   int id = -1;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // compute (+ result download)
+  hipStream_t copy = nullptr;    // host-API input upload
   uint32_t* gtab[2] = {nullptr, nullptr};
   DevBuf ws;     // Work + Plan
-  DevBuf stage;  // host-API inputs
-  DevBuf out;    // host-API bitmap words + reasons
+  DevBuf stage;  // key registration input
+  DevBuf out;    // key registration status
+  Slot slot[kSlots];
+  uint32_t next_slot = 0;
   Registry reg[2];
   hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipEvent_t done = nullptr;  // end of the last pass (orders passes across streams)
@@ -171,6 +220,7 @@ int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl, bool reg = false) {
   pl->slot_tab = (uint32_t*)take(hc * 4);
   pl->rec_slot = (uint32_t*)take(ns * 4);
   pl->comb_list = (uint32_t*)take(ns * 4);
+  pl->comb_order = pl->comb_list;
   pl->ladder_list = (uint32_t*)take(ns * 4);
   pl->rec_tab = (uint32_t*)take(ns * 4);
   pl->counters = (uint32_t*)take(16);
@@ -222,6 +272,11 @@ int dev_init(Dev& d, int id) {
     return fail(BH_E_NODEV, std::string("device ") + std::to_string(id) + " is " +
                                 prop.gcnArchName + ", this build targets gfx950 only");
   HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+  for (Slot& sl : d.slot) {
+    HIPCHK(hipEventCreateWithFlags(&sl.uploaded, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  }
   for (int c = 0; c < 2; c++) {
     HIPCHK(hipMalloc(&d.gtab[c], kGtabWords * 4));
     HIPCHK(bh::launch_gtab_build(c, d.gtab[c], d.stream));
@@ -236,11 +291,20 @@ void dev_free(Dev& d) {
   (void)hipSetDevice(d.id);
   if (d.done_recorded) (void)hipEventSynchronize(d.done);
   if (d.stream) (void)hipStreamSynchronize(d.stream);
+  if (d.copy) (void)hipStreamSynchronize(d.copy);
   for (auto& g : d.gtab)
     if (g) (void)hipFree(g);
   d.ws.release();
   d.stage.release();
   d.out.release();
+  for (Slot& sl : d.slot) {
+    sl.stage.release();
+    sl.out.release();
+    sl.host_out.release();
+    if (sl.uploaded) (void)hipEventDestroy(sl.uploaded);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+  }
+  if (d.copy) (void)hipStreamDestroy(d.copy);
   for (auto& r : d.reg) r.mem.release();
   for (auto& e : d.ev)
     if (e) (void)hipEventDestroy(e);
@@ -318,8 +382,9 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
   // the workspace is shared by every pass on this device: a pass on another
   // stream starts after the previous one ended
   if (d.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.done, 0));
-  for (size_t base = 0; base < n; base += kMaxChunk) {
-    const size_t m = std::min(kMaxChunk, n - base);
+  const size_t chunk = max_chunk();
+  for (size_t base = 0; base < n; base += chunk) {
+    const size_t m = std::min(chunk, n - base);
     bh::Work w;
     bh::Plan pl;
     int rc = carve_work(d, m, &w, &pl);
@@ -361,29 +426,39 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
   return BH_OK;
 }
 
-// ---- host-buffer staging ---------------------------------------------------
-// A variable-length field over records [lo, lo + m): its byte range in the
-// caller's buffer and the offsets rebased to that range.
+// ---- host-buffer pipeline ----------------------------------------------------
+// A host batch is split into contiguous 64-aligned shards, one per device.
+// Each shard takes one of the device's kSlots pipeline slots:
+//   copy stream    : H2D of the shard's arrays into the slot's staging
+//   compute stream : wait(uploaded) -> verify passes -> D2H of bitmap words and
+//                    reasons into the slot's pinned host buffer -> record done
+// bh_verify_submit returns after enqueueing; bh_verify_wait collects. With two
+// slots, batch k+1's upload runs under batch k's kernels,
+// provided the caller's buffers are page-locked (bh_host_alloc): a copy from
+// pageable memory is staged by the HIP runtime and does not overlap.
+//
+// Variable-length fields are not rebased on the host: the staged bytes cover
+// [min off, max off + len) of the shard and the device pointer is biased by
+// -min off, so the caller's offsets index the staging copy directly.
 struct VarField {
   uint64_t lo = 0, bytes = 0;
-  std::vector<uint64_t> off;
 };
 
-VarField rebase(const uint64_t* off, const uint32_t* len, size_t lo, size_t m) {
-  VarField v;
+VarField span(const uint64_t* off, const uint32_t* len, size_t lo, size_t m) {
   uint64_t a = UINT64_MAX, z = 0;
   for (size_t i = lo; i < lo + m; i++) {
-    a = std::min<uint64_t>(a, off[i]);
-    z = std::max<uint64_t>(z, off[i] + len[i]);
+    const uint64_t o = off[i];
+    a = o < a ? o : a;
+    const uint64_t e = o + len[i];
+    z = e > z ? e : z;
   }
+  VarField v;
   v.lo = (a == UINT64_MAX) ? 0 : a;
   v.bytes = z > v.lo ? z - v.lo : 0;
-  v.off.resize(m);
-  for (size_t i = 0; i < m; i++) v.off[i] = off[lo + i] - v.lo;
   return v;
 }
 
-// Carves the device staging buffer and queues one H2D copy per array.
+// Carves a device staging buffer and queues one H2D copy per array.
 struct Uploader {
   char* base;
   hipStream_t s;
@@ -398,8 +473,10 @@ struct Uploader {
       err = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
     return (const T*)dst;
   }
+  // staged bytes of v, as a pointer the caller's offsets index directly
   const uint8_t* put(const uint8_t* data, const VarField& v) {
-    return put<uint8_t>(data ? data + v.lo : nullptr, data ? v.bytes : 0);
+    const uint8_t* p = put<uint8_t>(data ? data + v.lo : nullptr, data ? v.bytes : 0);
+    return p - v.lo;
   }
 };
 
@@ -410,8 +487,8 @@ struct HostFields {
 
 HostFields fields(const bh_batch* b, size_t lo, size_t m) {
   HostFields f;
-  f.var.push_back(rebase(b->sig_off, b->sig_len, lo, m));
-  f.var.push_back(rebase(b->msg_off, b->msg_len, lo, m));
+  f.var.push_back(span(b->sig_off, b->sig_len, lo, m));
+  f.var.push_back(span(b->msg_off, b->msg_len, lo, m));
   f.bytes = round256(m * 64 + 1) + 4 * round256(m * 8 + 1) + round256(f.var[0].bytes + 1) +
             round256(f.var[1].bytes + 1);
   return f;
@@ -420,9 +497,9 @@ HostFields fields(const bh_batch* b, size_t lo, size_t m) {
 bh_batch upload(Uploader& u, const bh_batch* b, size_t lo, size_t m, const HostFields& f) {
   bh_batch d;
   d.pub = u.put(b->pub + lo * 64, m * 64);
-  d.sig_off = u.put(f.var[0].off.data(), m);
+  d.sig_off = u.put(b->sig_off + lo, m);
   d.sig_len = u.put(b->sig_len + lo, m);
-  d.msg_off = u.put(f.var[1].off.data(), m);
+  d.msg_off = u.put(b->msg_off + lo, m);
   d.msg_len = u.put(b->msg_len + lo, m);
   d.sig = u.put(b->sig, f.var[0]);
   d.msg = u.put(b->msg, f.var[1]);
@@ -431,9 +508,9 @@ bh_batch upload(Uploader& u, const bh_batch* b, size_t lo, size_t m, const HostF
 
 HostFields fields(const bh_bdls_batch* b, size_t lo, size_t m) {
   HostFields f;
-  f.var.push_back(rebase(b->r_off, b->r_len, lo, m));
-  f.var.push_back(rebase(b->s_off, b->s_len, lo, m));
-  f.var.push_back(rebase(b->msg_off, b->msg_len, lo, m));
+  f.var.push_back(span(b->r_off, b->r_len, lo, m));
+  f.var.push_back(span(b->s_off, b->s_len, lo, m));
+  f.var.push_back(span(b->msg_off, b->msg_len, lo, m));
   f.bytes = round256(m * 64 + 1) + 7 * round256(m * 8 + 1);
   for (auto& v : f.var) f.bytes += round256(v.bytes + 1);
   return f;
@@ -443,12 +520,12 @@ bh_bdls_batch upload(Uploader& u, const bh_bdls_batch* b, size_t lo, size_t m,
                      const HostFields& f) {
   bh_bdls_batch d;
   d.xy = u.put(b->xy + lo * 64, m * 64);
-  d.r_off = u.put(f.var[0].off.data(), m);
+  d.r_off = u.put(b->r_off + lo, m);
   d.r_len = u.put(b->r_len + lo, m);
-  d.s_off = u.put(f.var[1].off.data(), m);
+  d.s_off = u.put(b->s_off + lo, m);
   d.s_len = u.put(b->s_len + lo, m);
   d.version = u.put(b->version + lo, m);
-  d.msg_off = u.put(f.var[2].off.data(), m);
+  d.msg_off = u.put(b->msg_off + lo, m);
   d.msg_len = u.put(b->msg_len + lo, m);
   d.r = u.put(b->r, f.var[0]);
   d.s = u.put(b->s, f.var[1]);
@@ -456,62 +533,142 @@ bh_bdls_batch upload(Uploader& u, const bh_bdls_batch* b, size_t lo, size_t m,
   return d;
 }
 
-// One device's share [lo, lo + m) of a host batch: stage, verify, gather.
-template <class B>
-int host_shard(Dev& d, int curve, const B* b, size_t lo, size_t m, uint32_t flags,
-               uint8_t* bitmap, uint8_t* reason) {
-  std::lock_guard<std::mutex> g(d.mu);
+struct Part {
+  Dev* d;
+  int slot;
+  size_t lo, m;
+  bool done;
+};
+
+}  // namespace
+
+// An in-flight host batch (opaque bh_job of the C ABI).
+struct bh_job {
+  std::vector<Part> parts;
+  uint8_t* bitmap = nullptr;
+  uint8_t* reason = nullptr;
+  size_t n = 0;
+  int rc = BH_OK;
+  std::string err;
+};
+
+namespace {
+
+// Wait for part k of job j and copy its results out (caller holds d.mu).
+int finish_part(bh_job* j, size_t k) {
+  Part& p = j->parts[k];
+  if (p.done) return BH_OK;
+  Dev& d = *p.d;
+  Slot& sl = d.slot[p.slot];
+  p.done = true;
+  sl.owner = nullptr;
   HIPCHK(hipSetDevice(d.id));
-  const HostFields f = fields(b, lo, m);
-  int rc;
-  if ((rc = d.stage.ensure(f.bytes + 4096))) return rc;
-  if ((rc = d.out.ensure(round64(m) / 8 + m + 1024))) return rc;
-  hipStream_t s = d.stream;
-  // the staging buffer may still feed a pass queued by an earlier call
-  if (d.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.done, 0));
-  Uploader u{(char*)d.stage.p, s};
-  const B db = upload(u, b, lo, m, f);
-  HIPCHK(u.err);
-  uint64_t* dbm = (uint64_t*)d.out.p;
-  uint8_t* drs = (uint8_t*)(dbm + round64(m) / 64);
-  if ((rc = run_dev(d, curve, &db, m, flags, dbm, drs, s, nullptr))) return rc;
-  std::vector<uint64_t> words(round64(m) / 64);
-  HIPCHK(hipMemcpyAsync(words.data(), dbm, words.size() * 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(reason + lo, drs, m, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  std::memcpy(bitmap + lo / 8, words.data(), (m + 7) / 8);  // lo is a multiple of 64
+  hipError_t e = hipEventSynchronize(sl.done);
+  if (e != hipSuccess) return fail(BH_E_DEVICE, std::string("pass failed: ") + hipGetErrorString(e));
+  const uint64_t* words = (const uint64_t*)sl.host_out.p;
+  const uint8_t* rs = (const uint8_t*)(words + round64(p.m) / 64);
+  std::memcpy(j->bitmap + p.lo / 8, words, (p.m + 7) / 8);  // lo is a multiple of 64
+  std::memcpy(j->reason + p.lo, rs, p.m);
   return BH_OK;
 }
 
-// Host batch over all initialised devices: contiguous 64-aligned shards, one
-// host thread per device.
+// Enqueue shard [lo, lo + m) on device d (caller holds d.mu).
+template <class B>
+int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, uint32_t flags) {
+  HIPCHK(hipSetDevice(d.id));
+  const int k = (int)(d.next_slot++ % kSlots);
+  Slot& sl = d.slot[k];
+  if (sl.owner) {  // the slot still holds an uncollected batch: collect it now
+    bh_job* o = sl.owner;
+    int rc = finish_part(o, sl.owner_part);
+    if (rc && o->rc == BH_OK) {
+      o->rc = rc;
+      o->err = g_err;
+    }
+  }
+  const HostFields f = fields(b, lo, m);
+  int rc;
+  if ((rc = sl.stage.ensure(f.bytes + 4096))) return rc;
+  const size_t out_bytes = round64(m) / 8 + m + 1024;
+  if ((rc = sl.out.ensure(out_bytes))) return rc;
+  if ((rc = sl.host_out.ensure(out_bytes))) return rc;
+  Uploader u{(char*)sl.stage.p, d.copy};
+  const B db = upload(u, b, lo, m, f);
+  HIPCHK(u.err);
+  HIPCHK(hipEventRecord(sl.uploaded, d.copy));
+  hipStream_t s = d.stream;
+  HIPCHK(hipStreamWaitEvent(s, sl.uploaded, 0));
+  uint64_t* dbm = (uint64_t*)sl.out.p;
+  uint8_t* drs = (uint8_t*)(dbm + round64(m) / 64);
+  if ((rc = run_dev(d, curve, &db, m, flags, dbm, drs, s, nullptr))) return rc;
+  HIPCHK(hipMemcpyAsync(sl.host_out.p, dbm, round64(m) / 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync((uint8_t*)sl.host_out.p + round64(m) / 8, drs, m,
+                        hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(sl.done, s));
+  sl.owner = j;
+  sl.owner_part = j->parts.size();
+  j->parts.push_back(Part{&d, k, lo, m, false});
+  return BH_OK;
+}
+
+int wait_job(bh_job* j) {
+  int rc = j->rc;
+  std::string err = j->err;
+  for (size_t k = 0; k < j->parts.size(); k++) {
+    Dev& d = *j->parts[k].d;
+    std::lock_guard<std::mutex> g(d.mu);
+    int r = finish_part(j, k);
+    if (r && rc == BH_OK) {
+      rc = r;
+      err = g_err;
+    }
+  }
+  delete j;
+  if (rc) return fail(rc, err);
+  return BH_OK;
+}
+
+// Host batch over all initialised devices: contiguous 64-aligned shards,
+// enqueued from the calling thread (every step is asynchronous).
+template <class B>
+int submit_job(int curve, const B* b, size_t n, uint32_t flags, uint8_t* bitmap,
+               uint8_t* reason, bh_job** out) {
+  *out = nullptr;
+  std::vector<Dev*> devs = all_devs();
+  if (devs.empty()) return fail(BH_E_NOT_INIT, "bh_init not called");
+  bh_job* j = new bh_job();
+  j->bitmap = bitmap;
+  j->reason = reason;
+  j->n = n;
+  if (n) std::memset(bitmap, 0, (n + 7) / 8);
+  const size_t nd = std::min(devs.size(), (n + 63) / 64);
+  const size_t per = nd ? round64((n + nd - 1) / nd) : 0;
+  for (size_t k = 0; k < nd; k++) {
+    const size_t lo = k * per, hi = std::min(n, lo + per);
+    if (lo >= hi) break;
+    Dev& d = *devs[k];
+    int rc;
+    {
+      std::lock_guard<std::mutex> g(d.mu);
+      rc = enqueue_part(j, d, curve, b, lo, hi - lo, flags);
+    }
+    if (rc) {
+      const std::string err = g_err;
+      (void)wait_job(j);  // drain what was enqueued
+      return fail(rc, err);
+    }
+  }
+  *out = j;
+  return BH_OK;
+}
+
 template <class B>
 int host_verify(int curve, const B* b, size_t n, uint32_t flags, uint8_t* bitmap,
                 uint8_t* reason) {
-  std::vector<Dev*> devs = all_devs();
-  if (devs.empty()) return fail(BH_E_NOT_INIT, "bh_init not called");
-  std::memset(bitmap, 0, (n + 7) / 8);
-  if (n == 0) return BH_OK;
-  const size_t nd = std::min(devs.size(), (n + 63) / 64);
-  const size_t per = round64((n + nd - 1) / nd);
-  std::vector<int> rcs(nd, BH_OK);
-  std::vector<std::string> errs(nd);
-  auto work = [&](size_t k) {
-    const size_t lo = k * per, hi = std::min(n, lo + per);
-    if (lo >= hi) return;
-    rcs[k] = host_shard(*devs[k], curve, b, lo, hi - lo, flags, bitmap, reason);
-    if (rcs[k]) errs[k] = g_err;
-  };
-  if (nd == 1) {
-    work(0);
-  } else {
-    std::vector<std::thread> th;
-    for (size_t k = 0; k < nd; k++) th.emplace_back(work, k);
-    for (auto& t : th) t.join();
-  }
-  for (size_t k = 0; k < nd; k++)
-    if (rcs[k]) return fail(rcs[k], errs[k]);
-  return BH_OK;
+  bh_job* j = nullptr;
+  int rc = submit_job(curve, b, n, flags, bitmap, reason, &j);
+  if (rc) return rc;
+  return wait_job(j);
 }
 
 int check_curve(int curve) {
@@ -594,7 +751,7 @@ int bh_device_count(void) {
   return (int)g_devs.size();
 }
 
-size_t bh_workspace_bytes(size_t n) { return work_bytes(round64(std::min(n, kMaxChunk))); }
+size_t bh_workspace_bytes(size_t n) { return work_bytes(round64(std::min(n, max_chunk()))); }
 
 int bh_verify_dev(int device, int curve, const bh_batch* b, size_t n, uint32_t flags,
                   uint64_t* bitmap_words, uint8_t* reason, void* stream, int sync,
@@ -626,6 +783,41 @@ int bh_verify(int curve, const bh_batch* b, size_t n, uint32_t flags, uint8_t* b
   if (int rc = check_flags(flags)) return rc;
   if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
   return host_verify(curve, b, n, flags, bitmap, reason);
+}
+
+int bh_verify_submit(int curve, const bh_batch* b, size_t n, uint32_t flags, uint8_t* bitmap,
+                     uint8_t* reason, bh_job** job) {
+  if (!job) return fail(BH_E_INVALID, "null job");
+  *job = nullptr;
+  if (!b || (n && (!b->pub || !b->sig_off || !b->sig_len || !b->msg_off || !b->msg_len ||
+                   !bitmap || !reason)))
+    return fail(BH_E_INVALID, "null pointer in batch");
+  if (curve != BH_CURVE_P256) return fail(BH_E_INVALID, "curve not supported by bh_verify_submit");
+  if (int rc = check_flags(flags)) return rc;
+  if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
+  return submit_job(curve, b, n, flags, bitmap, reason, job);
+}
+
+int bh_verify_wait(bh_job* job) {
+  if (!job) return fail(BH_E_INVALID, "null job");
+  return wait_job(job);
+}
+
+int bh_host_alloc(size_t bytes, void** ptr) {
+  if (!ptr) return fail(BH_E_INVALID, "null ptr");
+  *ptr = nullptr;
+  hipError_t e = hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocPortable);
+  if (e != hipSuccess) {
+    *ptr = nullptr;
+    return fail(BH_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+  }
+  return BH_OK;
+}
+
+int bh_host_free(void* ptr) {
+  if (!ptr) return BH_OK;
+  HIPCHK(hipHostFree(ptr));
+  return BH_OK;
 }
 
 int bh_csp_verify_p256(const uint8_t pub[64], const uint8_t* sig, size_t sig_len,

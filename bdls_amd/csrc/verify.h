@@ -18,7 +18,7 @@
 #pragma once
 #include "blake2b.h"
 #include "der.h"
-#include "ec.h"
+#include "fe.h"
 #include "ec30.h"
 #include "sha256.h"
 #include "sha3.h"
@@ -89,7 +89,10 @@ struct Plan {
   uint32_t* slot_cnt;   // [hc] records verified equal to the representative key
   uint32_t* slot_tab;   // [hc] key-table index or kNone
   uint32_t* rec_slot;   // [ns] slot or kNone
-  uint32_t* comb_list;  // [ns] records on the key-comb path
+  uint32_t* comb_list;  // [ns] records on the key-comb path (k_split order)
+  uint32_t* comb_order; // the comb list k_keycomb reads: comb_list, or its
+                        // key-sorted copy (comb_sort; stored in rec_slot's
+                        // buffer, which is dead from then on)
   uint32_t* ladder_list;  // [ns] records on the variable-base ladder path
   uint32_t* counters;   // [0] n_comb, [1] n_ladder, [2] table builds
   uint32_t* rec_tab;    // [ns] table id of the record's key (kNone: ladder)

@@ -368,7 +368,7 @@ __global__ __launch_bounds__(256) BH_KEYCOMB_ATTR void k_keycomb(Work w, Plan pl
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t cnt = pl.counters[0];
   if (j >= cnt) return;
-  const uint32_t i = pl.comb_list[j];
+  const uint32_t i = pl.comb_order[j];
   const bool ok = stage_keycomb<P>(w, gtab, i, tab_ptr(pl, g, pl.rec_tab[i]));
   reason[i] = ok ? R_OK : R_MATH;
 }
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void k_keycomb_wide(Work w, Plan pl, KeyReg g,
   const uint32_t j = gid / L, l = gid % L;
   const uint32_t cnt = pl.counters[0];
   if (j >= cnt) return;  // whole groups exit together
-  const uint32_t i = pl.comb_list[j];
+  const uint32_t i = pl.comb_order[j];
   J30 C;
   bool c_inf;
   keycomb_part<P, L>(C, c_inf, w, gtab, i, tab_ptr(pl, g, pl.rec_tab[i]), l);
@@ -476,38 +476,52 @@ static hipError_t plan_reset(const Plan& pl, hipStream_t s) {
 
 // Key-grouped comb order: sort keys for the comb list (the record's table id;
 // entries past the list length get kNone and sort last, their values 0).
-__global__ __launch_bounds__(256) void k_comb_keys(Plan pl, uint32_t n, uint32_t* __restrict__ keys) {
+// Table ids are compacted to `bits` + 2 bits so the radix sort runs only the
+// passes it needs: a registry id (< 2^bits) as is, a per-batch id kLocal|job
+// (job < 2^16 <= 2^bits) as 2^bits | job, the padding past the list 2^(bits+1).
+__global__ __launch_bounds__(256) void k_comb_keys(Plan pl, uint32_t n, uint32_t bits,
+                                                   uint32_t* __restrict__ keys) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const uint32_t cnt = pl.counters[0];
   if (j < cnt) {
-    keys[j] = pl.rec_tab[pl.comb_list[j]];
+    const uint32_t t = pl.rec_tab[pl.comb_list[j]];
+    keys[j] = (t & kLocal) ? ((1u << bits) | (t & ~kLocal)) : t;
   } else {
-    keys[j] = kNone;
+    keys[j] = 2u << bits;
     pl.comb_list[j] = 0;
   }
 }
 
 // Sort the comb list by table id so the (on average 16) records of one key sit
 // in adjacent lanes of one wave: their table reads then hit the same L2 lines
-// instead of streaming the 58 KB table once per record. Runs on the plan's
-// dedup buffers, which are dead after k_split (slot_hash: sort temp; slot_rep,
-// slot_cnt: keys; rec_slot: the sorted list). Returns the list k_keycomb
-// reads. Result order never changes results (one record per lane).
+// instead of streaming the 58 KB table once per record. Runs on plan buffers
+// that are dead once k_split has routed every record: slot_hash holds the
+// sort temp, slot_rep / slot_cnt the keys, and rec_slot receives the sorted
+// list -- so after this call rec_slot no longer holds slots, and the sorted
+// list is published as Plan::comb_order (every later kernel reads that, never
+// rec_slot). Result order never changes results (one record per lane).
 constexpr uint32_t kSortMin = 65536;
-static hipError_t comb_sort(const Plan& pl, uint32_t n, hipStream_t s, Plan* out) {
+static hipError_t comb_sort(const Plan& pl, const KeyReg& g, uint32_t n, hipStream_t s,
+                            Plan* out) {
   *out = pl;
   if (n < kSortMin) return hipSuccess;
+  uint32_t bits = 16;
+  while ((1ull << bits) < (uint64_t)g.cap) bits++;
+  const int end_bit = (int)bits + 2;
   size_t temp = 0;
   hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp, pl.slot_rep, pl.slot_cnt,
-                                                    pl.comb_list, pl.rec_slot, (int)n, 0, 32, s);
+                                                    pl.comb_list, pl.rec_slot, (int)n, 0,
+                                                    end_bit, s);
   if (e) return e;
   if (temp > (size_t)pl.hc * 8) return hipSuccess;  // keep the unsorted list
-  hipLaunchKernelGGL(k_comb_keys, dim3((n + 255) / 256), dim3(256), 0, s, pl, n, pl.slot_rep);
+  hipLaunchKernelGGL(k_comb_keys, dim3((n + 255) / 256), dim3(256), 0, s, pl, n, bits,
+                     pl.slot_rep);
   e = hipcub::DeviceRadixSort::SortPairs(pl.slot_hash, temp, pl.slot_rep, pl.slot_cnt,
-                                         pl.comb_list, pl.rec_slot, (int)n, 0, 32, s);
+                                         pl.comb_list, pl.rec_slot, (int)n, 0, end_bit, s);
   if (e) return e;
-  out->comb_list = pl.rec_slot;
+  out->comb_order = pl.rec_slot;
+  out->rec_slot = nullptr;  // consumed: holds the sorted list now
   return hipSuccess;
 }
 
@@ -543,25 +557,26 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   hipLaunchKernelGGL(k_split, grd, blk, 0, s, w, pl, n, reason);
   Plan plc;
   if (o.wide <= 1) {
-    if ((e = comb_sort(pl, n, s, &plc))) return e;
+    if ((e = comb_sort(pl, g, n, s, &plc))) return e;
   } else {
     plc = pl;
   }
   REC(3);
   const uint32_t parts = pl.max_tables <= kSplitBuildMax ? 2u : 1u;
   const uint32_t tab_blocks = (parts * pl.max_tables + 255) / 256;
-  hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x), blk, 0, s, w, pl, g, gtab,
+  // from here on only plc (rec_slot consumed by the sort)
+  hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x), blk, 0, s, w, plc, g, gtab,
                      reason, tab_blocks, parts);
   REC(4);
-  if (o.keep) hipLaunchKernelGGL(k_reg_publish, dim3(tab_blocks), blk, 0, s, w, pl, g);
+  if (o.keep) hipLaunchKernelGGL(k_reg_publish, dim3(tab_blocks), blk, 0, s, w, plc, g);
   REC(5);
   switch (o.wide) {
     case 4:
-      hipLaunchKernelGGL((k_keycomb_wide<P, 4>), dim3((n * 4 + 255) / 256), blk, 0, s, w, pl, g,
+      hipLaunchKernelGGL((k_keycomb_wide<P, 4>), dim3((n * 4 + 255) / 256), blk, 0, s, w, plc, g,
                          gtab, reason);
       break;
     case 16:
-      hipLaunchKernelGGL((k_keycomb_wide<P, 16>), dim3((n * 16 + 255) / 256), blk, 0, s, w, pl,
+      hipLaunchKernelGGL((k_keycomb_wide<P, 16>), dim3((n * 16 + 255) / 256), blk, 0, s, w, plc,
                          g, gtab, reason);
       break;
     default:

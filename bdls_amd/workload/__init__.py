@@ -40,32 +40,53 @@ class Workload:
                 self.msg_len)
 
 
-def generate(n: int, nkeys: int, msg_len: int = 256, corrupt_den: int = 16, seed: int = 2,
-             nthreads: int | None = None, family: str = "SHA2") -> Workload:
-    """Records signed over Hash(msg) with the MSP hash family (SHA2: SHA-256,
-    SHA3: SHA3-256; msp/identities.go:219-227)."""
+def _empty(alloc, count: int, dtype):
+    """numpy array of `count` items, from alloc(nbytes) -> uint8 array if given
+    (e.g. page-locked memory for the pipelined host path)."""
+    if alloc is None:
+        return np.empty(count, dtype)
+    return alloc(count * np.dtype(dtype).itemsize).view(dtype)
+
+
+def generate_shard(n_total: int, lo: int, count: int, nkeys: int, msg_len: int = 256,
+                   corrupt_den: int = 16, seed: int = 2, nthreads: int | None = None,
+                   family: str = "SHA2", alloc=None) -> Workload:
+    """Records [lo, lo + count) of ONE seeded batch of n_total records: every
+    record is a function of (seed, global index), so the shards of any split
+    concatenate to the same batch (config 5: one 64M batch over N ranks).
+    nkeys >= n_total: one distinct key per record. Records are signed over
+    Hash(msg) with the MSP hash family (SHA2: SHA-256, SHA3: SHA3-256;
+    msp/identities.go:219-227)."""
     if not os.path.exists(_LIB):
         raise RuntimeError(f"{_LIB} not built (run `make`)")
     L = ctypes.CDLL(_LIB)
-    vp = ctypes.c_void_p
-    L.gen_p256_family.argtypes = [ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                  ctypes.c_uint64, ctypes.c_int, ctypes.c_int] + [vp] * 9
-    L.gen_p256_family.restype = ctypes.c_int
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.gen_p256_shard.argtypes = [sz, sz, sz, sz, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                 ctypes.c_int, ctypes.c_int] + [vp] * 9
+    L.gen_p256_shard.restype = ctypes.c_int
     fam = {"SHA2": 0, "SHA3": 1}[family]
     if nthreads is None:
         nthreads = min(16, os.cpu_count() or 1)
+    n = count
     w = Workload(
-        pub=np.empty(n * 64, np.uint8), msg=np.empty(n * msg_len, np.uint8),
-        msg_off=np.empty(n, np.uint64), msg_len=np.empty(n, np.uint32),
-        sig=np.zeros(n * SIG_STRIDE, np.uint8), sig_off=np.empty(n, np.uint64),
-        sig_len=np.empty(n, np.uint32), reason=np.empty(n, np.uint8), cls=np.empty(n, np.uint8))
-    rc = L.gen_p256_family(n, nkeys, msg_len, corrupt_den, seed, nthreads, fam, w.pub.ctypes.data,
-                    w.msg.ctypes.data, w.msg_off.ctypes.data, w.msg_len.ctypes.data,
-                    w.sig.ctypes.data, w.sig_off.ctypes.data, w.sig_len.ctypes.data,
-                    w.reason.ctypes.data, w.cls.ctypes.data)
+        pub=_empty(alloc, n * 64, np.uint8), msg=_empty(alloc, n * msg_len, np.uint8),
+        msg_off=_empty(alloc, n, np.uint64), msg_len=_empty(alloc, n, np.uint32),
+        sig=_empty(alloc, n * SIG_STRIDE, np.uint8), sig_off=_empty(alloc, n, np.uint64),
+        sig_len=_empty(alloc, n, np.uint32), reason=np.empty(n, np.uint8), cls=np.empty(n, np.uint8))
+    w.sig[:] = 0
+    rc = L.gen_p256_shard(n_total, lo, count, nkeys, msg_len, corrupt_den, seed, nthreads, fam,
+                          w.pub.ctypes.data, w.msg.ctypes.data, w.msg_off.ctypes.data,
+                          w.msg_len.ctypes.data, w.sig.ctypes.data, w.sig_off.ctypes.data,
+                          w.sig_len.ctypes.data, w.reason.ctypes.data, w.cls.ctypes.data)
     if rc != 0:
-        raise RuntimeError(f"gen_p256 failed: {rc}")
+        raise RuntimeError(f"gen_p256_shard failed: {rc}")
     return w
+
+
+def generate(n: int, nkeys: int, msg_len: int = 256, corrupt_den: int = 16, seed: int = 2,
+             nthreads: int | None = None, family: str = "SHA2", alloc=None) -> Workload:
+    """A whole batch of n records (see generate_shard)."""
+    return generate_shard(n, 0, n, nkeys, msg_len, corrupt_den, seed, nthreads, family, alloc)
 
 
 @dataclass

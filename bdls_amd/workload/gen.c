@@ -79,7 +79,8 @@ static size_t der_int(uint8_t *o, const BIGNUM *v, int nonmin, int longlen) {
 }
 
 typedef struct {
-  size_t lo, hi, n;
+  size_t lo, hi, n; /* global record range [lo, hi) of a batch of n records */
+  size_t base;      /* global index of output slot 0 (shard start) */
   uint64_t seed;
   int nkeys, msg_len, corrupt_den;
   const uint8_t *keypub; /* nkeys * 64 */
@@ -100,13 +101,31 @@ static void *gen_worker(void *arg) {
   EC_GROUP_get_order(g, n, ctx);
   EC_GROUP_get_curve(g, p, NULL, NULL, ctx);
   BN_rshift1(half, n);
-  EC_POINT *R = EC_POINT_new(g);
-  uint8_t dg[32], b32[32];
-  for (size_t i = j->lo; i < j->hi; i++) {
-    uint64_t st = j->seed * 0x100000001b3ull + i * 0x9e3779b97f4a7c15ull + 17;
+  EC_POINT *R = EC_POINT_new(g), *Q = EC_POINT_new(g);
+  const int unique = (size_t)j->nkeys >= j->n;  /* record i signs with key i */
+  uint8_t dg[32], b32[32], upub[64], upriv[32];
+  for (size_t gi = j->lo; gi < j->hi; gi++) {
+    const size_t i = gi - j->base; /* output slot */
+    uint64_t st = j->seed * 0x100000001b3ull + gi * 0x9e3779b97f4a7c15ull + 17;
     splitmix(&st);
     const uint64_t kr = splitmix(&st);
-    const int key = (size_t)j->nkeys >= j->n ? (int)i : (int)(kr % (uint64_t)j->nkeys);
+    const uint8_t *kpub, *kpriv;
+    if (unique) {
+      /* key gi, derived exactly as key_worker would (no n-sized key table) */
+      uint64_t ks = j->seed * 0xff51afd7ed558ccdull + (uint64_t)gi * 0xc4ceb9fe1a85ec53ull + 99;
+      rand_scalar(&ks, d, n, ctx);
+      EC_POINT_mul(g, Q, d, NULL, NULL, ctx);
+      EC_POINT_get_affine_coordinates(g, Q, x, t, ctx);
+      BN_bn2binpad(d, upriv, 32);
+      BN_bn2binpad(x, upub, 32);
+      BN_bn2binpad(t, upub + 32, 32);
+      kpub = upub;
+      kpriv = upriv;
+    } else {
+      const size_t key = (size_t)(kr % (uint64_t)j->nkeys);
+      kpub = j->keypub + 64 * key;
+      kpriv = j->keypriv + 32 * key;
+    }
     int cls = C_NONE;
     if (j->corrupt_den > 0 && splitmix(&st) % (uint64_t)j->corrupt_den == 0)
       cls = 1 + (int)(splitmix(&st) % (C_NUM - 1));
@@ -117,7 +136,7 @@ static void *gen_worker(void *arg) {
     if (j->family == 1) EVP_Digest(m, j->msg_len, dg, NULL, EVP_sha3_256(), NULL);
     else SHA256(m, j->msg_len, dg);
     /* sign: r = x(kG) mod n, s = k^-1 (e + r d) mod n, low-S */
-    BN_bin2bn(j->keypriv + 32 * key, 32, d);
+    BN_bin2bn(kpriv, 32, d);
     BN_bin2bn(dg, 32, e);
     BN_nnmod(e, e, n, ctx);
     do {
@@ -132,7 +151,7 @@ static void *gen_worker(void *arg) {
     } while (BN_is_zero(r) || BN_is_zero(s));
     if (BN_cmp(s, half) > 0) BN_sub(s, n, s);
     uint8_t *q = j->pub + (size_t)i * 64;
-    memcpy(q, j->keypub + 64 * key, 64);
+    memcpy(q, kpub, 64);
     /* corruptions */
     switch (cls) {
       case C_MSG_FLIP: m[splitmix(&st) % j->msg_len] ^= (uint8_t)(1u << (splitmix(&st) % 8)); break;
@@ -172,6 +191,7 @@ static void *gen_worker(void *arg) {
     j->cls[i] = (uint8_t)cls;
   }
   EC_POINT_free(R);
+  EC_POINT_free(Q);
   BIGNUM *v[] = {n, p, half, k, kinv, r, s, e, d, t, x};
   for (size_t q = 0; q < sizeof(v) / sizeof(v[0]); q++) BN_free(v[q]);
   BN_CTX_free(ctx);
@@ -208,37 +228,48 @@ static void *key_worker(void *arg) {
   return NULL;
 }
 
-/* Caller allocates: pub n*64, msg n*msg_len, sig n*80, moff/soff n u64,
- * mlen/slen n u32, reason/cls n u8. */
-int gen_p256_family(size_t n, int nkeys, int msg_len, int corrupt_den, uint64_t seed,
-                    int nthreads, int family, uint8_t *pub, uint8_t *msg, uint64_t *moff,
-                    uint32_t *mlen, uint8_t *sig, uint64_t *soff, uint32_t *slen,
-                    uint8_t *reason, uint8_t *cls) {
+/* Records [lo, lo + count) of one seeded batch of n_total records (a shard:
+ * the union over shards is the same batch for any split). Caller allocates
+ * for `count` records: pub *64, msg *msg_len, sig *80, moff/soff u64,
+ * mlen/slen u32, reason/cls u8; offsets are shard-local. nkeys >= n_total:
+ * one distinct key per record (config 5), derived per record. */
+int gen_p256_shard(size_t n_total, size_t lo, size_t count, size_t nkeys, int msg_len,
+                   int corrupt_den, uint64_t seed, int nthreads, int family, uint8_t *pub,
+                   uint8_t *msg, uint64_t *moff, uint32_t *mlen, uint8_t *sig, uint64_t *soff,
+                   uint32_t *slen, uint8_t *reason, uint8_t *cls) {
   if (family != 0 && family != 1) return -3;
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 128) nthreads = 128;
-  if (nkeys < 1 || msg_len < 1) return -1;
-  uint8_t *kpub = malloc((size_t)nkeys * 64), *kpriv = malloc((size_t)nkeys * 32);
-  if (!kpub || !kpriv) return -2;
+  if (nkeys < 1 || msg_len < 1 || lo + count > n_total) return -1;
+  const int unique = nkeys >= n_total;
+  uint8_t *kpub = NULL, *kpriv = NULL;
   pthread_t th[128];
-  kjob kj[128];
-  int per = (nkeys + nthreads - 1) / nthreads, used = 0;
-  for (int t = 0; t < nthreads; t++) {
-    int lo = t * per, hi = lo + per > nkeys ? nkeys : lo + per;
-    if (lo >= hi) break;
-    kj[t] = (kjob){lo, hi, seed, kpub, kpriv};
-    pthread_create(&th[t], NULL, key_worker, &kj[t]);
-    used++;
+  int used = 0;
+  if (!unique) {
+    if (nkeys > (1u << 30)) return -1;
+    kpub = malloc(nkeys * 64);
+    kpriv = malloc(nkeys * 32);
+    if (!kpub || !kpriv) return -2;
+    kjob kj[128];
+    int nk = (int)nkeys, per = (nk + nthreads - 1) / nthreads;
+    for (int t = 0; t < nthreads; t++) {
+      int a = t * per, b = a + per > nk ? nk : a + per;
+      if (a >= b) break;
+      kj[t] = (kjob){a, b, seed, kpub, kpriv};
+      pthread_create(&th[t], NULL, key_worker, &kj[t]);
+      used++;
+    }
+    for (int t = 0; t < used; t++) pthread_join(th[t], NULL);
   }
-  for (int t = 0; t < used; t++) pthread_join(th[t], NULL);
   gjob gj[128];
-  size_t gper = (n + nthreads - 1) / nthreads;
+  size_t gper = (count + nthreads - 1) / nthreads;
   used = 0;
   for (int t = 0; t < nthreads; t++) {
-    size_t lo = t * gper, hi = lo + gper > n ? n : lo + gper;
-    if (lo >= hi) break;
-    gj[t] = (gjob){lo, hi, n, seed, nkeys, msg_len, corrupt_den, kpub, kpriv,
-                   pub, msg, sig, reason, cls, moff, soff, mlen, slen, family};
+    size_t a = lo + t * gper, b = a + gper > lo + count ? lo + count : a + gper;
+    if (a >= b) break;
+    gj[t] = (gjob){a, b, n_total, lo, seed, (int)(nkeys > 0x7fffffff ? 0x7fffffff : nkeys),
+                   msg_len, corrupt_den, kpub, kpriv, pub, msg, sig, reason, cls, moff, soff,
+                   mlen, slen, family};
     pthread_create(&th[t], NULL, gen_worker, &gj[t]);
     used++;
   }
@@ -246,6 +277,15 @@ int gen_p256_family(size_t n, int nkeys, int msg_len, int corrupt_den, uint64_t 
   free(kpub);
   free(kpriv);
   return 0;
+}
+
+int gen_p256_family(size_t n, int nkeys, int msg_len, int corrupt_den, uint64_t seed,
+                    int nthreads, int family, uint8_t *pub, uint8_t *msg, uint64_t *moff,
+                    uint32_t *mlen, uint8_t *sig, uint64_t *soff, uint32_t *slen,
+                    uint8_t *reason, uint8_t *cls) {
+  if (nkeys < 1) return -1;
+  return gen_p256_shard(n, 0, n, (size_t)nkeys, msg_len, corrupt_den, seed, nthreads, family, pub,
+                        msg, moff, mlen, sig, soff, slen, reason, cls);
 }
 
 int gen_p256(size_t n, int nkeys, int msg_len, int corrupt_den, uint64_t seed, int nthreads,

@@ -4,14 +4,27 @@
 Workload (BASELINE.json configs[1] = SURVEY.md 8(d) config 2): per GPU, a batch
 of 1,048,576 P-256 records -- 256-byte messages hashed on device (fused
 SHA-256, identity.Verify semantics), 65,536 distinct keys, 1/16 of the records
-corrupted over eleven reject/accept classes, seed 2 (+ rank). One "step" = one
-full verify pass over the batch resident in HBM (DER parse, checks, SHA-256,
-batched inversion, u1 G + u2 Q, bitmap). `--config 5` gives one distinct key
-per record (the 64M-over-8-GPUs scaling shape, per-GPU share).
+corrupted over eleven reject/accept classes, seed 2 (+ rank).
 
-Multi-GPU: one process per GPU (torch.distributed.run); records shard with no
-data-path collective (weak scaling); a gloo barrier brackets the timed region
-and the max time over ranks is reported.
+One "step" = one BatchVerify of the whole batch through the host C ABI as SURVEY
+8(d) times config 2 (H2D + kernel + D2H): bh_verify_submit from page-locked
+host buffers (bh_host_alloc) -> upload on the device's copy stream -> verify
+passes (DER parse, checks, SHA-256, batched inversion, u1 G + u2 Q, bitmap) ->
+bitmap + reasons back to the host; bh_verify_wait. Two batches are in flight,
+so batch k+1's upload runs under batch k's kernels. `value` is that
+PCIe-inclusive rate; the same passes on batches already resident in HBM are
+reported beside it (`hbm_resident`).
+
+`--config 5`: ONE seeded batch of 67,108,864 records with a distinct key per
+record, split over the ranks by dist.shard_range (8,388,608 per rank at 8 GPUs,
+run through the library's 4M-record pass loop); strong scaling.
+`--config 3` / `--config 4`: latency of one block (2,000 records) / one BDLS
+round (336 SignedProtos), warm and cold.
+
+Multi-GPU: one process per GPU. Under torch.distributed.run the ranks come from
+the environment; `--gpus N` without a launcher spawns the N ranks itself (before
+anything touches a GPU). Records shard with no data-path collective; a gloo
+barrier brackets the timed region and the max time over ranks is reported.
 """
 from __future__ import annotations
 
@@ -19,6 +32,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -39,6 +54,7 @@ G_WINDOWS = (257 + G_COMB_BITS - 1) // G_COMB_BITS
 FP_LADDER, FP_KEYCOMB, FP_KTAB = 3200, 65 * 16 + G_WINDOWS * 11 + 23, 5720
 MACS_PER_VERIFY = FP_LADDER * MAC_PER_FP
 KERNELS = {"build_ladder_ms": "k_ktab_ladder", "keycomb_ms": "k_keycomb"}
+CONFIG5_TOTAL = 1 << 26
 
 
 def kernel_fp_ops(stage: str, routes: dict) -> float:
@@ -54,12 +70,14 @@ def alg_bytes_per_record(msg_len: int) -> float:
     return 64 + 72 + msg_len + 24 + 1 + 0.125
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1 << 20, help="records per GPU")
+    ap.add_argument("--n", type=int, default=1 << 20, help="config 2: records per GPU")
+    ap.add_argument("--n-total", type=int, default=CONFIG5_TOTAL,
+                    help="config 5: records of the one batch split over all GPUs")
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
                     help="2/5: throughput; 3 (block) / 4 (BDLS round): latency")
     ap.add_argument("--curve", type=int, default=1, help="config 4: 1 secp256k1 (as wired), 0 P-256")
@@ -68,12 +86,16 @@ def parse():
     ap.add_argument("--msg-len", type=int, default=256)
     ap.add_argument("--corrupt-den", type=int, default=16)
     ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--hbm-resident", type=int, default=1,
+                    help="also time the same passes on inputs already in HBM")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = os.cpu_count()")
     ap.add_argument("--mac-peak", type=float, default=float(os.environ.get("BH_MAC_PEAK", 0) or 0),
                     help="measured v_mad_u64_u32 peak (MAC/s); default: profiles/ubench.json")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: exercise the launcher and the rank plumbing only")
+    return ap.parse_args(argv)
 
 
 def mac_peak_default() -> tuple[float, str]:
@@ -91,6 +113,50 @@ def percentile(v, q):
     return float(np.percentile(np.asarray(v), q))
 
 
+def host_cpus() -> dict:
+    """The host's CPU count (os.cpu_count, = nproc without affinity limits) and
+    what this process may actually run on (affinity mask, cgroup quota)."""
+    info = {"nproc": os.cpu_count() or 1}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            info["cgroup_quota_cpus"] = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+# ---------------------------------------------------------------- launcher
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes (this
+    script again, one GPU each) -- the parent never touches a GPU -- and exit
+    with the worst child status. Rank 0 prints the JSON line."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+# ---------------------------------------------------------------- latency
 def bench_latency(a, rank, world, local):
     """Configs 3 and 4: latency of one batch through the host C ABI (H2D +
     verify + D2H, what a Go caller sees) and device-resident, p50/p99 over
@@ -191,9 +257,20 @@ def bench_latency(a, rank, world, local):
                                   st.ctypes.data))
     reg_ms = (time.perf_counter() - t) * 1e3
     warm = measure("warm")
+    _lib.check(L.bh_keys_clear(-1, curve))
     wire = measure_wire(a, L, curve, rank) if a.config == 4 else None
     _lib.check(L.bh_keys_clear(-1, curve))
-    p50 = dist.max_over_ranks(warm["host_p50"], world)
+    if wire is not None:
+        # config 4's value: the A16 entry (bh_bdls_preverify) that
+        # inputConsensusMessage calls, participants' keys registered
+        p50 = dist.max_over_ranks(wire["warm"]["p50"], world)
+        value_is = ("bh_bdls_preverify (agent-tcp/tcp_peer.go:176-192 inputConsensusMessage: "
+                    "decode + participant gate + proof checks + one device batch) on the raw "
+                    "wire round, participants' keys registered (warm) p50")
+    else:
+        p50 = dist.max_over_ranks(warm["host_p50"], world)
+        value_is = ("warm host_p50: keys registered before timing (bh_keys_register); "
+                    "cold = no key known")
     parity_ok = dist.all_true(cold["parity"] and warm["parity"], world)
     out = {
         "metric": ("block-validate latency (ms, one block's signatures, host C ABI)"
@@ -203,8 +280,7 @@ def bench_latency(a, rank, world, local):
         "scaling": "replicas", "vs_baseline": None,
         "dtype": "u32", "data": "synthetic (seeded keys/signatures, workload/gen.c)",
         "config": {"workload": workload_desc, "records": n, "distinct_keys": len(pubs),
-                   "value_is": "warm host_p50: keys registered before timing "
-                               "(bh_keys_register); cold = no key known"},
+                   "value_is": value_is},
         "parity": parity_ok,
         "latency_ms": {"warm": warm, "cold": cold,
                        "register_keys_ms": round(reg_ms, 3)},
@@ -215,21 +291,23 @@ def bench_latency(a, rank, world, local):
     if rank == 0 and a.cpu_baseline:
         from oracle import orc
         cpu = []
+        threads = a.cpu_threads or (os.cpu_count() or 1)
         deadline = time.perf_counter() + 10.0
         while time.perf_counter() < deadline and len(cpu) < a.steps:
             t = time.perf_counter()
             if a.config == 3:
                 got = orc.batch_verify(w.pub.reshape(-1, 64), w.msg, w.msg_off, w.msg_len, w.sig,
-                                       w.sig_off, w.sig_len, fused=True, nthreads=a.cpu_threads)
+                                       w.sig_off, w.sig_len, fused=True, nthreads=threads)
             else:
                 got = orc.bdls_verify(curve, *arrs)
             cpu.append((time.perf_counter() - t) * 1e3)
-        cores = a.cpu_threads if a.config == 3 else 1
+        cores = threads if a.config == 3 else 1
         out["cpu_baseline"] = {
             "value": round(percentile(cpu, 50), 4), "unit": "ms", "cores": cores, "kind": "port",
+            "host_cpus": host_cpus(),
             "sample": f"the same {n} records, {len(cpu)} repetitions, p50; "
                       + ("identity.Verify semantics, OpenSSL ECDSA_do_verify, "
-                         f"{cores} threads" if a.config == 3 else
+                         f"{cores} threads (= os.cpu_count())" if a.config == 3 else
                          "serial SignedProto.Verify as the consensus loop runs it "
                          "(BLAKE2b-256 + OpenSSL ECDSA_do_verify), 1 thread"),
             "parity": bool((got == expect).all()),
@@ -244,7 +322,9 @@ def measure_wire(a, L, curve, rank):
     """Config 4 through bh_bdls_preverify: the round as raw wire messages
     (what agent-tcp's inputConsensusMessage drains), decoded, gated and
     structurally checked on the host, every SignedProto verified in one device
-    batch (participants' keys registered, as for "warm")."""
+    batch. Cold = no key known to the device; warm = the wire round's own
+    participants registered first (the BDLS participant set,
+    consensus.go:456-466)."""
     from bdls_amd import _lib, workload
     ids, raws = workload.generate_bdls_wire_round(a.validators, curve, seed=a.seed + 1000 * rank)
     n = len(raws)
@@ -262,97 +342,175 @@ def measure_wire(a, L, curve, rank):
         return L.bh_bdls_preverify(curve, buf.ctypes.data, off.ctypes.data, ln.ctypes.data, n,
                                    parts.ctypes.data, len(ids), 0, res, rs.ctypes.data, cap,
                                    ctypes.byref(total))
-    for _ in range(max(1, a.warmup)):
-        _lib.check(call())
-    ms = []
-    for _ in range(a.steps):
-        t = time.perf_counter()
-        _lib.check(call())
-        ms.append((time.perf_counter() - t) * 1e3)
     t2p1 = 2 * ((a.validators - 1) // 3) + 1
-    ok = (total.value == 2 * a.validators + 2 * (1 + t2p1)
-          and all(res[i].status == 0 for i in range(n)) and not rs[:total.value].any())
-    return {"p50": round(percentile(ms, 50), 4), "p99": round(percentile(ms, 99), 4),
-            "messages": n, "wire_bytes": int(len(buf)), "signed_protos": int(total.value),
-            "parity": bool(ok)}
+
+    def run():
+        for _ in range(max(1, a.warmup)):
+            _lib.check(call())
+        ms = []
+        for _ in range(a.steps):
+            t = time.perf_counter()
+            _lib.check(call())
+            ms.append((time.perf_counter() - t) * 1e3)
+        ok = (total.value == 2 * a.validators + 2 * (1 + t2p1)
+              and all(res[i].status == 0 for i in range(n)) and not rs[:total.value].any())
+        return {"p50": round(percentile(ms, 50), 4), "p99": round(percentile(ms, 99), 4),
+                "parity": bool(ok)}
+
+    _lib.check(L.bh_keys_clear(-1, curve))
+    cold = run()
+    st = np.zeros(len(ids), np.uint8)
+    _lib.check(L.bh_keys_register(-1, curve, parts.ctypes.data, len(ids), st.ctypes.data))
+    assert not st.any(), "participant key registration failed"
+    warm = run()
+    return {"warm": warm, "cold": cold, "messages": n, "wire_bytes": int(len(buf)),
+            "signed_protos": int(total.value), "parity": bool(warm["parity"] and cold["parity"])}
 
 
-def main():
-    a = parse()
+# ---------------------------------------------------------------- throughput
+def load_counters(config: int, n_rank: int):
+    """Per-launch HBM traffic and counter-based VALU utilisation of the
+    kernels, from the rocprofv3 --pmc passes summarised in
+    profiles/traffic.json (tools/pmc_summary.py), when they were taken on
+    this same workload."""
+    prof = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(prof):
+        return None, {}
+    with open(prof) as f:
+        tr = json.load(f)
+    want = f"config{config}:n{n_rank}"
+    if tr.get("workload") not in (None, want) or (tr.get("workload") is None and
+                                                  (config, n_rank) != (2, 1 << 20)):
+        return None, {}
+    return tr.get("source"), tr.get("kernels", {})
+
+
+def bench_throughput(a, rank, world, local):
     from bdls_amd import _lib, dist, workload
-    rank, world, local = dist.env_rank()
-    dist.init(world)
-    if a.config in (3, 4):
-        return bench_latency(a, rank, world, local)
+    if a.config == 5:
+        n_total = a.n_total
+        lo, hi = dist.shard_range(n_total, rank, world)
+        seed, nkeys, corrupt = 5, n_total, 64
+        scaling = "strong"
+        desc = (f"BASELINE config 5: one seeded batch of {n_total} records, one distinct key "
+                f"per record, 256B messages, 1/64 corrupted, fused SHA-256; rank {rank} "
+                f"verifies records [{lo}, {hi}) (dist.shard_range)")
+    else:
+        lo, hi = 0, a.n
+        n_total = a.n * world
+        seed, nkeys, corrupt = a.seed + 1000 * rank, a.nkeys, a.corrupt_den
+        scaling = "weak"
+        desc = (f"BASELINE config 2: {a.n} records/GPU, {a.msg_len}B messages, {nkeys} distinct "
+                f"keys, 1/{corrupt} corrupted, fused SHA-256")
+    n = hi - lo
 
-    nkeys = a.n if a.config == 5 else a.nkeys
-    corrupt = 64 if a.config == 5 else a.corrupt_den
-    t_gen = time.time()
-    w = workload.generate(a.n, nkeys, a.msg_len, corrupt, seed=a.seed + 1000 * rank,
-                          nthreads=max(1, min(16, (os.cpu_count() or 1)) // max(1, min(world, 8)) or 1))
-    t_gen = time.time() - t_gen
-
-    # Device memory comes from libbdlship.so itself: torch ships its own HIP
-    # runtime, so torch is used only for torch.distributed (gloo) and never
-    # touches the GPU in this process.
-    _lib.check(_lib.lib().bh_init(1 << local, 0))
-    DA = _lib.DeviceArray
-    d = dict(pub=DA.from_numpy(local, w.pub), sig=DA.from_numpy(local, w.sig),
-             so=DA.from_numpy(local, w.sig_off), sl=DA.from_numpy(local, w.sig_len),
-             msg=DA.from_numpy(local, w.msg), mo=DA.from_numpy(local, w.msg_off),
-             ml=DA.from_numpy(local, w.msg_len))
-    n = w.n
-    words = DA(local, ((n + 63) // 64) * 8)
-    reason = DA(local, n)
-    b = _lib.BhBatch(d["pub"].ptr, d["sig"].ptr, d["so"].ptr, d["sl"].ptr, d["msg"].ptr,
-                     d["mo"].ptr, d["ml"].ptr)
+    # Page-locked host memory comes from libbdlship.so (bh_host_alloc); torch
+    # ships its own HIP runtime, so torch is used only for torch.distributed
+    # (gloo) and never touches the GPU in this process.
     L = _lib.lib()
+    _lib.check(L.bh_init(1 << local, 0))
+    pinned = []
+
+    def alloc(nbytes):
+        h = _lib.HostArray(nbytes)
+        pinned.append(h)
+        return h.u8
+
+    t_gen = time.time()
+    gen_threads = max(1, min(16, (os.cpu_count() or 1)) // max(1, min(world, 8)))
+    w = workload.generate_shard(n_total if a.config == 5 else a.n, lo, n, nkeys, a.msg_len,
+                                corrupt, seed=seed, nthreads=gen_threads, alloc=alloc)
+    t_gen = time.time() - t_gen
     flags = _lib.BH_F_HASH_SHA256
-    tm = _lib.BhTiming()
+    hb = _lib.BhBatch(*[x.ctypes.data for x in (w.pub, w.sig, w.sig_off, w.sig_len, w.msg,
+                                                w.msg_off, w.msg_len)])
+    outs = [(np.zeros((n + 7) // 8, np.uint8), np.zeros(n, np.uint8)) for _ in range(2)]
 
-    def step(timing):
-        # launch stream = the library's stream for this device (NULL); timing
-        # records HIP events around each kernel on that same stream.
-        _lib.check(L.bh_verify_dev(local, 0, ctypes.byref(b), n, flags, words.ptr, reason.ptr,
-                                   None, 0, ctypes.byref(timing) if timing is not None else None))
+    def submit(k):
+        job = ctypes.c_void_p()
+        bm, rs = outs[k % 2]
+        _lib.check(L.bh_verify_submit(0, ctypes.byref(hb), n, flags, bm.ctypes.data,
+                                      rs.ctypes.data, ctypes.byref(job)))
+        return job
 
-    for _ in range(a.warmup):
-        step(None)
+    def run_host(steps):
+        """steps BatchVerify calls, two in flight (submit k+1, then wait k)."""
+        prev = None
+        for k in range(steps):
+            job = submit(k)
+            if prev is not None:
+                _lib.check(L.bh_verify_wait(prev))
+            prev = job
+        if prev is not None:
+            _lib.check(L.bh_verify_wait(prev))
+
+    run_host(a.warmup)
     _lib.check(L.bh_sync(local))
     dist.barrier(world)
-    _lib.check(L.bh_sync(local))
-    # Timed region: K passes enqueued back to back on the library stream (no
-    # per-pass host sync); HIP events around every stage of every pass on that
-    # same stream (bh_timing_begin/_end) give the per-kernel durations.
+    # Timed region: K host-buffer batches; HIP events around every stage of
+    # every pass on the compute stream (bh_timing_begin/_end) give the
+    # per-kernel durations of these same passes.
     _lib.check(L.bh_timing_begin(local))
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step(None)
-    _lib.check(L.bh_sync(local))
+    run_host(a.steps)
     t1 = time.perf_counter()
+    tm = _lib.BhTiming()
     _lib.check(L.bh_timing_end(local, ctypes.byref(tm)))
     kern = {k: getattr(tm, k) for k in _lib.BhTiming.STAGES}
     routes = {"keycomb": tm.n_keycomb, "ladder": tm.n_ladder, "key_tables": tm.n_keytables}
     dist.barrier(world)
     elapsed = dist.max_over_ranks(t1 - t0, world)
+    bm, rs = outs[(a.steps - 1) % 2]
+    bits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    parity_ok = bool((rs == w.reason).all() and (bits == w.expected_valid).all())
 
-    # parity of the last pass: bit-exact vs the expected results of the batch
-    got_reason = reason.to_numpy(np.uint8, n)
-    bits = np.unpackbits(words.to_numpy(np.uint64, (n + 63) // 64).view(np.uint8),
-                         bitorder="little")[:n].astype(bool)
-    parity_ok = bool((got_reason == w.reason).all() and (bits == w.expected_valid).all())
+    # the same passes on inputs already resident in HBM (no PCIe in the loop)
+    resident = None
+    if a.hbm_resident:
+        DA = _lib.DeviceArray
+        d = [DA.from_numpy(local, x) for x in (w.pub, w.sig, w.sig_off, w.sig_len, w.msg,
+                                               w.msg_off, w.msg_len)]
+        words = DA(local, ((n + 63) // 64) * 8)
+        dreason = DA(local, n)
+        db = _lib.BhBatch(*[x.ptr for x in d])
+
+        def step():
+            _lib.check(L.bh_verify_dev(local, 0, ctypes.byref(db), n, flags, words.ptr,
+                                       dreason.ptr, None, 0, None))
+        for _ in range(max(1, a.warmup)):
+            step()
+        _lib.check(L.bh_sync(local))
+        dist.barrier(world)
+        r0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        _lib.check(L.bh_sync(local))
+        r1 = time.perf_counter()
+        r_el = dist.max_over_ranks(r1 - r0, world)
+        rbits = np.unpackbits(words.to_numpy(np.uint64, (n + 63) // 64).view(np.uint8),
+                              bitorder="little")[:n].astype(bool)
+        r_ok = bool((dreason.to_numpy(np.uint8, n) == w.reason).all()
+                    and (rbits == w.expected_valid).all())
+        parity_ok = parity_ok and r_ok
+        resident = {"value": round(dist.sum_over_ranks(n, world) * a.steps / r_el, 1),
+                    "ms_per_step": round(r_el * 1e3 / a.steps, 3), "parity": r_ok}
+        for x in d + [words, dreason]:
+            x.free()
     parity_ok = dist.all_true(parity_ok, world)
 
-    total = n * world * a.steps
+    total = dist.sum_over_ranks(n, world) * a.steps
     value = total / elapsed
     ms_per_step = elapsed * 1e3 / a.steps
     peak, peak_src = (a.mac_peak, "--mac-peak") if a.mac_peak else mac_peak_default()
     # dominant kernel of the step and its algorithmic work per launch
     dom = max(KERNELS, key=lambda k: kern[k])
-    dom_avg_s = kern[dom] * 1e-3 / a.steps
+    # the library verifies a shard in passes of <= 4M records (equal-sized
+    # here); kern sums every launch, routes count the last pass
+    passes = max(1, -(-n // (1 << 22)))
+    dom_avg_s = kern[dom] * 1e-3 / (a.steps * passes)
     fp_ops = kernel_fp_ops(dom, routes)
     achieved = fp_ops * MAC_PER_FP / dom_avg_s if dom_avg_s > 0 else 0.0
-
+    kname = KERNELS[dom]
     out = {
         "metric": "P-256 ECDSA verifies/sec (fused SHA-256, bit-exact vs Go crypto/ecdsa + Fabric low-S)",
         "value": round(value, 1),
@@ -362,22 +520,26 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (seeded P-256 keys/signatures, workload/gen.c)",
         "config": {
-            "workload": f"BASELINE config {a.config}: {n} records/GPU, {a.msg_len}B messages, "
-                        f"{nkeys} distinct keys, 1/{corrupt} corrupted, fused SHA-256",
-            "records_per_gpu": n, "msg_len": a.msg_len, "nkeys": nkeys,
-            "corrupt_den": corrupt, "parallelism": f"shard{world} (no collective)",
+            "workload": desc,
+            "records_per_gpu": n, "records_total": dist.sum_over_ranks(n, world),
+            "msg_len": a.msg_len, "nkeys": nkeys, "corrupt_den": corrupt,
+            "parallelism": f"shard{world} (no collective)",
+            "value_is": ("host C ABI BatchVerify (bh_verify_submit/wait) from page-locked host "
+                         "buffers: H2D + verify + D2H per step, two batches in flight "
+                         "(SURVEY 8(d) config-2 timed quantity)"),
         },
         "parity": parity_ok,
+        "hbm_resident": resident,
         "kernel_ms_per_step": {k: round(v / a.steps, 3) for k, v in kern.items()},
         "routes": routes,
         "roofline": {
             "bound": "valu",
-            "kernel": KERNELS[dom],
+            "kernel": kname,
             "achieved": achieved / 1e12,
             "peak": peak / 1e12,
             "unit": "TMAC/s (u32 x u32 -> u64)",
@@ -388,40 +550,84 @@ def main():
                                 f"{routes['keycomb']} key-table verifies x {FP_KEYCOMB}")
                                + f" F_p mul/sqr x {MAC_PER_FP} u32 MACs (SURVEY 8(d) units)",
             "fp_ops_per_launch": fp_ops,
+            "launch_ms": round(dom_avg_s * 1e3, 4),
             "peak_source": peak_src,
             "traffic": None,
             "alg_bytes_per_record": alg_bytes_per_record(a.msg_len),
         },
         "gen_s": round(t_gen, 2),
     }
-    prof = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(prof):
-        with open(prof) as f:
-            tr = json.load(f).get("kernels", {})
-        # the profile's per-launch bytes for this kernel, when it was taken on
-        # this same workload (bench default: config 2)
-        hit = [v for k, v in tr.items() if k.startswith(KERNELS[dom] + "<")]
-        if hit and a.config == 2 and n == 1 << 20:
-            out["roofline"]["traffic"] = hit[0]["bytes_per_launch"]
+    src, counters = load_counters(a.config, n)
+    hit = [v for k, v in counters.items() if k.startswith(kname + "<")]
+    if hit:
+        c = hit[0]
+        if "bytes_per_launch" in c:
+            out["roofline"]["traffic"] = c["bytes_per_launch"]
+        if "sq_insts_valu" in c:
+            out["roofline"]["valu_counters"] = {
+                "sq_insts_valu_per_launch": c["sq_insts_valu"],
+                "grbm_gui_active_per_launch": c["grbm_gui_active"],
+                "formula": "SQ_INSTS_VALU x cyc / (GRBM_GUI_ACTIVE/8 XCDs x 256 CUs x 4 SIMDs)",
+                "util_2cyc": c["valu_util_2cyc"],
+                "util_4cyc": c["valu_util_4cyc"],
+                "cost_model": ("2cyc: a wave64 VALU instruction occupies a SIMD-32 for 2 cycles "
+                               "(MI355X_MICROARCH.md:54); 4cyc: one wave's issue rate and the "
+                               "measured v_mad_u64_u32 / u32-add rate (profiles/ubench.json: "
+                               "13-16 lane-ops/cycle/SIMD)"),
+                "source": src,
+            }
 
     if rank == 0 and world == 1 and a.cpu_baseline:
         from oracle import orc
         m = min(a.cpu_sample, n)
+        threads = a.cpu_threads or (os.cpu_count() or 1)
         t = time.perf_counter()
         orc.batch_verify(w.pub[:64 * m].reshape(-1, 64), w.msg, w.msg_off[:m], w.msg_len[:m],
-                         w.sig, w.sig_off[:m], w.sig_len[:m], fused=True, nthreads=a.cpu_threads)
+                         w.sig, w.sig_off[:m], w.sig_len[:m], fused=True, nthreads=threads)
         dt = time.perf_counter() - t
         out["cpu_baseline"] = {
-            "value": round(m / dt, 1), "unit": "verifies/s", "cores": a.cpu_threads,
-            "kind": "port",
+            "value": round(m / dt, 1), "unit": "verifies/s", "cores": threads,
+            "kind": "port", "host_cpus": host_cpus(),
             "sample": f"first {m} records of the same batch, identity.Verify semantics "
                       f"(SHA-256 + DER + low-S + ECDSA via OpenSSL ECDSA_do_verify), "
-                      f"{a.cpu_threads} threads, {dt:.2f}s",
+                      f"{threads} threads = os.cpu_count(), {dt:.2f}s",
         }
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.finalize(world)
     return 0 if parity_ok else 3
+
+
+def dry_run(a, rank, world):
+    """Launcher + rank plumbing without a GPU (tests/test_bench_launch.py)."""
+    from bdls_amd import dist
+    dist.barrier(world)
+    t = dist.max_over_ranks(0.001 * (rank + 1), world)
+    ok = dist.all_true(True, world)
+    lo, hi = dist.shard_range(a.n_total if a.config == 5 else a.n * world, rank, world)
+    recs = dist.sum_over_ranks(hi - lo, world)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "config": a.config,
+                          "records_total": recs, "max_t": t, "parity": ok}), flush=True)
+    dist.finalize(world)
+    return 0
+
+
+def main(argv=None):
+    a = parse(argv)
+    from bdls_amd import dist
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(a.gpus)
+    rank, world, local = dist.env_rank()
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch with "
+                         f"--nproc-per-node {a.gpus}, or drop the launcher")
+    dist.init(world)
+    if a.dry_run:
+        return dry_run(a, rank, world)
+    if a.config in (3, 4):
+        return bench_latency(a, rank, world, local)
+    return bench_throughput(a, rank, world, local)
 
 
 if __name__ == "__main__":

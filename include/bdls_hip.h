@@ -110,6 +110,25 @@ size_t bh_workspace_bytes(size_t n);
 int bh_verify(int curve, const bh_batch *b, size_t n, uint32_t flags, uint8_t *bitmap,
               uint8_t *reason);
 
+/* Asynchronous form of bh_verify (the pipelined BatchVerify): enqueues the
+ * upload (copy stream), the verify passes and the result download (compute
+ * stream) on every device and returns at once with *job. bh_verify_wait(job)
+ * blocks until the batch is done, writes bitmap / reason and frees the job;
+ * every submitted job must be waited exactly once. The caller's input
+ * buffers must stay valid and unchanged until then. With two jobs in flight
+ * per device, the next batch's H2D runs under this batch's kernels; this needs
+ * page-locked inputs (bh_host_alloc) -- pageable inputs are correct but their
+ * upload is staged synchronously by the HIP runtime. bh_verify = submit+wait. */
+typedef struct bh_job bh_job;
+int bh_verify_submit(int curve, const bh_batch *b, size_t n, uint32_t flags, uint8_t *bitmap,
+                     uint8_t *reason, bh_job **job);
+int bh_verify_wait(bh_job *job);
+
+/* Page-locked host memory, DMA-able by every device (hipHostMalloc portable).
+ * A cgo caller packs its SoA batch straight into it (no further copy). */
+int bh_host_alloc(size_t bytes, void **ptr);
+int bh_host_free(void *ptr);
+
 /* Device-resident batch on one device: every pointer in *b and the outputs
  * are device pointers on `device`. Enqueued on `stream` (hipStream_t; NULL =
  * the library's stream for that device) and synchronised before return when

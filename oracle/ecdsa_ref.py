@@ -27,7 +27,7 @@ Parity pinning: the DER rules are pinned by the reference's own fixed vectors
 (bccsp/sw/impl_test.go:924-961, bccsp/utils/ecdsa_test.go:19-110) and the curve
 arithmetic by the fixed certificate fixture msp/testdata/mspid (a real P-256
 ECDSA-SHA256 signature chain produced outside this repo); the full fixture set is
-additionally cross-checked against OpenSSL libcrypto (oracle/xcheck_openssl.c).
+additionally cross-checked against OpenSSL libcrypto (oracle/orc.c).
 """
 from __future__ import annotations
 

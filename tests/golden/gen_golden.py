@@ -9,7 +9,7 @@ Outputs (committed):
 
 Every expected (valid, reason) comes from oracle/ecdsa_ref.py (the CPU
 restatement); tests/test_oracle_golden.py re-derives them and
-oracle/xcheck_openssl.c cross-checks the curve math against OpenSSL libcrypto.
+oracle/orc.c cross-checks the curve math against OpenSSL libcrypto.
 
 Sources of fixed data from the reference (read as data, never executed):
   * bccsp/sw/impl_test.go:924-961      five DER vectors that must be rejected

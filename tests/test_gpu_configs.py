@@ -1,0 +1,181 @@
+"""GPU parity on the shapes BASELINE configs 3 and 5 actually hit, plus the
+host-API pipeline (bh_verify_submit / bh_verify_wait, page-locked inputs).
+
+Bit-exact bar as everywhere: bitmap AND per-record reason equal the expected
+results (by construction, confirmed on samples against oracle/orc.c).
+  * config 3: one block (generate_block: 500 creators over 4 KB + 1,500
+    endorsements over 1.5 KB), cold (ladder) and warm (registered keys);
+  * the multi-pass loop for batches above the 4M-record pass size
+    (bdls_hip.cpp run_dev) at its real size, and forced on small batches with
+    BH_MAX_CHUNK, with kept keys (registry ids mixed with per-batch ids in the
+    key-sorted comb list);
+  * the key-table overflow route: more than 65,536 keys used >= 4 times, so
+    k_key_plan drops builds past max_tables and those records take the ladder.
+"""
+import ctypes
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from bdls_amd import _lib, workload
+from oracle import orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    _lib.ensure_init()
+    return _lib.lib()
+
+
+def host_verify(L, w, flags=_lib.BH_F_HASH_SHA256):
+    n = w.n
+    bm = np.zeros((n + 7) // 8 or 1, np.uint8)
+    rs = np.zeros(n or 1, np.uint8)
+    b = _lib.BhBatch(*[x.ctypes.data for x in w.arrays()])
+    _lib.check(L.bh_verify(0, ctypes.byref(b), n, flags, bm.ctypes.data, rs.ctypes.data))
+    return np.unpackbits(bm, bitorder="little")[:n].astype(bool), rs[:n]
+
+
+def dev_verify(L, w, flags=_lib.BH_F_HASH_SHA256):
+    DA = _lib.DeviceArray
+    d = [DA.from_numpy(0, x) for x in w.arrays()]
+    words = DA(0, ((w.n + 63) // 64) * 8)
+    reason = DA(0, w.n)
+    b = _lib.BhBatch(*[x.ptr for x in d])
+    tm = _lib.BhTiming()
+    _lib.check(L.bh_verify_dev(0, 0, ctypes.byref(b), w.n, flags, words.ptr, reason.ptr, None, 1,
+                               ctypes.byref(tm)))
+    bits = np.unpackbits(words.to_numpy(np.uint64, (w.n + 63) // 64).view(np.uint8),
+                         bitorder="little")[:w.n].astype(bool)
+    out = bits, reason.to_numpy(np.uint8, w.n), tm
+    for x in d + [words, reason]:
+        x.free()
+    return out
+
+
+def orc_sample(w, k, seed=0):
+    idx = np.random.default_rng(seed).choice(w.n, k, replace=False)
+    for i in idx:
+        q = bytes(w.pub[64 * i:64 * i + 64])
+        s = bytes(w.sig[w.sig_off[i]:w.sig_off[i] + w.sig_len[i]])
+        dg = hashlib.sha256(bytes(w.msg[w.msg_off[i]:w.msg_off[i] + w.msg_len[i]])).digest()
+        assert orc.csp_verify(q, s, dg) == w.reason[i], i
+
+
+def test_config3_block_cold_and_warm(L):
+    """BASELINE config 3 through the host ABI: cold (no key known: ladder) and
+    warm (the block's 54 keys registered: key-table path)."""
+    w = workload.generate_block(seed=3)
+    assert w.n == 2000
+    orc_sample(w, 300)
+    _lib.check(L.bh_keys_clear(-1, 0))
+    valid, reason = host_verify(L, w)
+    assert (reason == w.reason).all() and (valid == w.expected_valid).all()
+    _, dreason, tm = dev_verify(L, w)
+    assert (dreason == w.reason).all() and tm.n_keycomb == 0
+    pubs = np.unique(w.pub.reshape(-1, 64), axis=0)
+    st = np.zeros(len(pubs), np.uint8)
+    _lib.check(L.bh_keys_register(-1, 0, np.ascontiguousarray(pubs).ctypes.data, len(pubs),
+                                  st.ctypes.data))
+    # the off-curve / >= p corruptions are not valid keys; every real key registers
+    good = st == 0
+    assert good.sum() >= 54
+    valid, reason = host_verify(L, w)
+    assert (reason == w.reason).all() and (valid == w.expected_valid).all()
+    _, dreason, tm = dev_verify(L, w)
+    assert (dreason == w.reason).all()
+    assert tm.n_keycomb >= 0.97 * (tm.n_keycomb + tm.n_ladder)
+    _lib.check(L.bh_keys_clear(-1, 0))
+
+
+def test_pass_loop_real_size(L):
+    """4M + 65 records: the library's multi-pass loop (4,194,304-record passes),
+    one full pass and a ragged 65-record one, on the host and device APIs."""
+    n = (1 << 22) + 65
+    w = workload.generate(n, 4096, 64, 16, seed=41)
+    valid, reason = host_verify(L, w)
+    assert (reason == w.reason).all()
+    assert (valid == w.expected_valid).all()
+    bits, dreason, _ = dev_verify(L, w)
+    assert (dreason == w.reason).all() and (bits == w.expected_valid).all()
+    # the records straddling the pass boundary, against the oracle
+    for i in range((1 << 22) - 3, n):
+        q = bytes(w.pub[64 * i:64 * i + 64])
+        s = bytes(w.sig[w.sig_off[i]:w.sig_off[i] + w.sig_len[i]])
+        dg = hashlib.sha256(bytes(w.msg[w.msg_off[i]:w.msg_off[i] + w.msg_len[i]])).digest()
+        assert orc.csp_verify(q, s, dg) == reason[i]
+
+
+@pytest.fixture
+def small_chunks():
+    os.environ["BH_MAX_CHUNK"] = "131072"
+    yield 131072
+    del os.environ["BH_MAX_CHUNK"]
+
+
+def test_pass_loop_forced_with_kept_keys(L, small_chunks):
+    """200k records in 131,072-record passes with BH_F_KEEP_KEYS and a small
+    registry: pass 1 fills the registry and overflows to per-batch tables, so
+    the key-sorted comb list mixes registry ids and per-batch ids; pass 2 hits
+    the registry. Host and device APIs, twice (second call: all keys kept)."""
+    w = workload.generate(200_000, 3000, 100, 16, seed=42)
+    _lib.check(L.bh_keys_reserve(0, 0, 1024))
+    try:
+        for _ in range(2):
+            valid, reason = host_verify(L, w, _lib.BH_F_HASH_SHA256 | _lib.BH_F_KEEP_KEYS)
+            assert (reason == w.reason).all() and (valid == w.expected_valid).all()
+        cnt = ctypes.c_size_t()
+        _lib.check(L.bh_keys_count(0, 0, ctypes.byref(cnt)))
+        assert cnt.value == 1024
+        bits, dreason, tm = dev_verify(L, w, _lib.BH_F_HASH_SHA256 | _lib.BH_F_KEEP_KEYS)
+        assert (dreason == w.reason).all() and (bits == w.expected_valid).all()
+        assert tm.n_keycomb > 0.9 * (tm.n_keycomb + tm.n_ladder)
+    finally:
+        _lib.check(L.bh_keys_reserve(0, 0, 65536))
+        _lib.check(L.bh_keys_clear(0, 0))
+
+
+def test_key_table_overflow_to_ladder(L):
+    """600k records over 100k keys (~85k keys used >= 4 times): k_key_plan
+    builds the first 65,536 tables and the rest of the repeated keys' records
+    are routed to the variable-base ladder."""
+    w = workload.generate(600_000, 100_000, 64, 16, seed=43)
+    bits, reason, tm = dev_verify(L, w)
+    assert (reason == w.reason).all() and (bits == w.expected_valid).all()
+    assert tm.n_keytables == 65536
+    assert tm.n_ladder > 50_000 and tm.n_keycomb > 300_000
+    orc_sample(w, 200, seed=1)
+
+
+def test_submit_wait_pipeline(L):
+    """Several batches in flight from page-locked buffers: slot reuse collects
+    an uncollected batch early, waits may come in any order."""
+    ws = [workload.generate(30_000 + 777 * k, 500, 128, 8, seed=50 + k) for k in range(4)]
+    keep, jobs = [], []
+    for w in ws:
+        arrs = []
+        for x in w.arrays():
+            h, v = _lib.HostArray.from_numpy(x)
+            keep.append(h)
+            arrs.append(v)
+        b = _lib.BhBatch(*[x.ctypes.data for x in arrs])
+        keep.append(b)
+        bm = np.zeros((w.n + 7) // 8, np.uint8)
+        rs = np.zeros(w.n, np.uint8)
+        job = ctypes.c_void_p()
+        _lib.check(L.bh_verify_submit(0, ctypes.byref(b), w.n, _lib.BH_F_HASH_SHA256,
+                                      bm.ctypes.data, rs.ctypes.data, ctypes.byref(job)))
+        jobs.append((job, bm, rs, w))
+    for job, bm, rs, w in [jobs[2], jobs[0], jobs[3], jobs[1]]:
+        _lib.check(L.bh_verify_wait(job))
+        assert (rs == w.reason).all()
+        assert (np.unpackbits(bm, bitorder="little")[:w.n].astype(bool) == w.expected_valid).all()
+    # an empty batch is a valid job
+    job = ctypes.c_void_p()
+    b = _lib.BhBatch(*([0] * 7))
+    _lib.check(L.bh_verify_submit(0, ctypes.byref(b), 0, 0, None, None, ctypes.byref(job)))
+    _lib.check(L.bh_verify_wait(job))
