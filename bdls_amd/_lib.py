@@ -28,7 +28,7 @@ EXPORTS = (
     "bh_parse_der_sig", "bh_dev_alloc", "bh_dev_free", "bh_memcpy_h2d", "bh_memcpy_d2h",
     "bh_sync", "bh_verify_bdls", "bh_verify_bdls_dev", "bh_keys_reserve", "bh_keys_register",
     "bh_keys_clear", "bh_keys_count", "bh_timing_begin", "bh_timing_end", "bh_bdls_preverify",
-    "bh_verify_submit", "bh_verify_wait", "bh_host_alloc", "bh_host_free",
+    "bh_verify_submit", "bh_verify_wait", "bh_host_alloc", "bh_host_free", "bh_csp_stats",
 )
 KEY_FULL = 255  # bh_keys_register status: registry full
 
@@ -111,6 +111,8 @@ def lib() -> ctypes.CDLL:
         L.bh_csp_verify_p256.argtypes = [vp, vp, sz, vp, sz, ctypes.POINTER(i32),
                                          ctypes.POINTER(i32)]
         L.bh_csp_verify_p256.restype = i32
+        L.bh_csp_stats.argtypes = [vp]
+        L.bh_csp_stats.restype = i32
         L.bh_parse_der_sig.argtypes = [vp, sz, vp, vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         L.bh_parse_der_sig.restype = i32
         L.bh_verify_bdls.argtypes = [i32, ctypes.POINTER(BhBdlsBatch), sz, vp, vp]

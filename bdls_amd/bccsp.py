@@ -156,9 +156,16 @@ class HipCSP:
             raise BCCSPError(-1, "Invalid Key. It must not be nil.")
         if not isinstance(k, ECDSAPublicKey) or k.curve != "P-256":
             raise BCCSPError(-1, f"Unsupported 'VerifyKey' provided [{k}]")
-        valid, reason = verify_packed(*pack_records([k], [bytes(signature or b"")],
-                                                    [bytes(digest or b"")]), flags=self._flags)
-        return self._result(int(reason[0]), bool(valid[0]), opts)
+        sig, dg = bytes(signature or b""), bytes(digest or b"")
+        if self._flags:  # a no-low-S provider: plain one-record batch
+            valid, reason = verify_packed(*pack_records([k], [sig], [dg]), flags=self._flags)
+            return self._result(int(reason[0]), bool(valid[0]), opts)
+        # bh_csp_verify_p256: concurrent callers share device passes (coalescer);
+        # ctypes releases the GIL for the call
+        v, r = ctypes.c_int(), ctypes.c_int()
+        _lib.check(_lib.lib().bh_csp_verify_p256(k.raw64(), sig, len(sig), dg, len(dg),
+                                                 ctypes.byref(v), ctypes.byref(r)))
+        return self._result(r.value, bool(v.value), opts)
 
     def _result(self, reason: int, valid: bool, opts) -> bool:
         if reason in ERROR_REASONS:

@@ -10,6 +10,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <memory>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -705,6 +709,170 @@ int for_devices(int device, const std::function<int(Dev&)>& fn) {
   return BH_OK;
 }
 
+// ---- coalescing single-signature verifier -------------------------------------
+// BCCSP.Verify is called one signature at a time by up to validatorPoolSize
+// goroutines (core/peer/config.go:269-272, fan-out v20/validator.go:193-208),
+// plus the orderer's broadcast handlers. bh_csp_verify_p256 does not run a
+// device pass per call: callers append their record to the batch being
+// filled and block; one flusher thread submits that batch whenever a
+// pipeline slot is free (so a lone caller is flushed at once, and under load
+// the records that arrive while one batch is on the device ride together in
+// the next), optionally lingering BH_COALESCE_US microseconds for more
+// arrivals when nothing is in flight. Results are bit-identical to a
+// one-record batch: records are independent.
+struct CspReq {
+  int valid = 0, reason = 0, rc = BH_OK;
+  std::string err;
+  bool done = false;
+};
+
+struct CspBatch {
+  std::vector<uint8_t> pub, sig, dg;
+  std::vector<uint64_t> sig_off, dg_off;
+  std::vector<uint32_t> sig_len, dg_len;
+  std::vector<CspReq*> reqs;
+  std::vector<uint8_t> bitmap, reason;
+  bh_job* job = nullptr;
+  bh_batch b{};
+  void clear() {
+    pub.clear(); sig.clear(); dg.clear();
+    sig_off.clear(); dg_off.clear(); sig_len.clear(); dg_len.clear();
+    reqs.clear();
+    job = nullptr;
+  }
+};
+
+struct Coalescer {
+  std::mutex mu;
+  std::condition_variable cv_work, cv_done;
+  std::unique_ptr<CspBatch> filling{new CspBatch()};
+  std::deque<std::unique_ptr<CspBatch>> inflight;
+  std::vector<std::unique_ptr<CspBatch>> spare;
+  std::thread th;
+  bool running = false, stop = false;
+  uint64_t n_req = 0, n_batch = 0, max_batch = 0;
+  size_t cap = 65536;      // records per batch at most
+  size_t max_inflight = 2; // = pipeline slots per device
+  long linger_us = 0;
+
+  void complete(CspBatch& b, int rc, const std::string& err) {
+    for (size_t i = 0; i < b.reqs.size(); i++) {
+      CspReq* r = b.reqs[i];
+      r->done = true;
+      r->rc = rc;
+      r->err = err;
+      if (rc == BH_OK) {
+        r->valid = (b.bitmap[i >> 3] >> (i & 7)) & 1;
+        r->reason = b.reason[i];
+      }
+    }
+  }
+
+  void run() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv_work.wait(lk, [&] { return stop || !filling->reqs.empty() || !inflight.empty(); });
+      if (stop && filling->reqs.empty() && inflight.empty()) return;
+      if (!filling->reqs.empty() && inflight.size() < max_inflight) {
+        if (inflight.empty() && linger_us > 0 && filling->reqs.size() < cap && !stop) {
+          const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(linger_us);
+          cv_work.wait_until(lk, until, [&] { return stop || filling->reqs.size() >= cap; });
+        }
+        std::unique_ptr<CspBatch> b = std::move(filling);
+        if (spare.empty()) {
+          filling.reset(new CspBatch());
+        } else {
+          filling = std::move(spare.back());
+          spare.pop_back();
+        }
+        filling->clear();
+        const size_t n = b->reqs.size();
+        n_req += n;
+        n_batch++;
+        max_batch = std::max<uint64_t>(max_batch, n);
+        lk.unlock();
+        b->bitmap.assign((n + 7) / 8, 0);
+        b->reason.assign(n, 0);
+        b->b = bh_batch{b->pub.data(), b->sig.data(), b->sig_off.data(), b->sig_len.data(),
+                        b->dg.data(), b->dg_off.data(), b->dg_len.data()};
+        int rc = submit_job(BH_CURVE_P256, &b->b, n, 0u, b->bitmap.data(), b->reason.data(),
+                            &b->job);
+        const std::string err = rc ? g_err : std::string();
+        lk.lock();
+        if (rc) {
+          complete(*b, rc, err);
+          spare.push_back(std::move(b));
+          cv_done.notify_all();
+        } else {
+          inflight.push_back(std::move(b));
+        }
+        continue;
+      }
+      if (!inflight.empty()) {
+        std::unique_ptr<CspBatch> b = std::move(inflight.front());
+        inflight.pop_front();
+        lk.unlock();
+        int rc = wait_job(b->job);
+        const std::string err = rc ? g_err : std::string();
+        lk.lock();
+        complete(*b, rc, err);
+        spare.push_back(std::move(b));
+        cv_done.notify_all();
+      }
+    }
+  }
+
+  int verify(const uint8_t* pub, const uint8_t* sig, size_t sl, const uint8_t* dg, size_t dl,
+             int* valid, int* reason) {
+    CspReq req;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      if (!running) {
+        stop = false;
+        running = true;
+        th = std::thread([this] { run(); });
+      }
+      CspBatch& b = *filling;
+      b.pub.insert(b.pub.end(), pub, pub + 64);
+      b.sig_off.push_back(b.sig.size());
+      b.sig_len.push_back((uint32_t)sl);
+      if (sl) b.sig.insert(b.sig.end(), sig, sig + sl);
+      b.dg_off.push_back(b.dg.size());
+      b.dg_len.push_back((uint32_t)dl);
+      if (dl) b.dg.insert(b.dg.end(), dg, dg + dl);
+      b.reqs.push_back(&req);
+      cv_work.notify_one();
+      cv_done.wait(lk, [&] { return req.done; });
+    }
+    if (req.rc) return fail(req.rc, req.err);
+    *valid = req.valid;
+    *reason = req.reason;
+    return BH_OK;
+  }
+
+  void shutdown() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!running) return;
+      stop = true;
+    }
+    cv_work.notify_all();
+    th.join();
+    std::lock_guard<std::mutex> lk(mu);
+    running = false;
+    stop = false;
+  }
+};
+
+Coalescer& coalescer() {
+  static Coalescer* c = [] {
+    Coalescer* x = new Coalescer();
+    if (const char* e = getenv("BH_COALESCE_US")) x->linger_us = std::max(0L, atol(e));
+    return x;
+  }();
+  return *c;
+}
+
 }  // namespace
 
 extern "C" {
@@ -737,6 +905,7 @@ int bh_init(uint32_t device_mask, uint32_t flags) {
 }
 
 int bh_shutdown(void) {
+  coalescer().shutdown();  // drains queued single-signature calls first
   std::lock_guard<std::mutex> g(g_mu);
   for (Dev* d : g_devs) {
     dev_free(*d);
@@ -823,15 +992,20 @@ int bh_host_free(void* ptr) {
 int bh_csp_verify_p256(const uint8_t pub[64], const uint8_t* sig, size_t sig_len,
                        const uint8_t* digest, size_t digest_len, int* valid, int* reason) {
   if (!pub || !valid || !reason) return fail(BH_E_INVALID, "null argument");
-  static const uint8_t empty = 0;
-  uint64_t so = 0, mo = 0;
-  uint32_t sl = (uint32_t)sig_len, ml = (uint32_t)digest_len;
-  bh_batch b{pub, sig ? sig : &empty, &so, &sl, digest ? digest : &empty, &mo, &ml};
-  uint8_t bm = 0, rs = 0;
-  int rc = bh_verify(BH_CURVE_P256, &b, 1, 0, &bm, &rs);
-  if (rc) return rc;
-  *valid = bm & 1;
-  *reason = rs;
+  if ((sig_len && !sig) || (digest_len && !digest)) return fail(BH_E_INVALID, "null argument");
+  if (sig_len > 0xffffffffull || digest_len > 0xffffffffull)
+    return fail(BH_E_INVALID, "argument too large");
+  if (all_devs().empty()) return fail(BH_E_NOT_INIT, "bh_init not called");
+  return coalescer().verify(pub, sig, sig_len, digest, digest_len, valid, reason);
+}
+
+int bh_csp_stats(uint64_t out[3]) {
+  if (!out) return fail(BH_E_INVALID, "null argument");
+  Coalescer& c = coalescer();
+  std::lock_guard<std::mutex> lk(c.mu);
+  out[0] = c.n_req;
+  out[1] = c.n_batch;
+  out[2] = c.max_batch;
   return BH_OK;
 }
 

@@ -291,7 +291,9 @@ def bench_latency(a, rank, world, local):
     if rank == 0 and a.cpu_baseline:
         from oracle import orc
         cpu = []
-        threads = a.cpu_threads or (os.cpu_count() or 1)
+        cpus = host_cpus()
+        threads = a.cpu_threads or int(min(cpus.get("affinity", cpus["nproc"]),
+                                           cpus.get("cgroup_quota_cpus", cpus["nproc"]))) or 1
         deadline = time.perf_counter() + 10.0
         while time.perf_counter() < deadline and len(cpu) < a.steps:
             t = time.perf_counter()
@@ -304,10 +306,10 @@ def bench_latency(a, rank, world, local):
         cores = threads if a.config == 3 else 1
         out["cpu_baseline"] = {
             "value": round(percentile(cpu, 50), 4), "unit": "ms", "cores": cores, "kind": "port",
-            "host_cpus": host_cpus(),
+            "host_cpus": cpus,
             "sample": f"the same {n} records, {len(cpu)} repetitions, p50; "
                       + ("identity.Verify semantics, OpenSSL ECDSA_do_verify, "
-                         f"{cores} threads (= os.cpu_count())" if a.config == 3 else
+                         f"{cores} threads (the CPUs this process may use)" if a.config == 3 else
                          "serial SignedProto.Verify as the consensus loop runs it "
                          "(BLAKE2b-256 + OpenSSL ECDSA_do_verify), 1 thread"),
             "parity": bool((got == expect).all()),
@@ -385,6 +387,37 @@ def load_counters(config: int, n_rank: int):
     return tr.get("source"), tr.get("kernels", {})
 
 
+def cpu_baseline(a, w, n):
+    """oracle/orc.c (Fabric DER + low-S rules restated in C, the ECDSA core in
+    OpenSSL's P-256 assembly) on this host's CPUs, on the first records of the
+    same batch. Timed twice: with the CPUs this process may actually use
+    (affinity mask and cgroup quota -- on the GPU box a 16-CPU quota of a
+    256-thread host) and with os.cpu_count() threads (nproc); `value` is the
+    faster of the two (the conservative baseline for the GPU's claim)."""
+    from oracle import orc
+    cpus = host_cpus()
+    usable = int(min(cpus.get("affinity", cpus["nproc"]),
+                     cpus.get("cgroup_quota_cpus", cpus["nproc"]))) or 1
+    m = min(a.cpu_sample, n)
+    runs = {}
+    for threads in sorted({a.cpu_threads or usable, cpus["nproc"]}):
+        t = time.perf_counter()
+        orc.batch_verify(w.pub[:64 * m].reshape(-1, 64), w.msg, w.msg_off[:m], w.msg_len[:m],
+                         w.sig, w.sig_off[:m], w.sig_len[:m], fused=True, nthreads=threads)
+        dt = time.perf_counter() - t
+        runs[threads] = {"value": round(m / dt, 1), "seconds": round(dt, 3)}
+    best = max(runs, key=lambda k: runs[k]["value"])
+    return {
+        "value": runs[best]["value"], "unit": "verifies/s", "cores": best, "kind": "port",
+        "host_cpus": cpus,
+        "by_threads": {str(k): v for k, v in runs.items()},
+        "per_thread": round(runs[best]["value"] / min(best, usable), 1),
+        "sample": f"first {m} records of the same batch, identity.Verify semantics (SHA-256 + "
+                  f"DER + low-S + ECDSA via OpenSSL ECDSA_do_verify), timed at {sorted(runs)} "
+                  f"threads (usable CPUs, os.cpu_count()); value = the faster",
+    }
+
+
 def bench_throughput(a, rank, world, local):
     from bdls_amd import _lib, dist, workload
     if a.config == 5:
@@ -446,6 +479,18 @@ def bench_throughput(a, rank, world, local):
 
     run_host(a.warmup)
     _lib.check(L.bh_sync(local))
+    # one batch alone (nothing in flight): H2D + verify + D2H latency, and the
+    # page-locked H2D bandwidth of the batch's largest array
+    t = time.perf_counter()
+    run_host(1)
+    single_ms = (time.perf_counter() - t) * 1e3
+    probe = _lib.DeviceArray(local, w.msg.nbytes)
+    t = time.perf_counter()
+    _lib.check(L.bh_memcpy_h2d(local, probe.ptr, w.msg.ctypes.data, w.msg.nbytes))
+    h2d_gbps = w.msg.nbytes / (time.perf_counter() - t) / 1e9
+    probe.free()
+    batch_bytes = sum(int(x.nbytes) for x in (w.pub, w.sig, w.sig_off, w.sig_len, w.msg,
+                                              w.msg_off, w.msg_len))
     dist.barrier(world)
     # Timed region: K host-buffer batches; HIP events around every stage of
     # every pass on the compute stream (bh_timing_begin/_end) give the
@@ -535,6 +580,10 @@ def bench_throughput(a, rank, world, local):
         },
         "parity": parity_ok,
         "hbm_resident": resident,
+        "host_path": {"single_batch_ms": round(single_ms, 3), "batch_bytes": batch_bytes,
+                      "h2d_gbps_pinned": round(h2d_gbps, 2),
+                      "note": "value amortises the first batch's upload (pipeline fill) "
+                              "over --steps batches"},
         "kernel_ms_per_step": {k: round(v / a.steps, 3) for k, v in kern.items()},
         "routes": routes,
         "roofline": {
@@ -578,20 +627,7 @@ def bench_throughput(a, rank, world, local):
             }
 
     if rank == 0 and world == 1 and a.cpu_baseline:
-        from oracle import orc
-        m = min(a.cpu_sample, n)
-        threads = a.cpu_threads or (os.cpu_count() or 1)
-        t = time.perf_counter()
-        orc.batch_verify(w.pub[:64 * m].reshape(-1, 64), w.msg, w.msg_off[:m], w.msg_len[:m],
-                         w.sig, w.sig_off[:m], w.sig_len[:m], fused=True, nthreads=threads)
-        dt = time.perf_counter() - t
-        out["cpu_baseline"] = {
-            "value": round(m / dt, 1), "unit": "verifies/s", "cores": threads,
-            "kind": "port", "host_cpus": host_cpus(),
-            "sample": f"first {m} records of the same batch, identity.Verify semantics "
-                      f"(SHA-256 + DER + low-S + ECDSA via OpenSSL ECDSA_do_verify), "
-                      f"{threads} threads = os.cpu_count(), {dt:.2f}s",
-        }
+        out["cpu_baseline"] = cpu_baseline(a, w, n)
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.finalize(world)

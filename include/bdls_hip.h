@@ -139,10 +139,21 @@ int bh_verify_dev(int device, int curve, const bh_batch *b, size_t n, uint32_t f
                   bh_timing *timing);
 
 /* Single signature with exact BCCSP.Verify semantics (the sw provider's
- * Verify for an ECDSA P-256 public key; runs on device 0). *valid = 1/0,
- * *reason = BH_R_*; return BH_OK unless the engine itself failed. */
+ * Verify for an ECDSA P-256 public key, bccsp/sw/impl.go:247-270). *valid =
+ * 1/0, *reason = BH_R_*; return BH_OK unless the engine itself failed.
+ * Concurrent callers are COALESCED (the drop-in Verify is called by up to
+ * validatorPoolSize goroutines at once, core/peer/config.go:269-272): each
+ * call joins the batch being filled and blocks; a library thread submits that
+ * batch as soon as a pipeline slot is free (a lone call goes at once; under
+ * load, calls arriving while one batch runs share the next device pass).
+ * BH_COALESCE_US (environment, default 0) makes an idle flusher linger that
+ * many microseconds for more calls. The caller's buffers are copied before
+ * the call blocks. */
 int bh_csp_verify_p256(const uint8_t pub[64], const uint8_t *sig, size_t sig_len,
                        const uint8_t *digest, size_t digest_len, int *valid, int *reason);
+/* Coalescer counters: out[0] single calls served, out[1] device batches they
+ * formed, out[2] largest batch. */
+int bh_csp_stats(uint64_t out[3]);
 
 /* Host-side Go-exact DER unmarshal (bccsp/utils/ecdsa.go:41-65). Returns the
  * reason (BH_R_OK, BH_R_DER, BH_R_R_NONPOS, BH_R_S_NONPOS); on BH_R_OK fills

@@ -218,6 +218,48 @@ def test_concurrent_callers(csp, golden):
     assert not errors
 
 
+def test_coalesced_single_verify_64_threads(csp, golden):
+    """64 threads calling the single-signature Verify concurrently (validator
+    pool of core/peer/config.go:269-272): every result matches the golden
+    vector, and the calls share device passes (bh_csp_stats)."""
+    import time
+    recs = golden[:160]
+    L = _lib.lib()
+    before = (ctypes.c_uint64 * 3)()
+    _lib.check(L.bh_csp_stats(before))
+    bad, calls = [], [0]
+    lock = threading.Lock()
+
+    def worker(j):
+        rng = random.Random(j)
+        for _ in range(40):
+            r = recs[rng.randrange(len(recs))]
+            k = ECDSAPublicKey(int(r["qx"], 16), int(r["qy"], 16))
+            try:
+                got = (csp.verify(k, bytes.fromhex(r["sig"]), bytes.fromhex(r["digest"])), 0)
+            except BCCSPError as e:
+                got = (False, e.reason)
+            want = (r["valid"], r["reason"] if r["reason"] in (1, 2, 3, 4, 5, 6) else 0)
+            with lock:
+                calls[0] += 1
+                if got != want:
+                    bad.append((r["tag"], got, want))
+
+    t = time.perf_counter()
+    th = [threading.Thread(target=worker, args=(j,)) for j in range(64)]
+    [x.start() for x in th]
+    [x.join() for x in th]
+    dt = time.perf_counter() - t
+    after = (ctypes.c_uint64 * 3)()
+    _lib.check(L.bh_csp_stats(after))
+    assert not bad, bad[:5]
+    reqs, batches = after[0] - before[0], after[1] - before[1]
+    assert reqs == calls[0] == 64 * 40
+    assert batches < reqs / 4, (reqs, batches)  # passes are shared
+    print(f"coalesced: {reqs} calls in {batches} device batches (max {after[2]}), "
+          f"{reqs / dt:.0f} verifies/s from 64 threads")
+
+
 @pytest.mark.parametrize("nkeys,min_frac", [(1, 0.99), (7, 0.99), (20_000, 0.0)])
 def test_key_routing(csp, nkeys, min_frac):
     """Both verify paths, bit-exact: repeated keys -> per-key tables, unique keys -> ladder."""
