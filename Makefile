@@ -23,7 +23,11 @@ $(LIB)/bdls_msg.o: $(CSRC)/bdls_msg.cpp include/bdls_hip.h
 	@mkdir -p $(LIB)
 	g++ -O2 -std=c++17 -fPIC -Wall -c $< -o $@
 
-$(LIB)/libbdlship.so: $(LIB)/verify_kernels.o $(LIB)/bdls_hip.o $(LIB)/bdls_msg.o
+$(LIB)/fabric.o: $(CSRC)/fabric.cpp $(HDRS)
+	@mkdir -p $(LIB)
+	g++ -O2 -std=c++17 -fPIC -Wall -Wno-unknown-pragmas -c $< -o $@
+
+$(LIB)/libbdlship.so: $(LIB)/verify_kernels.o $(LIB)/bdls_hip.o $(LIB)/bdls_msg.o $(LIB)/fabric.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
 $(LIB)/libbdlsgen.so: bdls_amd/workload/gen.c

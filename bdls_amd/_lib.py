@@ -29,6 +29,7 @@ EXPORTS = (
     "bh_sync", "bh_verify_bdls", "bh_verify_bdls_dev", "bh_keys_reserve", "bh_keys_register",
     "bh_keys_clear", "bh_keys_count", "bh_timing_begin", "bh_timing_end", "bh_bdls_preverify",
     "bh_verify_submit", "bh_verify_wait", "bh_host_alloc", "bh_host_free", "bh_csp_stats",
+    "bh_fabric_block_preverify",
 )
 KEY_FULL = 255  # bh_keys_register status: registry full
 
@@ -67,6 +68,18 @@ class BhBdlsMsgResult(ctypes.Structure):
                 ("type", ctypes.c_uint32), ("distinct_signers", ctypes.c_uint32),
                 ("height", ctypes.c_uint64), ("round", ctypes.c_uint64),
                 ("sp_first", ctypes.c_uint32), ("sp_count", ctypes.c_uint32)]
+
+
+class BhFabTx(ctypes.Structure):
+    """include/bdls_hip.h bh_fab_tx."""
+    _fields_ = [("status", ctypes.c_int32), ("type", ctypes.c_int32),
+                ("creator", ctypes.c_uint32), ("endorse_first", ctypes.c_uint32),
+                ("endorse_count", ctypes.c_uint32), ("valid_endorsers", ctypes.c_uint32)]
+
+
+BH_FAB_F_SHA3 = 1
+BH_FAB_F_KEEP_KEYS = 2
+BH_FAB_F_DECODE_ONLY = 4
 
 
 class EngineError(RuntimeError):
@@ -111,6 +124,9 @@ def lib() -> ctypes.CDLL:
         L.bh_csp_verify_p256.argtypes = [vp, vp, sz, vp, sz, ctypes.POINTER(i32),
                                          ctypes.POINTER(i32)]
         L.bh_csp_verify_p256.restype = i32
+        L.bh_fabric_block_preverify.argtypes = [vp, sz, u32, vp, sz, ctypes.POINTER(sz), vp, sz,
+                                                ctypes.POINTER(sz)]
+        L.bh_fabric_block_preverify.restype = i32
         L.bh_csp_stats.argtypes = [vp]
         L.bh_csp_stats.restype = i32
         L.bh_parse_der_sig.argtypes = [vp, sz, vp, vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]

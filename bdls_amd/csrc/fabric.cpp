@@ -1,0 +1,870 @@
+// Fabric block pre-verification (bh_fabric_block_preverify, include/bdls_hip.h).
+//
+// Host side of SURVEY.md 8(f) rank 1 (rows A9-A12): the peer validates a block
+// with one goroutine per transaction (core/committer/txvalidator/v20/
+// validator.go:180-265, validateTx :297-453), and every transaction costs one
+// creator signature check (core/common/validation/msgvalidation.go:26-64 via
+// ValidateTransaction :248-320) plus one check per endorsement inside the
+// endorsement-policy evaluation (statebased/validator_keylevel.go:244-282 ->
+// common/policies/policy.go:363-395 SignatureSetToValidIdentities), each a
+// separate bccsp Verify. Here the serialized block is decoded once, every
+// signature the validator would check is put into ONE device batch
+// (bh_verify, fused SHA-256 / SHA3-256 of the signed bytes), and the result
+// per transaction is returned in the validator's order of checks: the
+// verified-signature set the unchanged validator then consults.
+//
+// Wire decoding restates google.golang.org/protobuf v1.30.0 (vendored; the
+// runtime behind github.com/golang/protobuf v1.5.3 and fabric-protos-go
+// v0.3.1) internal/impl/decode.go unmarshalPointer + encoding/protowire:
+//   * tag: varint; field number in [1, 2^29-1]; wire type 4 (end group) at
+//     message level is an error; wire types 6 and 7 are errors;
+//   * a known field arriving with another wire type is an UNKNOWN field (kept,
+//     no error); unknown fields are consumed by ConsumeFieldValue (groups
+//     nest, end-group number must match);
+//   * varint: at most 10 bytes, the 10th <= 1; lengths past the end: error;
+//   * singular bytes / scalars: last occurrence wins; singular message fields
+//     MERGE across occurrences; repeated fields append;
+//   * proto3 `string` fields are UTF-8 validated (unicode/utf8.Valid) -- an
+//     invalid string fails the whole Unmarshal.
+// Identities: msp/mspimpl.go:398-422 deserializeIdentityInternal (pem.Decode,
+// x509.ParseCertificate, key import) is restated far enough to get the P-256
+// public key; an identity this code cannot resolve is reported as such and
+// left to the Go path (the verified set never claims what it did not check).
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/bdls_hip.h"
+#include "bh_common.h"
+#include "der.h"
+
+namespace bh {
+int host_fail(int code, const char* msg);
+}
+
+namespace {
+
+// ---------------------------------------------------------------- protobuf-go
+struct Span {
+  const uint8_t* p = nullptr;
+  size_t n = 0;
+  bool set = false;  // Go: non-nil slice
+};
+
+constexpr uint64_t kMaxField = (1ull << 29) - 1;  // protowire.MaxValidNumber
+
+// protowire.ConsumeVarint: bytes consumed, or 0 on error
+size_t pb_varint(const uint8_t* b, size_t n, uint64_t* v) {
+  uint64_t x = 0;
+  for (size_t i = 0; i < 10; i++) {
+    if (i >= n) return 0;                   // errCodeTruncated
+    const uint64_t y = b[i];
+    if (i == 9) {
+      if (y > 1) return 0;                  // errCodeOverflow
+      *v = x | (y << 63);
+      return 10;
+    }
+    x |= (y & 0x7f) << (7 * i);
+    if (y < 0x80) {
+      *v = x;
+      return i + 1;
+    }
+  }
+  return 0;
+}
+
+// protowire.consumeFieldValueD: bytes consumed by the value of a field with
+// wire type `typ` (and number `num` for groups), or 0 on error (a valid value
+// always consumes >= 1 byte: a bytes value has its length varint).
+size_t pb_field_value(uint64_t num, uint32_t typ, const uint8_t* b, size_t n, int depth) {
+  uint64_t v;
+  switch (typ) {
+    case 0:
+      return pb_varint(b, n, &v);
+    case 1:
+      return n >= 8 ? 8 : 0;
+    case 5:
+      return n >= 4 ? 4 : 0;
+    case 2: {
+      const size_t k = pb_varint(b, n, &v);
+      if (!k || v > n - k) return 0;
+      return k + (size_t)v;
+    }
+    case 3: {
+      if (depth < 0) return 0;  // errCodeRecursionDepth
+      size_t i = 0;
+      for (;;) {
+        uint64_t tag;
+        const size_t k = pb_varint(b + i, n - i, &tag);
+        if (!k) return 0;
+        const uint64_t num2 = tag >> 3;
+        if (num2 > 0x7fffffffull || num2 < 1) return 0;  // DecodeTag -1 / < MinValidNumber
+        i += k;
+        const uint32_t typ2 = (uint32_t)(tag & 7);
+        if (typ2 == 4) return num2 == num ? i : 0;
+        const size_t m = pb_field_value(num2, typ2, b + i, n - i, depth - 1);
+        if (!m) return 0;
+        i += m;
+      }
+    }
+    default:  // 4: errCodeEndGroup, 6/7: errCodeReserved
+      return 0;
+  }
+}
+
+// One decoded field of a message.
+struct Field {
+  uint64_t num;
+  uint32_t typ;
+  uint64_t v;  // varint value (typ 0)
+  Span s;      // bytes value (typ 2)
+};
+
+// Walks the fields of a message in order; `on` returns false to fail the
+// Unmarshal (a known field's own error). Returns false on a wire error.
+template <class F>
+bool pb_walk(const uint8_t* b, size_t n, F&& on) {
+  size_t i = 0;
+  while (i < n) {
+    uint64_t tag;
+    const size_t k = pb_varint(b + i, n - i, &tag);
+    if (!k) return false;
+    i += k;
+    const uint64_t num = tag >> 3;
+    if (num < 1 || num > kMaxField) return false;
+    const uint32_t typ = (uint32_t)(tag & 7);
+    if (typ == 4) return false;  // end group without a group (groupTag 0)
+    Field f{num, typ, 0, {}};
+    size_t m;
+    if (typ == 0) {
+      m = pb_varint(b + i, n - i, &f.v);
+    } else if (typ == 2) {
+      uint64_t len;
+      const size_t h = pb_varint(b + i, n - i, &len);
+      if (!h || len > n - i - h) return false;
+      f.s = Span{b + i + h, (size_t)len, true};
+      m = h + (size_t)len;
+    } else {
+      m = pb_field_value(num, typ, b + i, n - i, 10000);
+    }
+    if (!m) return false;
+    i += m;
+    if (!on(f)) return false;
+  }
+  return true;
+}
+
+// unicode/utf8.Valid
+bool utf8_valid(const uint8_t* p, size_t n) {
+  size_t i = 0;
+  while (i < n) {
+    const uint8_t c = p[i];
+    if (c < 0x80) {
+      i++;
+      continue;
+    }
+    size_t len;
+    uint8_t lo = 0x80, hi = 0xbf;
+    if (c >= 0xc2 && c <= 0xdf) len = 2;
+    else if (c == 0xe0) { len = 3; lo = 0xa0; }
+    else if (c >= 0xe1 && c <= 0xec) len = 3;
+    else if (c == 0xed) { len = 3; hi = 0x9f; }
+    else if (c >= 0xee && c <= 0xef) len = 3;
+    else if (c == 0xf0) { len = 4; lo = 0x90; }
+    else if (c >= 0xf1 && c <= 0xf3) len = 4;
+    else if (c == 0xf4) { len = 4; hi = 0x8f; }
+    else return false;
+    if (i + len > n) return false;
+    if (p[i + 1] < lo || p[i + 1] > hi) return false;
+    for (size_t k = 2; k < len; k++)
+      if (p[i + k] < 0x80 || p[i + k] > 0xbf) return false;
+    i += len;
+  }
+  return true;
+}
+
+// field helpers: true if the field was this one and consumed (or failed)
+inline bool is_bytes(const Field& f, uint64_t num) { return f.num == num && f.typ == 2; }
+inline bool is_varint(const Field& f, uint64_t num) { return f.num == num && f.typ == 0; }
+
+// ---- messages on the validation path (fabric-protos-go v0.3.1) ----
+struct Envelope {  // common.Envelope
+  Span payload, signature;
+};
+bool dec_envelope(Span in, Envelope* o) {
+  return pb_walk(in.p, in.n, [&](const Field& f) {
+    if (is_bytes(f, 1)) o->payload = f.s;
+    else if (is_bytes(f, 2)) o->signature = f.s;
+    return true;
+  });
+}
+
+struct Header {  // common.Header
+  Span channel_header, signature_header;
+};
+bool dec_header_into(Span in, Header* o) {  // merges into *o
+  return pb_walk(in.p, in.n, [&](const Field& f) {
+    if (is_bytes(f, 1)) o->channel_header = f.s;
+    else if (is_bytes(f, 2)) o->signature_header = f.s;
+    return true;
+  });
+}
+
+struct Payload {  // common.Payload
+  bool has_header = false;
+  Header header;
+  Span data;
+};
+bool dec_payload(Span in, Payload* o) {
+  return pb_walk(in.p, in.n, [&](const Field& f) {
+    if (is_bytes(f, 1)) {
+      o->has_header = true;
+      return dec_header_into(f.s, &o->header);
+    }
+    if (is_bytes(f, 2)) o->data = f.s;
+    return true;
+  });
+}
+
+bool dec_timestamp(Span in) {  // google.protobuf.Timestamp: only wire errors matter
+  return pb_walk(in.p, in.n, [&](const Field&) { return true; });
+}
+
+struct ChannelHeader {  // common.ChannelHeader
+  int32_t type = 0;
+  uint64_t epoch = 0;
+  Span channel_id, tx_id;
+};
+bool dec_channel_header(Span in, ChannelHeader* o) {
+  return pb_walk(in.p, in.n, [&](const Field& f) {
+    if (is_varint(f, 1)) o->type = (int32_t)f.v;
+    else if (is_bytes(f, 3)) return dec_timestamp(f.s);
+    else if (is_bytes(f, 4)) { o->channel_id = f.s; return utf8_valid(f.s.p, f.s.n); }
+    else if (is_bytes(f, 5)) { o->tx_id = f.s; return utf8_valid(f.s.p, f.s.n); }
+    else if (is_varint(f, 6)) o->epoch = f.v;
+    return true;  // 2 version (int32), 7 extension, 8 tls_cert_hash: no checks
+  });
+}
+
+struct SignatureHeader {  // common.SignatureHeader
+  Span creator, nonce;
+};
+bool dec_signature_header(Span in, SignatureHeader* o) {
+  return pb_walk(in.p, in.n, [&](const Field& f) {
+    if (is_bytes(f, 1)) o->creator = f.s;
+    else if (is_bytes(f, 2)) o->nonce = f.s;
+    return true;
+  });
+}
+
+struct TxAction {  // peer.TransactionAction
+  Span header, payload;
+};
+bool dec_transaction(Span in, std::vector<TxAction>* acts) {  // peer.Transaction
+  return pb_walk(in.p, in.n, [&](const Field& f) {
+    if (!is_bytes(f, 1)) return true;
+    TxAction a;
+    bool ok = pb_walk(f.s.p, f.s.n, [&](const Field& g) {
+      if (is_bytes(g, 1)) a.header = g.s;
+      else if (is_bytes(g, 2)) a.payload = g.s;
+      return true;
+    });
+    acts->push_back(a);
+    return ok;
+  });
+}
+
+struct Endorsement {  // peer.Endorsement
+  Span endorser, signature;
+};
+struct EndorsedAction {  // peer.ChaincodeEndorsedAction
+  Span prp;
+  std::vector<Endorsement> endorsements;
+};
+bool dec_endorsed_action_into(Span in, EndorsedAction* o) {
+  return pb_walk(in.p, in.n, [&](const Field& f) {
+    if (is_bytes(f, 1)) {
+      o->prp = f.s;
+    } else if (is_bytes(f, 2)) {
+      Endorsement e;
+      bool ok = pb_walk(f.s.p, f.s.n, [&](const Field& g) {
+        if (is_bytes(g, 1)) e.endorser = g.s;
+        else if (is_bytes(g, 2)) e.signature = g.s;
+        return true;
+      });
+      o->endorsements.push_back(e);
+      return ok;
+    }
+    return true;
+  });
+}
+
+struct ActionPayload {  // peer.ChaincodeActionPayload
+  Span ccpp;
+  bool has_action = false;
+  EndorsedAction action;
+};
+bool dec_action_payload(Span in, ActionPayload* o) {
+  return pb_walk(in.p, in.n, [&](const Field& f) {
+    if (is_bytes(f, 1)) o->ccpp = f.s;
+    else if (is_bytes(f, 2)) {
+      o->has_action = true;
+      return dec_endorsed_action_into(f.s, &o->action);
+    }
+    return true;
+  });
+}
+
+bool dec_prp(Span in) {  // peer.ProposalResponsePayload: bytes fields only
+  return pb_walk(in.p, in.n, [&](const Field&) { return true; });
+}
+
+struct SerializedIdentity {  // msp.SerializedIdentity
+  Span mspid, id_bytes;
+};
+bool dec_serialized_identity(Span in, SerializedIdentity* o) {
+  return pb_walk(in.p, in.n, [&](const Field& f) {
+    if (is_bytes(f, 1)) { o->mspid = f.s; return utf8_valid(f.s.p, f.s.n); }
+    if (is_bytes(f, 2)) o->id_bytes = f.s;
+    return true;
+  });
+}
+
+bool dec_block(Span in, std::vector<Span>* data) {  // common.Block -> BlockData.data
+  return pb_walk(in.p, in.n, [&](const Field& f) {
+    if (is_bytes(f, 1)) {  // BlockHeader
+      return pb_walk(f.s.p, f.s.n, [&](const Field&) { return true; });
+    }
+    if (is_bytes(f, 2)) {  // BlockData (merges: entries append)
+      return pb_walk(f.s.p, f.s.n, [&](const Field& g) {
+        if (is_bytes(g, 1)) data->push_back(g.s);
+        return true;
+      });
+    }
+    if (is_bytes(f, 3)) {  // BlockMetadata
+      return pb_walk(f.s.p, f.s.n, [&](const Field&) { return true; });
+    }
+    return true;
+  });
+}
+
+// ---------------------------------------------------------------- PEM
+// Restates Go encoding/pem Decode (first block; type not checked by the MSP,
+// msp/mspimpl.go:400). Returns false when Go returns a nil block.
+size_t find(const uint8_t* d, size_t n, const char* pat, size_t from = 0) {
+  const size_t m = strlen(pat);
+  if (m > n) return SIZE_MAX;
+  for (size_t i = from; i + m <= n; i++)
+    if (!memcmp(d + i, pat, m)) return i;
+  return SIZE_MAX;
+}
+
+// getLine: first \n (or \r\n) delimited line, trailing spaces/tabs trimmed
+void get_line(const uint8_t* d, size_t n, size_t* line_len, size_t* rest_off) {
+  size_t i = 0;
+  while (i < n && d[i] != '\n') i++;
+  size_t j;
+  if (i == n) {
+    j = n;
+  } else {
+    j = i + 1;
+    if (i > 0 && d[i - 1] == '\r') i--;
+  }
+  while (i > 0 && (d[i - 1] == ' ' || d[i - 1] == '\t')) i--;
+  *line_len = i;
+  *rest_off = j;
+}
+
+int b64val(uint8_t c) {
+  if (c >= 'A' && c <= 'Z') return c - 'A';
+  if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+  if (c >= '0' && c <= '9') return c - '0' + 52;
+  if (c == '+') return 62;
+  if (c == '/') return 63;
+  return -1;
+}
+
+// base64.StdEncoding.Decode with \r and \n ignored (padding required).
+bool b64_decode(const std::vector<uint8_t>& in, std::vector<uint8_t>* out) {
+  std::vector<uint8_t> c;
+  c.reserve(in.size());
+  for (uint8_t x : in)
+    if (x != '\r' && x != '\n') c.push_back(x);
+  if (c.size() % 4) return false;
+  out->clear();
+  for (size_t q = 0; q < c.size(); q += 4) {
+    const bool last = q + 4 == c.size();
+    int v[4];
+    int pad = 0;
+    for (int k = 0; k < 4; k++) {
+      if (c[q + k] == '=') {
+        if (!last || k < 2) return false;
+        pad++;
+        v[k] = 0;
+        continue;
+      }
+      if (pad) return false;  // data after padding
+      v[k] = b64val(c[q + k]);
+      if (v[k] < 0) return false;
+    }
+    const uint32_t w = (uint32_t)v[0] << 18 | (uint32_t)v[1] << 12 | (uint32_t)v[2] << 6 | (uint32_t)v[3];
+    out->push_back((uint8_t)(w >> 16));
+    if (pad < 2) out->push_back((uint8_t)(w >> 8));
+    if (pad < 1) out->push_back((uint8_t)w);
+  }
+  return true;
+}
+
+bool pem_decode(const uint8_t* data, size_t n, std::vector<uint8_t>* der) {
+  static const char kStart[] = "\n-----BEGIN ";
+  static const char kEnd[] = "\n-----END ";
+  size_t rest = 0;  // offset of `rest` in data
+  for (;;) {
+    if (n - rest >= 11 && !memcmp(data + rest, kStart + 1, 11)) {
+      rest += 11;
+    } else {
+      const size_t at = find(data, n, kStart, rest);
+      if (at == SIZE_MAX) return false;
+      rest = at + 12;
+    }
+    size_t ll, ro;
+    get_line(data + rest, n - rest, &ll, &ro);
+    const uint8_t* type_line = data + rest;
+    if (ll < 5 || memcmp(type_line + ll - 5, "-----", 5)) {
+      rest += ro;
+      continue;
+    }
+    const size_t tlen = ll - 5;
+    rest += ro;
+    int headers = 0;
+    for (;;) {
+      if (rest >= n) return false;
+      get_line(data + rest, n - rest, &ll, &ro);
+      const uint8_t* colon = (const uint8_t*)memchr(data + rest, ':', ll);
+      if (!colon) break;
+      headers++;  // (a repeated key still counts; the MSP's PEMs carry none)
+      rest += ro;
+    }
+    size_t end_idx, trailer;
+    if (headers == 0 && n - rest >= 9 && !memcmp(data + rest, kEnd + 1, 9)) {
+      end_idx = rest;
+      trailer = rest + 9;
+    } else {
+      end_idx = find(data, n, kEnd, rest);
+      if (end_idx == SIZE_MAX) continue;  // Go: continue (searches again from rest)
+      trailer = end_idx + 10;
+    }
+    const size_t tl = tlen + 5;
+    if (n - trailer < tl) continue;
+    if (memcmp(data + trailer, type_line, tlen) || memcmp(data + trailer + tlen, "-----", 5))
+      continue;
+    get_line(data + trailer + tl, n - trailer - tl, &ll, &ro);
+    if (ll != 0) continue;
+    std::vector<uint8_t> b64;
+    for (size_t i = rest; i < end_idx; i++)
+      if (data[i] != ' ' && data[i] != '\t') b64.push_back(data[i]);
+    if (!b64_decode(b64, der)) continue;
+    return true;
+  }
+}
+
+// ---------------------------------------------------------------- X.509
+// Minimal DER walk to the subject public key (RFC 5280 Certificate ->
+// tbsCertificate -> subjectPublicKeyInfo) and the certificate signature.
+struct Tlv {
+  uint8_t tag;
+  const uint8_t* p;  // content
+  size_t n;
+  const uint8_t* raw;  // whole TLV
+  size_t raw_n;
+};
+
+bool tlv(const uint8_t* b, size_t n, size_t* off, Tlv* t) {
+  if (*off >= n) return false;
+  const size_t start = *off;
+  t->tag = b[(*off)++];
+  if ((t->tag & 0x1f) == 0x1f) return false;
+  if (*off >= n) return false;
+  size_t len = b[(*off)++];
+  if (len & 0x80) {
+    const size_t k = len & 0x7f;
+    if (k == 0 || k > 4 || *off + k > n) return false;
+    len = 0;
+    for (size_t i = 0; i < k; i++) len = len << 8 | b[(*off)++];
+    if (len < 0x80 || (k > 1 && (len >> ((k - 1) * 8)) == 0)) return false;  // non-minimal
+  }
+  if (len > n - *off) return false;
+  t->p = b + *off;
+  t->n = len;
+  t->raw = b + start;
+  t->raw_n = *off + len - start;
+  *off += len;
+  return true;
+}
+
+const uint8_t kOidEcPub[] = {0x2a, 0x86, 0x48, 0xce, 0x3d, 0x02, 0x01};
+const uint8_t kOidP256[] = {0x2a, 0x86, 0x48, 0xce, 0x3d, 0x03, 0x01, 0x07};
+const uint8_t kOidEcdsaSha256[] = {0x2a, 0x86, 0x48, 0xce, 0x3d, 0x04, 0x03, 0x02};
+
+struct Cert {
+  Tlv tbs;               // tbsCertificate (raw = the signed bytes)
+  uint8_t pub[64];       // subject P-256 key X || Y
+  bool p256 = false;
+  Tlv sig_alg_oid;       // outer signatureAlgorithm OID
+  Tlv sig;               // signatureValue BIT STRING content (after the unused-bits byte)
+  bool has_sig = false;
+};
+
+bool parse_cert(const uint8_t* d, size_t n, Cert* c) {
+  size_t off = 0;
+  Tlv cert;
+  if (!tlv(d, n, &off, &cert) || cert.tag != 0x30 || off != n) return false;
+  size_t o = 0;
+  if (!tlv(cert.p, cert.n, &o, &c->tbs) || c->tbs.tag != 0x30) return false;
+  Tlv alg, sv;
+  if (!tlv(cert.p, cert.n, &o, &alg) || alg.tag != 0x30) return false;
+  if (!tlv(cert.p, cert.n, &o, &sv) || sv.tag != 0x03 || sv.n < 1 || sv.p[0] != 0) return false;
+  size_t ao = 0;
+  if (!tlv(alg.p, alg.n, &ao, &c->sig_alg_oid) || c->sig_alg_oid.tag != 0x06) return false;
+  c->sig = Tlv{0x03, sv.p + 1, sv.n - 1, sv.raw, sv.raw_n};
+  c->has_sig = true;
+  // tbs: [0] version?, serial, signature, issuer, validity, subject, spki
+  size_t t = 0;
+  Tlv f;
+  if (!tlv(c->tbs.p, c->tbs.n, &t, &f)) return false;
+  if (f.tag == 0xa0 && !tlv(c->tbs.p, c->tbs.n, &t, &f)) return false;  // then serial
+  if (f.tag != 0x02) return false;
+  for (int k = 0; k < 4; k++)  // signature, issuer, validity, subject
+    if (!tlv(c->tbs.p, c->tbs.n, &t, &f) || f.tag != 0x30) return false;
+  Tlv spki;
+  if (!tlv(c->tbs.p, c->tbs.n, &t, &spki) || spki.tag != 0x30) return false;
+  size_t s = 0;
+  Tlv algid, bits;
+  if (!tlv(spki.p, spki.n, &s, &algid) || algid.tag != 0x30) return false;
+  if (!tlv(spki.p, spki.n, &s, &bits) || bits.tag != 0x03 || s != spki.n) return false;
+  size_t a = 0;
+  Tlv oid1, oid2;
+  if (!tlv(algid.p, algid.n, &a, &oid1) || oid1.tag != 0x06) return false;
+  if (!tlv(algid.p, algid.n, &a, &oid2)) return false;
+  c->p256 = oid1.n == sizeof(kOidEcPub) && !memcmp(oid1.p, kOidEcPub, sizeof(kOidEcPub)) &&
+            oid2.tag == 0x06 && oid2.n == sizeof(kOidP256) &&
+            !memcmp(oid2.p, kOidP256, sizeof(kOidP256)) && a == algid.n && bits.n == 66 &&
+            bits.p[0] == 0 && bits.p[1] == 0x04;
+  if (c->p256) memcpy(c->pub, bits.p + 2, 64);
+  return true;
+}
+
+// ---------------------------------------------------------------- identities
+// SerializedIdentity bytes -> resolved P-256 key + the identity key used by
+// SignatureSetToValidIdentities' de-duplication (Mspid + Id, where Id hashes
+// the SANITIZED certificate: newIdentity, msp/identities.go:55-85 ->
+// sanitizeCert -> sanitizeECDSASignedCert, msp/cert.go:76-116, which rewrites
+// an ECDSA certificate signature to low-S). Here: mspid || tbs || r || low-S s.
+struct Ident {
+  bool ok = false;
+  uint8_t pub[64];
+  std::string key;
+};
+
+constexpr uint32_t kP256HalfN[8] = {0x7e3192a8, 0x79dce561, 0xd38bcf42, 0xde737d56,
+                                    0xffffffff, 0x7fffffff, 0x80000000, 0x7fffffff};
+constexpr uint32_t kP256N[8] = {0xfc632551, 0xf3b9cac2, 0xa7179e84, 0xbce6faad,
+                                0xffffffff, 0xffffffff, 0x00000000, 0xffffffff};
+
+std::string dedupe_key(const Span& mspid, const Cert& c) {
+  std::string k((const char*)mspid.p, mspid.n);
+  k.push_back('\0');
+  k.append((const char*)c.tbs.raw, c.tbs.raw_n);
+  bh::DerSig ds;
+  memset(&ds, 0, sizeof(ds));
+  if (c.has_sig && bh::der_parse_sig(c.sig.p, (uint32_t)c.sig.n, &ds) == bh::R_OK && !ds.s_big &&
+      !ds.r_big) {
+    uint32_t s[8];
+    memcpy(s, ds.s, 32);
+    bool high = false;  // s > n/2 -> n - s
+    for (int i = 7; i >= 0; i--)
+      if (s[i] != kP256HalfN[i]) {
+        high = s[i] > kP256HalfN[i];
+        break;
+      }
+    if (high) {
+      uint64_t br = 0;
+      for (int i = 0; i < 8; i++) {
+        const uint64_t t = (uint64_t)kP256N[i] - s[i] - br;
+        s[i] = (uint32_t)t;
+        br = (t >> 63) & 1;
+      }
+    }
+    k.append((const char*)ds.r, 32);
+    k.append((const char*)s, 32);
+  } else if (c.has_sig) {
+    k.append((const char*)c.sig.p, c.sig.n);
+  }
+  return k;
+}
+
+Ident resolve(Span ser) {
+  Ident id;
+  SerializedIdentity si;
+  if (!dec_serialized_identity(ser, &si)) return id;
+  std::vector<uint8_t> der;
+  if (!si.id_bytes.set || !pem_decode(si.id_bytes.p, si.id_bytes.n, &der)) return id;
+  Cert c;
+  if (!parse_cert(der.data(), der.size(), &c) || !c.p256) return id;
+  id.ok = true;
+  memcpy(id.pub, c.pub, 64);
+  id.key = dedupe_key(si.mspid, c);
+  return id;
+}
+
+// Long-lived cache of resolved identities (the device-side twin of the MSP's
+// deserializer cache, msp/cache/cache.go): serialized bytes -> Ident.
+using IdentP = std::shared_ptr<const Ident>;
+struct IdentCache {
+  std::mutex mu;
+  std::unordered_map<std::string, IdentP> m;
+  static constexpr size_t kCap = 1 << 16;
+  IdentP get(Span ser) {
+    std::string k((const char*)ser.p, ser.n);
+    {
+      std::lock_guard<std::mutex> g(mu);
+      auto it = m.find(k);
+      if (it != m.end()) return it->second;
+    }
+    IdentP id = std::make_shared<const Ident>(resolve(ser));
+    std::lock_guard<std::mutex> g(mu);
+    if (m.size() >= kCap) m.clear();
+    m.emplace(std::move(k), id);
+    return id;
+  }
+};
+
+IdentCache& ident_cache() {
+  static IdentCache* c = new IdentCache();
+  return *c;
+}
+
+// ---------------------------------------------------------------- the block
+struct EndRec {
+  IdentP id;
+  Span endorser, sig, prp;
+  uint8_t out = BH_SP_NOT_VERIFIED;
+};
+
+struct TxRec {
+  int32_t status = BH_FAB_OK;
+  int32_t type = 0;
+  bool creator_check = false;  // creator signature goes to the device
+  IdentP creator;
+  Span payload, signature;
+  uint8_t creator_out = BH_SP_NOT_VERIFIED;
+  std::vector<EndRec> ends;
+  uint32_t valid_endorsers = 0;
+};
+
+// Go's order of checks up to the signatures (validateTx, ValidateTransaction,
+// validateEndorserTransaction). Checks that do not gate which signatures are
+// verified (CheckTxID, the proposal hash, ledger / channel state) are left to
+// the unchanged validator.
+void decode_tx(Span env_bytes, TxRec* t) {
+  Envelope env;
+  if (!dec_envelope(env_bytes, &env)) {
+    t->status = BH_FAB_ENVELOPE;  // GetEnvelopeFromBlock: INVALID_OTHER_REASON
+    return;
+  }
+  Payload pl;
+  if (!dec_payload(env.payload, &pl)) {
+    t->status = BH_FAB_PAYLOAD;  // BAD_PAYLOAD
+    return;
+  }
+  ChannelHeader ch;
+  SignatureHeader sh;
+  // validateCommonHeader: nil header, unmarshal ChannelHeader, SignatureHeader,
+  // validateChannelHeader (type, epoch), validateSignatureHeader (nonce, creator)
+  if (!pl.has_header || !dec_channel_header(pl.header.channel_header, &ch) ||
+      !dec_signature_header(pl.header.signature_header, &sh) ||
+      !(ch.type == 1 || ch.type == 2 || ch.type == 3) || ch.epoch != 0 || sh.nonce.n == 0 ||
+      sh.creator.n == 0) {
+    t->status = BH_FAB_HEADER;  // BAD_COMMON_HEADER
+    return;
+  }
+  t->type = ch.type;
+  // checkSignatureFromCreator: nil arguments, then DeserializeIdentity, Verify
+  t->payload = env.payload;
+  t->signature = env.signature;
+  if (!env.signature.set || !env.payload.set) {
+    t->status = BH_FAB_CREATOR_SIGNATURE;  // "nil arguments"
+  } else {
+    t->creator = ident_cache().get(sh.creator);
+    if (!t->creator->ok) t->status = BH_FAB_CREATOR_IDENTITY;
+    else t->creator_check = true;
+  }
+  if (ch.type == 2) {  // CONFIG_UPDATE: UNSUPPORTED_TX_PAYLOAD after the creator check
+    if (t->status == BH_FAB_OK) t->status = BH_FAB_UNSUPPORTED;
+    return;
+  }
+  if (ch.type != 3) return;  // CONFIG: no endorsements
+  // validateEndorserTransaction structure (reached only if the creator check
+  // passes; decoded regardless, so the endorsements ride in the same batch)
+  std::vector<TxAction> acts;
+  int32_t tx_status = BH_FAB_OK;
+  ActionPayload ap;
+  if (!dec_transaction(pl.data, &acts) || acts.size() != 1) {
+    tx_status = BH_FAB_TX;
+  } else {
+    SignatureHeader ash;
+    if (!dec_signature_header(acts[0].header, &ash) || ash.nonce.n == 0 || ash.creator.n == 0 ||
+        !dec_action_payload(acts[0].payload, &ap) ||
+        !ap.has_action /* Go dereferences a nil Action here */ ||
+        !dec_prp(ap.action.prp))
+      tx_status = BH_FAB_TX;
+  }
+  if (tx_status != BH_FAB_OK) {
+    if (t->status == BH_FAB_OK) t->status = tx_status;
+    return;
+  }
+  for (const Endorsement& e : ap.action.endorsements) {
+    EndRec r;
+    r.endorser = e.endorser;
+    r.sig = e.signature;
+    r.prp = ap.action.prp;
+    // SignatureSetToValidIdentities: DeserializeIdentity failure -> skipped
+    r.id = ident_cache().get(e.endorser);
+    if (!r.id->ok) r.out = BH_FAB_E_BAD_IDENTITY;
+    t->ends.push_back(r);
+  }
+}
+
+// One device batch of signatures: creator (payload) and endorsement
+// (prp || endorser) records, messages hashed on the device.
+struct Batch {
+  std::vector<uint8_t> pub, sig, msg;
+  std::vector<uint64_t> sig_off, msg_off;
+  std::vector<uint32_t> sig_len, msg_len;
+  std::vector<uint8_t*> dst;  // where each record's reason goes
+  void add(const uint8_t pub64[64], Span s, const Span* m, int nm, uint8_t* out) {
+    pub.insert(pub.end(), pub64, pub64 + 64);
+    sig_off.push_back(sig.size());
+    sig_len.push_back((uint32_t)s.n);
+    if (s.n) sig.insert(sig.end(), s.p, s.p + s.n);
+    msg_off.push_back(msg.size());
+    size_t L = 0;
+    for (int k = 0; k < nm; k++) {
+      if (m[k].n) msg.insert(msg.end(), m[k].p, m[k].p + m[k].n);
+      L += m[k].n;
+    }
+    msg_len.push_back((uint32_t)L);
+    dst.push_back(out);
+  }
+  size_t size() const { return dst.size(); }
+  int run(uint32_t flags) {
+    const size_t n = size();
+    if (!n) return BH_OK;
+    std::vector<uint8_t> bitmap((n + 7) / 8), reason(n);
+    sig.push_back(0);
+    msg.push_back(0);
+    bh_batch b{pub.data(), sig.data(), sig_off.data(), sig_len.data(),
+               msg.data(), msg_off.data(), msg_len.data()};
+    int rc = bh_verify(BH_CURVE_P256, &b, n, flags, bitmap.data(), reason.data());
+    if (rc) return rc;
+    for (size_t i = 0; i < n; i++) *dst[i] = reason[i];
+    return BH_OK;
+  }
+};
+
+}  // namespace
+
+extern "C" int bh_fabric_block_preverify(const uint8_t* block, size_t len, uint32_t flags,
+                                         bh_fab_tx* txs, size_t tx_cap, size_t* n_tx,
+                                         uint8_t* endorse, size_t endorse_cap,
+                                         size_t* n_endorse) {
+  if (!n_tx || !n_endorse || (len && !block))
+    return bh::host_fail(BH_E_INVALID, "null argument");
+  if (flags & ~(uint32_t)(BH_FAB_F_SHA3 | BH_FAB_F_KEEP_KEYS | BH_FAB_F_DECODE_ONLY))
+    return bh::host_fail(BH_E_INVALID, "unknown flag");
+  std::vector<Span> data;
+  if (!dec_block(Span{block, len, true}, &data))
+    return bh::host_fail(BH_E_INVALID, "block does not unmarshal (common.Block)");
+  std::vector<TxRec> t(data.size());
+  size_t n_end = 0;
+  for (size_t i = 0; i < data.size(); i++) {
+    decode_tx(data[i], &t[i]);
+    n_end += t[i].ends.size();
+  }
+  *n_tx = t.size();
+  *n_endorse = n_end;
+  if ((t.size() && (!txs || tx_cap < t.size())) || (n_end && (!endorse || endorse_cap < n_end)))
+    return bh::host_fail(BH_E_INVALID, "result buffers too small (see *n_tx, *n_endorse)");
+  const uint32_t vflags = ((flags & BH_FAB_F_SHA3) ? BH_F_HASH_SHA3_256 : BH_F_HASH_SHA256) |
+                          ((flags & BH_FAB_F_KEEP_KEYS) ? BH_F_KEEP_KEYS : 0u);
+  // Round 1: every creator signature, and per transaction the FIRST
+  // endorsement of each identity (SignatureSetToValidIdentities verifies a
+  // later one of the same identity only if the earlier ones failed).
+  Batch b;
+  for (TxRec& x : t) {
+    if (x.creator_check) b.add(x.creator->pub, x.signature, &x.payload, 1, &x.creator_out);
+    std::vector<const std::string*> seen;
+    for (EndRec& e : x.ends) {
+      if (!e.id->ok) continue;
+      bool dup = false;
+      for (const std::string* k : seen) dup |= (*k == e.id->key);
+      if (dup) continue;
+      seen.push_back(&e.id->key);
+      const Span m[2] = {e.prp, e.endorser};  // data = prp || endorser (validator_keylevel.go:248-250)
+      b.add(e.id->pub, e.sig, m, 2, &e.out);
+    }
+  }
+  const bool decode_only = (flags & BH_FAB_F_DECODE_ONLY) != 0;
+  if (decode_only) {
+    b = Batch();
+  } else if (int rc = b.run(vflags)) {
+    return rc;
+  }
+  // Replay the de-duplication in order; a failed first check of an identity
+  // makes Go verify its next occurrence: later rounds (rare) verify those.
+  for (int round = 0; round < 64; round++) {
+    Batch more;
+    for (TxRec& x : t) {
+      std::vector<const std::string*> valid;
+      for (EndRec& e : x.ends) {
+        if (!e.id->ok) continue;
+        bool dup = false;
+        for (const std::string* k : valid) dup |= (*k == e.id->key);
+        if (dup) {
+          e.out = BH_FAB_E_DUPLICATE;
+          continue;
+        }
+        if (e.out == BH_SP_NOT_VERIFIED) {  // reached: verify it in the next round
+          const Span m[2] = {e.prp, e.endorser};
+          more.add(e.id->pub, e.sig, m, 2, &e.out);
+          break;  // later entries of this tx depend on this result
+        }
+        if (e.out == BH_R_OK) valid.push_back(&e.id->key);
+      }
+      x.valid_endorsers = (uint32_t)valid.size();
+    }
+    if (!more.size() || decode_only) break;
+    if (int rc = more.run(vflags)) return rc;
+  }
+  size_t k = 0;
+  for (size_t i = 0; i < t.size(); i++) {
+    TxRec& x = t[i];
+    // the creator check precedes the endorser-transaction checks
+    if (!decode_only && x.creator_check && x.creator_out != BH_R_OK &&
+        (x.status == BH_FAB_OK || x.status == BH_FAB_TX || x.status == BH_FAB_UNSUPPORTED))
+      x.status = BH_FAB_CREATOR_SIGNATURE;
+    txs[i].status = x.status;
+    txs[i].type = x.type;
+    txs[i].creator = x.creator_out;
+    txs[i].endorse_first = (uint32_t)k;
+    txs[i].endorse_count = (uint32_t)x.ends.size();
+    txs[i].valid_endorsers = x.valid_endorsers;
+    for (const EndRec& e : x.ends) endorse[k++] = e.out;
+  }
+  return BH_OK;
+}

@@ -1,0 +1,63 @@
+"""Host-side mirror of the block-validation batch point
+over bh_fabric_block_preverify (include/bdls_hip.h).
+
+The reference validates a block transaction by transaction
+(core/committer/txvalidator/v20/validator.go:180-265): per transaction one
+creator identity.Verify (core/common/validation/msgvalidation.go:26-64) and,
+inside the endorsement policy, one identity.Verify per de-duplicated endorser
+(common/policies/policy.go:363-395). `block_preverify` runs all of those
+signature checks for a whole serialized block as one device batch and returns
+them per transaction: the verified-signature set the unchanged validator
+consults.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+
+FAB_STATUS = {0: "OK", 1: "ENVELOPE", 2: "PAYLOAD", 3: "HEADER", 4: "CREATOR_IDENTITY",
+              5: "CREATOR_SIGNATURE", 6: "TX", 7: "UNSUPPORTED"}
+E_DUPLICATE, E_BAD_IDENTITY, NOT_VERIFIED = 253, 254, 255
+
+
+@dataclass
+class TxResult:
+    status: int
+    type: int
+    creator: int              # BH_R_* or NOT_VERIFIED
+    endorse: list[int]        # per endorsement: BH_R_*, E_DUPLICATE, E_BAD_IDENTITY, NOT_VERIFIED
+    valid_endorsers: int
+
+
+def block_preverify(block: bytes, sha3: bool = False, keep_keys: bool = False,
+                    decode_only: bool = False) -> list[TxResult]:
+    """All signature checks of one serialized common.Block in one device batch.
+    decode_only: host decode / identity resolution only (no device work)."""
+    L = _lib.lib()
+    if not decode_only:
+        _lib.ensure_init()
+    flags = ((_lib.BH_FAB_F_SHA3 if sha3 else 0) | (_lib.BH_FAB_F_KEEP_KEYS if keep_keys else 0)
+             | (_lib.BH_FAB_F_DECODE_ONLY if decode_only else 0))
+    buf = np.frombuffer(bytes(block) + b"\0", np.uint8)
+    ntx, nend = ctypes.c_size_t(), ctypes.c_size_t()
+    # sizing pass (decode only, no device work), then the real call
+    rc = L.bh_fabric_block_preverify(buf.ctypes.data, len(block), flags | _lib.BH_FAB_F_DECODE_ONLY,
+                                     None, 0, ctypes.byref(ntx), None, 0, ctypes.byref(nend))
+    if rc != 0 and (ntx.value == 0 and nend.value == 0):
+        _lib.check(rc)
+    txs = (_lib.BhFabTx * max(1, ntx.value))()
+    end = np.zeros(max(1, nend.value), np.uint8)
+    _lib.check(L.bh_fabric_block_preverify(buf.ctypes.data, len(block), flags, txs, ntx.value,
+                                           ctypes.byref(ntx), end.ctypes.data, nend.value,
+                                           ctypes.byref(nend)))
+    out = []
+    for i in range(ntx.value):
+        t = txs[i]
+        out.append(TxResult(t.status, t.type, t.creator,
+                            [int(x) for x in end[t.endorse_first:t.endorse_first + t.endorse_count]],
+                            t.valid_endorsers))
+    return out

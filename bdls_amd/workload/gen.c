@@ -623,3 +623,76 @@ int gen_bdls_wire_round(int curve, int nval, int t2p1, uint64_t seed, uint8_t *p
   EC_GROUP_free(g);
   return rc_ ? rc_ : k;
 }
+
+/* ---------------------------------------------------------------------------
+ * Helpers for the Fabric block generator (bdls_amd/workload/fabric.py): seeded
+ * P-256 key pairs and DER signatures over given 32-byte digests, signed as
+ * bccsp/sw/ecdsa.go:27-39 signs (ecdsa.Sign, ToLowS, MarshalECDSASignature).
+ * ------------------------------------------------------------------------- */
+int gen_p256_keypair(uint64_t seed, uint64_t idx, uint8_t *priv32, uint8_t *pub64) {
+  EC_GROUP *g = EC_GROUP_new_by_curve_name(NID_X9_62_prime256v1);
+  BN_CTX *ctx = BN_CTX_new();
+  BIGNUM *n = BN_new(), *d = BN_new(), *x = BN_new(), *y = BN_new();
+  EC_GROUP_get_order(g, n, ctx);
+  EC_POINT *Q = EC_POINT_new(g);
+  uint64_t st = seed * 0xff51afd7ed558ccdull + idx * 0xc4ceb9fe1a85ec53ull + 7;
+  rand_scalar(&st, d, n, ctx);
+  EC_POINT_mul(g, Q, d, NULL, NULL, ctx);
+  EC_POINT_get_affine_coordinates(g, Q, x, y, ctx);
+  BN_bn2binpad(d, priv32, 32);
+  BN_bn2binpad(x, pub64, 32);
+  BN_bn2binpad(y, pub64 + 32, 32);
+  EC_POINT_free(Q);
+  BN_free(n); BN_free(d); BN_free(x); BN_free(y);
+  BN_CTX_free(ctx);
+  EC_GROUP_free(g);
+  return 0;
+}
+
+/* n signatures: record i signs digest i (32 B) with private key i (32 B);
+ * out + 80 i receives the DER signature, len[i] its length. high_s != 0
+ * leaves S as drawn (possibly > n/2) instead of normalising to low-S. */
+int gen_p256_sign_batch(size_t n, const uint8_t *priv, const uint8_t *digest, uint64_t seed,
+                        int high_s, uint8_t *out, uint32_t *len) {
+  EC_GROUP *g = EC_GROUP_new_by_curve_name(NID_X9_62_prime256v1);
+  BN_CTX *ctx = BN_CTX_new();
+  BIGNUM *nn = BN_new(), *half = BN_new(), *k = BN_new(), *kinv = BN_new(), *r = BN_new(),
+         *s = BN_new(), *e = BN_new(), *d = BN_new(), *t = BN_new(), *x = BN_new();
+  EC_GROUP_get_order(g, nn, ctx);
+  BN_rshift1(half, nn);
+  EC_POINT *R = EC_POINT_new(g);
+  for (size_t i = 0; i < n; i++) {
+    uint64_t st = seed * 0x100000001b3ull + i * 0x9e3779b97f4a7c15ull + 0x51;
+    BN_bin2bn(priv + 32 * i, 32, d);
+    BN_bin2bn(digest + 32 * i, 32, e);
+    BN_nnmod(e, e, nn, ctx);
+    do {
+      rand_scalar(&st, k, nn, ctx);
+      EC_POINT_mul(g, R, k, NULL, NULL, ctx);
+      EC_POINT_get_affine_coordinates(g, R, x, NULL, ctx);
+      BN_nnmod(r, x, nn, ctx);
+      BN_mod_inverse(kinv, k, nn, ctx);
+      BN_mod_mul(t, r, d, nn, ctx);
+      BN_mod_add(t, t, e, nn, ctx);
+      BN_mod_mul(s, kinv, t, nn, ctx);
+    } while (BN_is_zero(r) || BN_is_zero(s));
+    if (high_s) {
+      if (BN_cmp(s, half) <= 0) BN_sub(s, nn, s);
+    } else if (BN_cmp(s, half) > 0) {
+      BN_sub(s, nn, s);
+    }
+    uint8_t body[SIG_STRIDE], *o = out + (size_t)i * SIG_STRIDE;
+    size_t bl = der_int(body, r, 0, 0);
+    bl += der_int(body + bl, s, 0, 0);
+    o[0] = 0x30;
+    o[1] = (uint8_t)bl;
+    memcpy(o + 2, body, bl);
+    len[i] = (uint32_t)(bl + 2);
+  }
+  EC_POINT_free(R);
+  BIGNUM *v[] = {nn, half, k, kinv, r, s, e, d, t, x};
+  for (size_t q = 0; q < sizeof(v) / sizeof(v[0]); q++) BN_free(v[q]);
+  BN_CTX_free(ctx);
+  EC_GROUP_free(g);
+  return 0;
+}

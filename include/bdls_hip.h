@@ -272,6 +272,62 @@ int bh_bdls_preverify(int curve, const uint8_t *msgs, const uint64_t *msg_off,
                       size_t n_participants, uint32_t flags, bh_bdls_msg_result *results,
                       uint8_t *sp_reason, size_t sp_cap, size_t *sp_total);
 
+/* ---- Fabric block pre-verification ------------------------------------------
+ * Replaces the per-signature bccsp Verify calls of one block's validation
+ * (core/committer/txvalidator/v20/validator.go:180-265, validateTx :297-453)
+ * with ONE device batch: the serialized common.Block is decoded (protobuf-go
+ * wire rules), and for every transaction
+ *   - the creator signature over Envelope.payload by SignatureHeader.creator
+ *     (core/common/validation/msgvalidation.go:26-64, checked at :274), and
+ *   - for ENDORSER_TRANSACTIONs each endorsement over
+ *     proposal_response_payload || endorser by the endorser
+ *     (core/common/validation/statebased/validator_keylevel.go:246-260),
+ *     de-duplicated per identity exactly as common/policies/policy.go:363-395
+ *     SignatureSetToValidIdentities does (a later signature of an identity
+ *     is checked only while no earlier one of it verified)
+ * are verified with identity.Verify semantics (msp/identities.go:170-199:
+ * SHA-256, or SHA3-256 with BH_FAB_F_SHA3; Fabric's low-S rule). Identities
+ * (msp.SerializedIdentity: PEM X.509) resolve to P-256 keys through a
+ * long-lived cache; one this library cannot resolve is reported, never
+ * guessed. Checks that do not decide which signatures are verified
+ * (CheckTxID, the proposal hash, channel / ledger state, policies) stay with
+ * the unchanged validator, which consults the per-signature results.
+ *
+ * txs[i] (tx_cap >= number of transactions) and endorse[] (one byte per
+ * endorsement, tx i's at [endorse_first, +endorse_count)); *n_tx and
+ * *n_endorse are always set, and with too small buffers the call fails with
+ * BH_E_INVALID before any device work. endorse[j]: BH_R_* when verified,
+ * BH_FAB_E_DUPLICATE (skipped by the de-duplication), BH_FAB_E_BAD_IDENTITY,
+ * or BH_SP_NOT_VERIFIED. */
+#define BH_FAB_F_SHA3 1u      /* the MSPs' SignatureHashFamily is SHA3 */
+#define BH_FAB_F_KEEP_KEYS 2u /* keys used >= 2 times get kept tables (BH_F_KEEP_KEYS) */
+#define BH_FAB_F_DECODE_ONLY 4u /* decode, resolve and plan only: no device work, every
+                                   signature BH_SP_NOT_VERIFIED (host-side structure checks) */
+
+#define BH_FAB_OK 0                 /* every check below passed */
+#define BH_FAB_ENVELOPE 1           /* Envelope does not unmarshal: INVALID_OTHER_REASON (validator.go:310) */
+#define BH_FAB_PAYLOAD 2            /* Payload does not unmarshal: BAD_PAYLOAD (msgvalidation.go:257-261) */
+#define BH_FAB_HEADER 3             /* validateCommonHeader failed: BAD_COMMON_HEADER (:264-269) */
+#define BH_FAB_CREATOR_IDENTITY 4   /* creator not resolvable here (Go's DeserializeIdentity decides) */
+#define BH_FAB_CREATOR_SIGNATURE 5  /* creator.Verify failed (or nil signature): BAD_CREATOR_SIGNATURE */
+#define BH_FAB_TX 6                 /* endorser-transaction structure: INVALID_ENDORSER_TRANSACTION */
+#define BH_FAB_UNSUPPORTED 7        /* CONFIG_UPDATE envelope: UNSUPPORTED_TX_PAYLOAD */
+#define BH_FAB_E_DUPLICATE 253
+#define BH_FAB_E_BAD_IDENTITY 254
+
+typedef struct bh_fab_tx {
+  int32_t status;           /* BH_FAB_*: the first failing check in the validator's order */
+  int32_t type;             /* ChannelHeader.type (0 if the header did not decode) */
+  uint32_t creator;         /* BH_R_* of the creator signature, or BH_SP_NOT_VERIFIED */
+  uint32_t endorse_first;   /* this transaction's endorsements in endorse[] */
+  uint32_t endorse_count;
+  uint32_t valid_endorsers; /* |SignatureSetToValidIdentities(endorsement set)| */
+} bh_fab_tx;
+
+int bh_fabric_block_preverify(const uint8_t *block, size_t len, uint32_t flags, bh_fab_tx *txs,
+                              size_t tx_cap, size_t *n_tx, uint8_t *endorse, size_t endorse_cap,
+                              size_t *n_endorse);
+
 /* ---- device buffers on an initialised device (callers that keep batches
  * resident in HBM, e.g. bench.py; the library owns the HIP runtime so callers
  * never mix runtimes). Copies are synchronous on the device's stream. ---- */

@@ -1,0 +1,188 @@
+"""Fabric block pre-verification (bh_fabric_block_preverify) against the CPU
+oracle (oracle/fabric_ref.py: the reference's sequential validateTx /
+ValidateTransaction / SignatureSetToValidIdentities flow and protobuf-go wire
+rules, restated) and the generator's by-construction expectations.
+
+CPU (no device work): the oracle against the generator on every corruption
+class; the C++ decode / identity resolution (BH_FAB_F_DECODE_ONLY) against the
+oracle's, on the generated blocks and on thousands of mutated envelopes.
+GPU: the full pre-verification, bit-exact per transaction and per
+endorsement, on config 3's block and on every corruption class.
+"""
+import hashlib
+import random
+
+import pytest
+
+from bdls_amd import fabric
+from bdls_amd.workload import fabric as F
+from oracle import ecdsa_ref as O
+from oracle import fabric_ref as R
+
+
+def _py_verify(x, y, msg, sig):
+    return O.identity_verify(O.P256, x, y, msg, sig)[1]
+
+
+def _orc_verify(x, y, msg, sig):
+    from oracle import orc
+    return orc.csp_verify(x.to_bytes(32, "big") + y.to_bytes(32, "big"), sig,
+                          hashlib.sha256(msg).digest())
+
+
+def _want(fb, i):
+    return (fb.tx_status[i], fb.tx_creator[i], fb.tx_endorse[i], fb.tx_valid_identities[i])
+
+
+def _got(t):
+    return (t.status, t.creator, t.endorse, t.valid_endorsers)
+
+
+@pytest.fixture(scope="module")
+def classes_block():
+    return F.generate_fabric_block(ntx=2 * len(F.CORRUPTIONS), corrupt_den=0,
+                                   classes=F.CORRUPTIONS, seed=7)
+
+
+def test_oracle_matches_construction(classes_block):
+    fb = classes_block
+    out = R.validate_block(fb.block, _py_verify)
+    assert [_got(o) for o in out] == [_want(fb, i) for i in range(fb.ntx)]
+
+
+def _decode_pair(block):
+    py = R.validate_block(block, None, decode_only=True)
+    cc = fabric.block_preverify(block, decode_only=True)
+    return [_got(o) for o in py], [_got(o) for o in cc]
+
+
+def test_decode_only_matches_oracle(classes_block):
+    py, cc = _decode_pair(classes_block.block)
+    assert py == cc
+
+
+def _block_of(envs):
+    data = b"".join(F.pb_bytes(1, e) for e in envs)
+    return F.pb_bytes(2, data)
+
+
+def _envelopes(block):
+    blk = R.unmarshal(block, R.BLOCK_SPEC)
+    return blk["data"]["data"]
+
+
+def _mutate(rng, b: bytes) -> bytes:
+    b = bytearray(b)
+    for _ in range(rng.randrange(1, 4)):
+        op = rng.randrange(6)
+        if op == 0 and b:
+            b[rng.randrange(len(b))] = rng.randrange(256)
+        elif op == 1 and b:
+            i = rng.randrange(len(b))
+            del b[i:i + rng.randrange(1, 6)]
+        elif op == 2:
+            b.insert(rng.randrange(len(b) + 1), rng.randrange(256))
+        elif op == 3 and b:  # truncate
+            b = b[:rng.randrange(len(b))]
+        elif op == 4 and b:  # flip a varint continuation bit
+            b[rng.randrange(len(b))] ^= 0x80
+        else:  # a field with a rare wire type / number
+            tag = rng.choice([0x0b, 0x0c, 0x0e, 0x0f, 0x14, 0x1a, 0x08, 0xf8, 0x80])
+            b[rng.randrange(len(b) + 1):0] = bytes([tag, rng.randrange(256)])
+    return bytes(b)
+
+
+def _nested_mutation(rng, env: bytes) -> bytes:
+    """Mutate one nested message (payload / header / channel header /
+    signature header / transaction / endorsement) and re-encode outward."""
+    e = R.unmarshal(env, R.ENVELOPE_SPEC)
+    pl = R.unmarshal(e["payload"], R.PAYLOAD_SPEC)
+    which = rng.randrange(6)
+    hdr = pl["header"]
+    ch, sh = hdr["channel_header"], hdr["signature_header"]
+    data = pl["data"]
+    if which == 0:
+        ch = _mutate(rng, ch)
+    elif which == 1:
+        sh = _mutate(rng, sh)
+    elif which == 2:
+        data = _mutate(rng, data)
+    elif which == 3:
+        tx = R.unmarshal(data, R.TRANSACTION_SPEC)
+        act = tx["actions"][0]
+        cap = R.unmarshal(act["payload"], R.CC_ACTION_PAYLOAD_SPEC)
+        ea = cap["action"]
+        ends = ea["endorsements"]
+        k = rng.randrange(len(ends))
+        enc = [F.pb_bytes(1, x["endorser"]) + F.pb_bytes(2, x["signature"]) for x in ends]
+        enc[k] = _mutate(rng, enc[k]) if rng.random() < 0.5 else \
+            F.pb_bytes(1, _mutate(rng, ends[k]["endorser"])) + F.pb_bytes(2, ends[k]["signature"])
+        cea = F.pb_bytes(1, ea["proposal_response_payload"]) + b"".join(F.pb_bytes(2, x) for x in enc)
+        capb = F.pb_bytes(1, cap["chaincode_proposal_payload"]) + F.pb_bytes(2, cea)
+        data = F.pb_bytes(1, F.pb_bytes(1, act["header"]) + F.pb_bytes(2, capb))
+    elif which == 4:
+        hdr_b = _mutate(rng, F.pb_bytes(1, ch) + F.pb_bytes(2, sh))
+        return F.pb_bytes(1, F.pb_bytes(1, hdr_b) + F.pb_bytes(2, data)) + F.pb_bytes(2, e["signature"])
+    else:
+        return _mutate(rng, env)
+    payload = F.pb_bytes(1, F.pb_bytes(1, ch) + F.pb_bytes(2, sh)) + F.pb_bytes(2, data)
+    return F.pb_bytes(1, payload) + F.pb_bytes(2, e["signature"])
+
+
+def test_decode_fuzz_matches_oracle(classes_block):
+    rng = random.Random(11)
+    envs = _envelopes(classes_block.block)
+    base = [envs[0], envs[3], envs[4]]  # a valid tx and two endorsement variants
+    for it in range(3000):
+        env = _nested_mutation(rng, rng.choice(base))
+        block = _block_of([env])
+        py, cc = _decode_pair(block)
+        assert py == cc, (it, env.hex())
+
+
+def test_identity_pem_variants():
+    """PEM framing cases of Go encoding/pem Decode as the MSP meets them."""
+    fb = F.generate_fabric_block(ntx=1, corrupt_den=0, seed=9)
+    env = _envelopes(fb.block)[0]
+    e = R.unmarshal(env, R.ENVELOPE_SPEC)
+    pl = R.unmarshal(e["payload"], R.PAYLOAD_SPEC)
+    sh = R.unmarshal(pl["header"]["signature_header"], R.SIGNATURE_HEADER_SPEC)
+    si = R.unmarshal(sh["creator"], R.SERIALIZED_IDENTITY_SPEC)
+    p = si["id_bytes"]
+    body = p.split(b"\n", 1)[1].rsplit(b"-----END", 1)[0]
+    variants = [p, b"junk\n" + p, p.replace(b"\n", b"\r\n"), p + b"trailing",
+                b"-----BEGIN CERTIFICATE-----\nX: y\n\n" + body + b"-----END CERTIFICATE-----\n",
+                p.replace(b"-----END CERTIFICATE-----", b"-----END CERT-----"),
+                p.replace(b"\n-----END", b"  \t\n-----END"), p[:-1], p.replace(b"=", b""),
+                b"-----BEGIN CERTIFICATE-----\n" + body.replace(b"\n", b" \n") +
+                b"-----END CERTIFICATE-----   \n"]
+    for v in variants:
+        ser = F.pb_bytes(1, si["mspid"]) + F.pb_bytes(2, v)
+        sh2 = F.pb_bytes(1, ser) + F.pb_bytes(2, sh["nonce"])
+        payload = F.pb_bytes(1, F.pb_bytes(1, pl["header"]["channel_header"]) + F.pb_bytes(2, sh2)) \
+            + F.pb_bytes(2, pl["data"])
+        block = _block_of([F.pb_bytes(1, payload) + F.pb_bytes(2, e["signature"])])
+        py, cc = _decode_pair(block)
+        assert py == cc, v
+
+
+@pytest.mark.gpu
+def test_gpu_every_class(classes_block):
+    fb = classes_block
+    got = fabric.block_preverify(fb.block)
+    assert [_got(t) for t in got] == [_want(fb, i) for i in range(fb.ntx)]
+
+
+@pytest.mark.gpu
+def test_gpu_config3_block():
+    """BASELINE config 3's block: 500 txs x (creator + 3 endorsements), 1/100
+    corrupted; bit-exact against the construction and the oracle (OpenSSL
+    verify), then again with the endorser keys kept in the device registry."""
+    fb = F.generate_fabric_block(seed=3)
+    assert fb.ntx == 500
+    want = [_want(fb, i) for i in range(fb.ntx)]
+    oracle = [_got(o) for o in R.validate_block(fb.block, _orc_verify)]
+    assert oracle == want
+    for keep in (False, True, True):
+        got = fabric.block_preverify(fb.block, keep_keys=keep)
+        assert [_got(t) for t in got] == want
