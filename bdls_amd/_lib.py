@@ -29,7 +29,7 @@ EXPORTS = (
     "bh_sync", "bh_verify_bdls", "bh_verify_bdls_dev", "bh_keys_reserve", "bh_keys_register",
     "bh_keys_clear", "bh_keys_count", "bh_timing_begin", "bh_timing_end", "bh_bdls_preverify",
     "bh_verify_submit", "bh_verify_wait", "bh_host_alloc", "bh_host_free", "bh_csp_stats",
-    "bh_fabric_block_preverify",
+    "bh_fabric_block_preverify", "bh_verify_x509",
 )
 KEY_FULL = 255  # bh_keys_register status: registry full
 
@@ -127,6 +127,8 @@ def lib() -> ctypes.CDLL:
         L.bh_fabric_block_preverify.argtypes = [vp, sz, u32, vp, sz, ctypes.POINTER(sz), vp, sz,
                                                 ctypes.POINTER(sz)]
         L.bh_fabric_block_preverify.restype = i32
+        L.bh_verify_x509.argtypes = [vp, vp, vp, vp, sz, vp, vp]
+        L.bh_verify_x509.restype = i32
         L.bh_csp_stats.argtypes = [vp]
         L.bh_csp_stats.restype = i32
         L.bh_parse_der_sig.argtypes = [vp, sz, vp, vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]

@@ -777,7 +777,160 @@ struct Batch {
   }
 };
 
+
+// ---------------------------------------------------------------- x509
+// golang.org/x/crypto/cryptobyte (as used by Go 1.21 crypto/ecdsa
+// parseSignature for VerifyASN1): readASN1 with DER length rules, tag exact.
+bool cb_read(const uint8_t* b, size_t n, size_t* off, uint8_t want_tag, const uint8_t** out,
+             size_t* out_n) {
+  if (n - *off < 2) return false;
+  const uint8_t tag = b[*off], lb = b[*off + 1];
+  if ((tag & 0x1f) == 0x1f) return false;  // high-tag-number form unsupported
+  size_t hl, len;
+  if (!(lb & 0x80)) {
+    hl = 2;
+    len = lb;
+  } else {
+    const size_t ll = lb & 0x7f;
+    if (ll == 0 || ll > 4 || n - *off < 2 + ll) return false;
+    uint32_t l32 = 0;
+    for (size_t i = 0; i < ll; i++) l32 = l32 << 8 | b[*off + 2 + i];
+    if (l32 < 128) return false;                    // should be short form
+    if ((l32 >> ((ll - 1) * 8)) == 0) return false; // leading zero octet
+    hl = 2 + ll;
+    len = l32;
+  }
+  if (len > n - *off - hl) return false;
+  if (tag != want_tag) return false;
+  *out = b + *off + hl;
+  *out_n = len;
+  *off += hl + len;
+  return true;
+}
+
+// cryptobyte readASN1Bytes: minimal, non-negative INTEGER, leading zeros stripped
+bool cb_uint(const uint8_t* b, size_t n, size_t* off, std::vector<uint8_t>* v) {
+  const uint8_t* p;
+  size_t l;
+  if (!cb_read(b, n, off, 0x02, &p, &l)) return false;
+  if (l == 0) return false;
+  if (l > 1 && ((p[0] == 0 && !(p[1] & 0x80)) || (p[0] == 0xff && (p[1] & 0x80)))) return false;
+  if (p[0] & 0x80) return false;
+  while (l > 1 && p[0] == 0) {
+    p++;
+    l--;
+  }
+  v->assign(p, p + l);
+  return true;
+}
+
+// crypto/ecdsa parseSignature: SEQUENCE { r INTEGER, s INTEGER }, nothing else
+bool strict_sig(const uint8_t* b, size_t n, std::vector<uint8_t>* r, std::vector<uint8_t>* s) {
+  size_t off = 0, io = 0;
+  const uint8_t* in;
+  size_t il;
+  if (!cb_read(b, n, &off, 0x30, &in, &il) || off != n) return false;
+  return cb_uint(in, il, &io, r) && cb_uint(in, il, &io, s) && io == il;
+}
+
+void der_uint(std::vector<uint8_t>* o, const std::vector<uint8_t>& v) {
+  const bool pad = v[0] & 0x80;
+  const size_t len = v.size() + (pad ? 1 : 0);
+  o->push_back(0x02);
+  if (len < 0x80) {
+    o->push_back((uint8_t)len);
+  } else {
+    o->push_back(0x81);  // <= 255: the signature's own length bounds it
+    o->push_back((uint8_t)len);
+  }
+  if (pad) o->push_back(0);
+  o->insert(o->end(), v.begin(), v.end());
+}
+
+// canonical DER of (r, s): what the device's Go-asn1 parser reads back exactly
+void canon_sig(std::vector<uint8_t>* o, const std::vector<uint8_t>& r,
+               const std::vector<uint8_t>& s) {
+  std::vector<uint8_t> body;
+  der_uint(&body, r);
+  der_uint(&body, s);
+  o->push_back(0x30);
+  if (body.size() < 0x80) {
+    o->push_back((uint8_t)body.size());
+  } else {
+    o->push_back(0x81);
+    o->push_back((uint8_t)body.size());
+  }
+  o->insert(o->end(), body.begin(), body.end());
+}
+
 }  // namespace
+
+// Go crypto/x509 Certificate.CheckSignatureFrom for ECDSA (checkSignature:
+// hash the raw TBSCertificate, ecdsa.VerifyASN1 = cryptobyte-strict DER, no
+// low-S rule), the check msp/mspimpl.go:717-722 (cert.Verify chain building)
+// and msp/cert.go:76-116 make per certificate of an identity's chain.
+extern "C" int bh_verify_x509(const uint8_t* certs, const uint64_t* cert_off,
+                              const uint32_t* cert_len, const uint8_t* issuer_pub, size_t n,
+                              uint8_t* bitmap, uint8_t* reason) {
+  if (n && (!certs || !cert_off || !cert_len || !issuer_pub || !bitmap || !reason))
+    return bh::host_fail(BH_E_INVALID, "null argument");
+  if (n > 0xffffffffull) return bh::host_fail(BH_E_INVALID, "batch too large");
+  memset(bitmap, 0, (n + 7) / 8);
+  Batch b;
+  std::vector<uint8_t> sigs;
+  std::vector<size_t> which;
+  std::vector<uint64_t> tbs_off;
+  std::vector<uint32_t> tbs_len, sig_len;
+  std::vector<uint64_t> sig_off;
+  for (size_t i = 0; i < n; i++) {
+    reason[i] = BH_R_UNSUPPORTED;
+    const uint8_t* d = certs + cert_off[i];
+    Cert c;
+    if (!parse_cert(d, cert_len[i], &c)) continue;
+    // the TBS signature field must name the same algorithm as the outer one
+    size_t t = 0;
+    Tlv f;
+    if (!tlv(c.tbs.p, c.tbs.n, &t, &f)) continue;
+    if (f.tag == 0xa0 && !tlv(c.tbs.p, c.tbs.n, &t, &f)) continue;
+    Tlv inner;
+    if (!tlv(c.tbs.p, c.tbs.n, &t, &inner) || inner.tag != 0x30) continue;
+    size_t io = 0;
+    Tlv inner_oid;
+    if (!tlv(inner.p, inner.n, &io, &inner_oid) || inner_oid.raw_n != c.sig_alg_oid.raw_n ||
+        memcmp(inner_oid.raw, c.sig_alg_oid.raw, inner_oid.raw_n))
+      continue;
+    if (c.sig_alg_oid.n != sizeof(kOidEcdsaSha256) ||
+        memcmp(c.sig_alg_oid.p, kOidEcdsaSha256, sizeof(kOidEcdsaSha256)))
+      continue;  // SHA-384 / SHA-512 / RSA: Go's x509 path
+    std::vector<uint8_t> r, s;
+    if (!strict_sig(c.sig.p, c.sig.n, &r, &s)) {
+      reason[i] = BH_R_DER;  // parseSignature fails: VerifyASN1 false
+      continue;
+    }
+    sig_off.push_back(sigs.size());
+    canon_sig(&sigs, r, s);
+    sig_len.push_back((uint32_t)(sigs.size() - sig_off.back()));
+    tbs_off.push_back(cert_off[i] + (uint64_t)(c.tbs.raw - d));
+    tbs_len.push_back((uint32_t)c.tbs.raw_n);
+    which.push_back(i);
+  }
+  const size_t m = which.size();
+  if (!m) return BH_OK;
+  std::vector<uint8_t> pub(m * 64), bm((m + 7) / 8), rs(m);
+  for (size_t k = 0; k < m; k++) memcpy(&pub[64 * k], issuer_pub + 64 * which[k], 64);
+  sigs.push_back(0);
+  // messages: the TBS bytes inside the caller's certificate buffer
+  bh_batch bb{pub.data(), sigs.data(), sig_off.data(), sig_len.data(), certs, tbs_off.data(),
+              tbs_len.data()};
+  int rc = bh_verify(BH_CURVE_P256, &bb, m, BH_F_NO_LOW_S | BH_F_HASH_SHA256, bm.data(), rs.data());
+  if (rc) return rc;
+  for (size_t k = 0; k < m; k++) {
+    const size_t i = which[k];
+    reason[i] = rs[k];
+    if (rs[k] == BH_R_OK) bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
+  }
+  return BH_OK;
+}
 
 extern "C" int bh_fabric_block_preverify(const uint8_t* block, size_t len, uint32_t flags,
                                          bh_fab_tx* txs, size_t tx_cap, size_t* n_tx,

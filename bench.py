@@ -259,8 +259,17 @@ def bench_latency(a, rank, world, local):
     warm = measure("warm")
     _lib.check(L.bh_keys_clear(-1, curve))
     wire = measure_wire(a, L, curve, rank) if a.config == 4 else None
+    block = measure_block(a, L, rank) if a.config == 3 else None
     _lib.check(L.bh_keys_clear(-1, curve))
-    if wire is not None:
+    if block is not None:
+        # config 3's value: the whole block through bh_fabric_block_preverify
+        # (decode + identities + every creator / endorsement signature in one
+        # device batch), endorser / creator keys kept in the registry
+        p50 = dist.max_over_ranks(block["warm"]["p50"], world)
+        value_is = ("bh_fabric_block_preverify on the serialized common.Block (500 endorser "
+                    "txs, creator + 3 endorsements each): decode + identity resolution + one "
+                    "device batch, keys kept in the registry (warm) p50, host-to-host")
+    elif wire is not None:
         # config 4's value: the A16 entry (bh_bdls_preverify) that
         # inputConsensusMessage calls, participants' keys registered
         p50 = dist.max_over_ranks(wire["warm"]["p50"], world)
@@ -285,6 +294,10 @@ def bench_latency(a, rank, world, local):
         "latency_ms": {"warm": warm, "cold": cold,
                        "register_keys_ms": round(reg_ms, 3)},
     }
+    if block is not None:
+        out["latency_ms"]["block_preverify"] = block
+        out["parity"] = parity_ok = dist.all_true(parity_ok and block["parity"], world)
+        out["config"]["block_bytes"] = block["block_bytes"]
     if wire is not None:
         out["latency_ms"]["wire_preverify"] = wire
         out["parity"] = parity_ok = dist.all_true(parity_ok and wire["parity"], world)
@@ -318,6 +331,59 @@ def bench_latency(a, rank, world, local):
         print(json.dumps(out), flush=True)
     dist.finalize(world)
     return 0 if parity_ok else 3
+
+
+def measure_block(a, L, rank):
+    """Config 3 through bh_fabric_block_preverify: one serialized block
+    (bdls_amd/workload/fabric.py: 500 endorser txs, X.509 identities of 4 peers
+    and 50 clients, 1/100 corrupted). Cold = no key known to the device (every
+    signature on the ladder); warm = BH_FAB_F_KEEP_KEYS after a first block
+    (the peer's long-lived identities keep device tables)."""
+    from bdls_amd import _lib
+    from bdls_amd.workload import fabric as F
+    fb = F.generate_fabric_block(seed=a.seed + 1000 * rank)
+    buf = np.frombuffer(fb.block + b"\0", np.uint8)
+    ntx, nend = ctypes.c_size_t(), ctypes.c_size_t()
+    txs = (_lib.BhFabTx * fb.ntx)()
+    cap = sum(len(e) for e in fb.tx_endorse) + 64 * fb.ntx
+    end = np.zeros(cap, np.uint8)
+    want = [(fb.tx_status[i], fb.tx_creator[i], fb.tx_endorse[i], fb.tx_valid_identities[i])
+            for i in range(fb.ntx)]
+
+    def call(flags):
+        return L.bh_fabric_block_preverify(buf.ctypes.data, len(fb.block), flags, txs, fb.ntx,
+                                           ctypes.byref(ntx), end.ctypes.data, cap,
+                                           ctypes.byref(nend))
+
+    def check():
+        got = [(t.status, t.creator,
+                [int(x) for x in end[t.endorse_first:t.endorse_first + t.endorse_count]],
+                t.valid_endorsers) for t in txs[:ntx.value]]
+        return got == want
+
+    def run(flags, clear):
+        for _ in range(max(1, a.warmup)):
+            if clear:
+                _lib.check(L.bh_keys_clear(-1, 0))
+            _lib.check(call(flags))
+        ms = []
+        for _ in range(a.steps):
+            if clear:
+                _lib.check(L.bh_keys_clear(-1, 0))
+            t = time.perf_counter()
+            _lib.check(call(flags))
+            ms.append((time.perf_counter() - t) * 1e3)
+        return {"p50": round(percentile(ms, 50), 4), "p99": round(percentile(ms, 99), 4),
+                "parity": check()}
+
+    cold = run(0, True)
+    t = time.perf_counter()
+    _lib.check(call(_lib.BH_FAB_F_DECODE_ONLY))
+    decode_ms = (time.perf_counter() - t) * 1e3
+    warm = run(_lib.BH_FAB_F_KEEP_KEYS, False)
+    return {"warm": warm, "cold": cold, "decode_only_ms": round(decode_ms, 4),
+            "transactions": fb.ntx, "signatures": fb.n_signatures,
+            "block_bytes": len(fb.block), "parity": bool(warm["parity"] and cold["parity"])}
 
 
 def measure_wire(a, L, curve, rank):

@@ -51,6 +51,8 @@ extern "C" {
 #define BH_R_R_RANGE 8      /* ecdsa.Verify: r >= n                                     -> false */
 #define BH_R_MATH 9         /* ecdsa.Verify: x(u1 G + u2 Q) mod n != r, or infinity    -> false */
 #define BH_R_S_RANGE 10     /* ecdsa.Verify: s >= n (only with BH_F_NO_LOW_S)           -> false */
+#define BH_R_UNSUPPORTED 11 /* bh_verify_x509: not an ecdsa-with-SHA256 P-256 certificate
+                               signature this engine checks (the caller uses Go's x509)   */
 
 /* ---- flags ---- */
 #define BH_F_HASH_SHA256 1u /* msg[i] is a message; digest = SHA-256(msg[i]) (identity.Verify) */
@@ -327,6 +329,20 @@ typedef struct bh_fab_tx {
 int bh_fabric_block_preverify(const uint8_t *block, size_t len, uint32_t flags, bh_fab_tx *txs,
                               size_t tx_cap, size_t *n_tx, uint8_t *endorse, size_t endorse_cap,
                               size_t *n_endorse);
+
+/* ---- X.509 certificate signatures ---------------------------------------------
+ * Certificate i's signature against issuer key i (X || Y): Go crypto/x509
+ * Certificate.CheckSignatureFrom for an ECDSA issuer (checkSignature: SHA-256
+ * of the raw TBSCertificate, then ecdsa.VerifyASN1 -- cryptobyte-strict DER,
+ * r, s in [1, n-1], NO low-S rule), the per-link check of the MSP's chain
+ * validation (msp/mspimpl.go:717-722 cert.Verify, msp/cert.go:76-116). The
+ * TBS bytes are hashed on the device straight out of the caller's buffer.
+ * reason: BH_R_OK, BH_R_DER (signature not strict DER), BH_R_R_NONPOS /
+ * BH_R_S_NONPOS (zero), BH_R_BAD_KEY, BH_R_R_RANGE / BH_R_S_RANGE, BH_R_MATH,
+ * or BH_R_UNSUPPORTED (not ecdsa-with-SHA256, inner/outer algorithm mismatch,
+ * or not a certificate this parser walks). */
+int bh_verify_x509(const uint8_t *certs, const uint64_t *cert_off, const uint32_t *cert_len,
+                   const uint8_t *issuer_pub, size_t n, uint8_t *bitmap, uint8_t *reason);
 
 /* ---- device buffers on an initialised device (callers that keep batches
  * resident in HBM, e.g. bench.py; the library owns the HIP runtime so callers

@@ -16,6 +16,7 @@ for s in $STEPS; do
     ubench) timeout -k 10 120 bdls_amd/lib/ubench > gpurun_out/ubench.json 2> gpurun_out/ubench.err; rc=$?; cat gpurun_out/ubench.json; ok_or_stop $rc ubench ;;
     tests)  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${TEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -5 gpurun_out/pytest_gpu.log; ok_or_stop $rc tests ;;
     smoke)  timeout -k 10 300 python -u __graft_entry__.py > gpurun_out/smoke.log 2>&1; rc=$?; tail -2 gpurun_out/smoke.log; ok_or_stop $rc smoke ;;
+    lat)    for c in 3 4; do timeout -k 10 300 python -u bench.py --config $c --steps ${LAT_STEPS:-30} --warmup 3 > gpurun_out/lat$c.json 2> gpurun_out/lat$c.err; rc=$?; cat gpurun_out/lat$c.json; tail -3 gpurun_out/lat$c.err; case $rc in 0|3) ;; *) echo "STOP after lat$c (exit $rc)"; exit $rc ;; esac; done ;;
     hostinfo) (nproc; python -c "import os; print(os.cpu_count(), len(os.sched_getaffinity(0)))"; cat /sys/fs/cgroup/cpu.max 2>/dev/null; lscpu | head -20) > gpurun_out/hostinfo.txt 2>&1; cat gpurun_out/hostinfo.txt ;;
     bench)  timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err; ok_or_stop $rc bench ;;
     prof)   export TMPDIR=/tmp; timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0 > gpurun_out/prof.log 2>&1; rc=$?; tail -3 gpurun_out/prof.log; ok_or_stop $rc prof ;;
