@@ -29,7 +29,8 @@ EXPORTS = (
     "bh_sync", "bh_verify_bdls", "bh_verify_bdls_dev", "bh_keys_reserve", "bh_keys_register",
     "bh_keys_clear", "bh_keys_count", "bh_timing_begin", "bh_timing_end", "bh_bdls_preverify",
     "bh_verify_submit", "bh_verify_wait", "bh_host_alloc", "bh_host_free", "bh_csp_stats",
-    "bh_fabric_block_preverify", "bh_verify_x509",
+    "bh_fabric_block_preverify", "bh_verify_x509", "bh_signature_sets_verify",
+    "bh_envelopes_preverify", "bh_block_signatures_preverify",
 )
 KEY_FULL = 255  # bh_keys_register status: registry full
 
@@ -75,6 +76,17 @@ class BhFabTx(ctypes.Structure):
     _fields_ = [("status", ctypes.c_int32), ("type", ctypes.c_int32),
                 ("creator", ctypes.c_uint32), ("endorse_first", ctypes.c_uint32),
                 ("endorse_count", ctypes.c_uint32), ("valid_endorsers", ctypes.c_uint32)]
+
+
+class BhSdBatch(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in
+                ("identity", "identity_off", "identity_len", "data", "data_off", "data_len",
+                 "sig", "sig_off", "sig_len")]
+
+
+class BhBlocksigResult(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("sig_first", ctypes.c_uint32),
+                ("sig_count", ctypes.c_uint32), ("valid_identities", ctypes.c_uint32)]
 
 
 BH_FAB_F_SHA3 = 1
@@ -127,6 +139,13 @@ def lib() -> ctypes.CDLL:
         L.bh_fabric_block_preverify.argtypes = [vp, sz, u32, vp, sz, ctypes.POINTER(sz), vp, sz,
                                                 ctypes.POINTER(sz)]
         L.bh_fabric_block_preverify.restype = i32
+        L.bh_signature_sets_verify.argtypes = [ctypes.POINTER(BhSdBatch), sz, vp, sz, u32, vp, vp]
+        L.bh_signature_sets_verify.restype = i32
+        L.bh_envelopes_preverify.argtypes = [vp, vp, vp, sz, u32, vp, vp]
+        L.bh_envelopes_preverify.restype = i32
+        L.bh_block_signatures_preverify.argtypes = [vp, vp, vp, sz, u32, vp, vp, sz,
+                                                    ctypes.POINTER(sz)]
+        L.bh_block_signatures_preverify.restype = i32
         L.bh_verify_x509.argtypes = [vp, vp, vp, vp, sz, vp, vp]
         L.bh_verify_x509.restype = i32
         L.bh_csp_stats.argtypes = [vp]

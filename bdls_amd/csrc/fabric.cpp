@@ -649,13 +649,121 @@ IdentCache& ident_cache() {
   return *c;
 }
 
-// ---------------------------------------------------------------- the block
-struct EndRec {
-  IdentP id;
-  Span endorser, sig, prp;
+// ---------------------------------------------------------------- signature sets
+// One SignedData (protoutil/signeddata.go:25-29): the signer's identity, the
+// signed bytes (up to three pieces, concatenated) and the signature.
+struct SdEntry {
+  IdentP id;  // resolved identity (id->ok false: DeserializeIdentity fails)
+  Span seg[3];
+  int nseg = 0;
+  Span sig;
   uint8_t out = BH_SP_NOT_VERIFIED;
 };
 
+// One device batch of signatures (messages hashed on the device).
+struct Batch {
+  std::vector<uint8_t> pub, sig, msg;
+  std::vector<uint64_t> sig_off, msg_off;
+  std::vector<uint32_t> sig_len, msg_len;
+  std::vector<uint8_t*> dst;  // where each record's reason goes
+  void add(const uint8_t pub64[64], Span s, const Span* m, int nm, uint8_t* out) {
+    pub.insert(pub.end(), pub64, pub64 + 64);
+    sig_off.push_back(sig.size());
+    sig_len.push_back((uint32_t)s.n);
+    if (s.n) sig.insert(sig.end(), s.p, s.p + s.n);
+    msg_off.push_back(msg.size());
+    size_t L = 0;
+    for (int k = 0; k < nm; k++) {
+      if (m[k].n) msg.insert(msg.end(), m[k].p, m[k].p + m[k].n);
+      L += m[k].n;
+    }
+    msg_len.push_back((uint32_t)L);
+    dst.push_back(out);
+  }
+  void add(SdEntry& e) { add(e.id->pub, e.sig, e.seg, e.nseg, &e.out); }
+  size_t size() const { return dst.size(); }
+  int run(uint32_t flags) {
+    const size_t n = size();
+    if (!n) return BH_OK;
+    std::vector<uint8_t> bitmap((n + 7) / 8), reason(n);
+    sig.push_back(0);
+    msg.push_back(0);
+    bh_batch b{pub.data(), sig.data(), sig_off.data(), sig_len.data(),
+               msg.data(), msg_off.data(), msg_len.data()};
+    int rc = bh_verify(BH_CURVE_P256, &b, n, flags, bitmap.data(), reason.data());
+    if (rc) return rc;
+    for (size_t i = 0; i < n; i++) *dst[i] = reason[i];
+    return BH_OK;
+  }
+};
+
+struct SetRange {
+  size_t first, count;
+};
+
+// common/policies/policy.go:363-395 SignatureSetToValidIdentities over each
+// set, batched: round 1 verifies the first entry of every identity of every
+// set (plus `extra`, e.g. creator signatures, in the same device batch);
+// the in-order replay then marks entries Go skips as duplicates (an identity
+// already validated earlier in the set) and, where an identity's earlier
+// signature failed, queues its next entry for another round (Go checks it).
+// Entries whose identity does not resolve are skipped, as Go skips them.
+int verify_sets(std::vector<SdEntry>& e, const std::vector<SetRange>& sets, uint32_t vflags,
+                bool decode_only, std::vector<uint32_t>* valid, Batch* extra) {
+  Batch b;
+  if (extra) b = std::move(*extra);
+  for (const SetRange& r : sets) {
+    std::vector<const std::string*> seen;
+    for (size_t i = r.first; i < r.first + r.count; i++) {
+      SdEntry& x = e[i];
+      if (!x.id || !x.id->ok) {
+        x.out = BH_FAB_E_BAD_IDENTITY;
+        continue;
+      }
+      bool dup = false;
+      for (const std::string* k : seen) dup |= (*k == x.id->key);
+      if (dup) continue;
+      seen.push_back(&x.id->key);
+      b.add(x);
+    }
+  }
+  if (!decode_only)
+    if (int rc = b.run(vflags)) return rc;
+  valid->assign(sets.size(), 0);
+  for (int round = 0; round < 256; round++) {
+    Batch more;
+    for (size_t k = 0; k < sets.size(); k++) {
+      const SetRange& r = sets[k];
+      std::vector<const std::string*> ok;
+      for (size_t i = r.first; i < r.first + r.count; i++) {
+        SdEntry& x = e[i];
+        if (!x.id || !x.id->ok) continue;
+        bool dup = false;
+        for (const std::string* key : ok) dup |= (*key == x.id->key);
+        if (dup) {
+          x.out = BH_FAB_E_DUPLICATE;
+          continue;
+        }
+        if (x.out == BH_SP_NOT_VERIFIED) {  // Go reaches it: verify next round
+          if (!decode_only) more.add(x);
+          break;  // later entries of this set depend on its result
+        }
+        if (x.out == BH_R_OK) ok.push_back(&x.id->key);
+      }
+      (*valid)[k] = (uint32_t)ok.size();
+    }
+    if (!more.size() || decode_only) break;
+    if (int rc = more.run(vflags)) return rc;
+  }
+  return BH_OK;
+}
+
+uint32_t verify_flags(uint32_t flags) {
+  return ((flags & BH_FAB_F_SHA3) ? BH_F_HASH_SHA3_256 : BH_F_HASH_SHA256) |
+         ((flags & BH_FAB_F_KEEP_KEYS) ? BH_F_KEEP_KEYS : 0u);
+}
+
+// ---------------------------------------------------------------- the block
 struct TxRec {
   int32_t status = BH_FAB_OK;
   int32_t type = 0;
@@ -663,15 +771,15 @@ struct TxRec {
   IdentP creator;
   Span payload, signature;
   uint8_t creator_out = BH_SP_NOT_VERIFIED;
-  std::vector<EndRec> ends;
-  uint32_t valid_endorsers = 0;
+  size_t end_first = 0, end_count = 0;  // endorsements in the shared entry list
 };
 
 // Go's order of checks up to the signatures (validateTx, ValidateTransaction,
 // validateEndorserTransaction). Checks that do not gate which signatures are
 // verified (CheckTxID, the proposal hash, ledger / channel state) are left to
 // the unchanged validator.
-void decode_tx(Span env_bytes, TxRec* t) {
+void decode_tx(Span env_bytes, TxRec* t, std::vector<SdEntry>* ends) {
+  t->end_first = ends->size();
   Envelope env;
   if (!dec_envelope(env_bytes, &env)) {
     t->status = BH_FAB_ENVELOPE;  // GetEnvelopeFromBlock: INVALID_OTHER_REASON
@@ -728,55 +836,19 @@ void decode_tx(Span env_bytes, TxRec* t) {
     if (t->status == BH_FAB_OK) t->status = tx_status;
     return;
   }
-  for (const Endorsement& e : ap.action.endorsements) {
-    EndRec r;
-    r.endorser = e.endorser;
-    r.sig = e.signature;
-    r.prp = ap.action.prp;
-    // SignatureSetToValidIdentities: DeserializeIdentity failure -> skipped
-    r.id = ident_cache().get(e.endorser);
-    if (!r.id->ok) r.out = BH_FAB_E_BAD_IDENTITY;
-    t->ends.push_back(r);
+  for (const Endorsement& en : ap.action.endorsements) {
+    // SignedData{data: prp || endorser, identity: endorser, signature}
+    // (validator_keylevel.go:246-260)
+    SdEntry x;
+    x.id = ident_cache().get(en.endorser);
+    x.seg[0] = ap.action.prp;
+    x.seg[1] = en.endorser;
+    x.nseg = 2;
+    x.sig = en.signature;
+    ends->push_back(x);
   }
+  t->end_count = ends->size() - t->end_first;
 }
-
-// One device batch of signatures: creator (payload) and endorsement
-// (prp || endorser) records, messages hashed on the device.
-struct Batch {
-  std::vector<uint8_t> pub, sig, msg;
-  std::vector<uint64_t> sig_off, msg_off;
-  std::vector<uint32_t> sig_len, msg_len;
-  std::vector<uint8_t*> dst;  // where each record's reason goes
-  void add(const uint8_t pub64[64], Span s, const Span* m, int nm, uint8_t* out) {
-    pub.insert(pub.end(), pub64, pub64 + 64);
-    sig_off.push_back(sig.size());
-    sig_len.push_back((uint32_t)s.n);
-    if (s.n) sig.insert(sig.end(), s.p, s.p + s.n);
-    msg_off.push_back(msg.size());
-    size_t L = 0;
-    for (int k = 0; k < nm; k++) {
-      if (m[k].n) msg.insert(msg.end(), m[k].p, m[k].p + m[k].n);
-      L += m[k].n;
-    }
-    msg_len.push_back((uint32_t)L);
-    dst.push_back(out);
-  }
-  size_t size() const { return dst.size(); }
-  int run(uint32_t flags) {
-    const size_t n = size();
-    if (!n) return BH_OK;
-    std::vector<uint8_t> bitmap((n + 7) / 8), reason(n);
-    sig.push_back(0);
-    msg.push_back(0);
-    bh_batch b{pub.data(), sig.data(), sig_off.data(), sig_len.data(),
-               msg.data(), msg_off.data(), msg_len.data()};
-    int rc = bh_verify(BH_CURVE_P256, &b, n, flags, bitmap.data(), reason.data());
-    if (rc) return rc;
-    for (size_t i = 0; i < n; i++) *dst[i] = reason[i];
-    return BH_OK;
-  }
-};
-
 
 // ---------------------------------------------------------------- x509
 // golang.org/x/crypto/cryptobyte (as used by Go 1.21 crypto/ecdsa
@@ -876,7 +948,6 @@ extern "C" int bh_verify_x509(const uint8_t* certs, const uint64_t* cert_off,
     return bh::host_fail(BH_E_INVALID, "null argument");
   if (n > 0xffffffffull) return bh::host_fail(BH_E_INVALID, "batch too large");
   memset(bitmap, 0, (n + 7) / 8);
-  Batch b;
   std::vector<uint8_t> sigs;
   std::vector<size_t> which;
   std::vector<uint64_t> tbs_off;
@@ -885,23 +956,35 @@ extern "C" int bh_verify_x509(const uint8_t* certs, const uint64_t* cert_off,
   for (size_t i = 0; i < n; i++) {
     reason[i] = BH_R_UNSUPPORTED;
     const uint8_t* d = certs + cert_off[i];
-    Cert c;
-    if (!parse_cert(d, cert_len[i], &c)) continue;
-    // the TBS signature field must name the same algorithm as the outer one
+    const size_t dn = cert_len[i];
+    // Certificate ::= SEQUENCE { tbsCertificate, signatureAlgorithm,
+    // signatureValue BIT STRING }; the algorithm OIDs of the outer field and
+    // of the TBS signature field must match (x509.ParseCertificate)
+    size_t off = 0, o = 0;
+    Tlv cert, tbs, alg, sv, outer_oid;
+    if (!tlv(d, dn, &off, &cert) || cert.tag != 0x30 || off != dn) continue;
+    if (!tlv(cert.p, cert.n, &o, &tbs) || tbs.tag != 0x30) continue;
+    if (!tlv(cert.p, cert.n, &o, &alg) || alg.tag != 0x30) continue;
+    if (!tlv(cert.p, cert.n, &o, &sv) || sv.tag != 0x03 || sv.n < 1 || sv.p[0] != 0) continue;
+    size_t ao = 0;
+    if (!tlv(alg.p, alg.n, &ao, &outer_oid) || outer_oid.tag != 0x06) continue;
     size_t t = 0;
     Tlv f;
-    if (!tlv(c.tbs.p, c.tbs.n, &t, &f)) continue;
-    if (f.tag == 0xa0 && !tlv(c.tbs.p, c.tbs.n, &t, &f)) continue;
-    Tlv inner;
-    if (!tlv(c.tbs.p, c.tbs.n, &t, &inner) || inner.tag != 0x30) continue;
+    if (!tlv(tbs.p, tbs.n, &t, &f)) continue;
+    if (f.tag == 0xa0 && !tlv(tbs.p, tbs.n, &t, &f)) continue;
+    if (f.tag != 0x02) continue;
+    Tlv inner, inner_oid;
+    if (!tlv(tbs.p, tbs.n, &t, &inner) || inner.tag != 0x30) continue;
     size_t io = 0;
-    Tlv inner_oid;
-    if (!tlv(inner.p, inner.n, &io, &inner_oid) || inner_oid.raw_n != c.sig_alg_oid.raw_n ||
-        memcmp(inner_oid.raw, c.sig_alg_oid.raw, inner_oid.raw_n))
+    if (!tlv(inner.p, inner.n, &io, &inner_oid) || inner_oid.raw_n != outer_oid.raw_n ||
+        memcmp(inner_oid.raw, outer_oid.raw, inner_oid.raw_n))
       continue;
-    if (c.sig_alg_oid.n != sizeof(kOidEcdsaSha256) ||
-        memcmp(c.sig_alg_oid.p, kOidEcdsaSha256, sizeof(kOidEcdsaSha256)))
+    if (outer_oid.n != sizeof(kOidEcdsaSha256) ||
+        memcmp(outer_oid.p, kOidEcdsaSha256, sizeof(kOidEcdsaSha256)))
       continue;  // SHA-384 / SHA-512 / RSA: Go's x509 path
+    Cert c;
+    c.tbs = tbs;
+    c.sig = Tlv{0x03, sv.p + 1, sv.n - 1, sv.raw, sv.raw_n};
     std::vector<uint8_t> r, s;
     if (!strict_sig(c.sig.p, c.sig.n, &r, &s)) {
       reason[i] = BH_R_DER;  // parseSignature fails: VerifyASN1 false
@@ -944,67 +1027,25 @@ extern "C" int bh_fabric_block_preverify(const uint8_t* block, size_t len, uint3
   if (!dec_block(Span{block, len, true}, &data))
     return bh::host_fail(BH_E_INVALID, "block does not unmarshal (common.Block)");
   std::vector<TxRec> t(data.size());
-  size_t n_end = 0;
-  for (size_t i = 0; i < data.size(); i++) {
-    decode_tx(data[i], &t[i]);
-    n_end += t[i].ends.size();
-  }
+  std::vector<SdEntry> ends;
+  for (size_t i = 0; i < data.size(); i++) decode_tx(data[i], &t[i], &ends);
   *n_tx = t.size();
-  *n_endorse = n_end;
-  if ((t.size() && (!txs || tx_cap < t.size())) || (n_end && (!endorse || endorse_cap < n_end)))
+  *n_endorse = ends.size();
+  if ((t.size() && (!txs || tx_cap < t.size())) ||
+      (ends.size() && (!endorse || endorse_cap < ends.size())))
     return bh::host_fail(BH_E_INVALID, "result buffers too small (see *n_tx, *n_endorse)");
-  const uint32_t vflags = ((flags & BH_FAB_F_SHA3) ? BH_F_HASH_SHA3_256 : BH_F_HASH_SHA256) |
-                          ((flags & BH_FAB_F_KEEP_KEYS) ? BH_F_KEEP_KEYS : 0u);
-  // Round 1: every creator signature, and per transaction the FIRST
-  // endorsement of each identity (SignatureSetToValidIdentities verifies a
-  // later one of the same identity only if the earlier ones failed).
-  Batch b;
-  for (TxRec& x : t) {
-    if (x.creator_check) b.add(x.creator->pub, x.signature, &x.payload, 1, &x.creator_out);
-    std::vector<const std::string*> seen;
-    for (EndRec& e : x.ends) {
-      if (!e.id->ok) continue;
-      bool dup = false;
-      for (const std::string* k : seen) dup |= (*k == e.id->key);
-      if (dup) continue;
-      seen.push_back(&e.id->key);
-      const Span m[2] = {e.prp, e.endorser};  // data = prp || endorser (validator_keylevel.go:248-250)
-      b.add(e.id->pub, e.sig, m, 2, &e.out);
-    }
-  }
   const bool decode_only = (flags & BH_FAB_F_DECODE_ONLY) != 0;
-  if (decode_only) {
-    b = Batch();
-  } else if (int rc = b.run(vflags)) {
+  // one device batch: every creator signature and the first round of every
+  // transaction's endorsement set
+  Batch creators;
+  std::vector<SetRange> sets;
+  for (TxRec& x : t) {
+    if (x.creator_check) creators.add(x.creator->pub, x.signature, &x.payload, 1, &x.creator_out);
+    sets.push_back(SetRange{x.end_first, x.end_count});
+  }
+  std::vector<uint32_t> valid;
+  if (int rc = verify_sets(ends, sets, verify_flags(flags), decode_only, &valid, &creators))
     return rc;
-  }
-  // Replay the de-duplication in order; a failed first check of an identity
-  // makes Go verify its next occurrence: later rounds (rare) verify those.
-  for (int round = 0; round < 64; round++) {
-    Batch more;
-    for (TxRec& x : t) {
-      std::vector<const std::string*> valid;
-      for (EndRec& e : x.ends) {
-        if (!e.id->ok) continue;
-        bool dup = false;
-        for (const std::string* k : valid) dup |= (*k == e.id->key);
-        if (dup) {
-          e.out = BH_FAB_E_DUPLICATE;
-          continue;
-        }
-        if (e.out == BH_SP_NOT_VERIFIED) {  // reached: verify it in the next round
-          const Span m[2] = {e.prp, e.endorser};
-          more.add(e.id->pub, e.sig, m, 2, &e.out);
-          break;  // later entries of this tx depend on this result
-        }
-        if (e.out == BH_R_OK) valid.push_back(&e.id->key);
-      }
-      x.valid_endorsers = (uint32_t)valid.size();
-    }
-    if (!more.size() || decode_only) break;
-    if (int rc = more.run(vflags)) return rc;
-  }
-  size_t k = 0;
   for (size_t i = 0; i < t.size(); i++) {
     TxRec& x = t[i];
     // the creator check precedes the endorser-transaction checks
@@ -1014,10 +1055,256 @@ extern "C" int bh_fabric_block_preverify(const uint8_t* block, size_t len, uint3
     txs[i].status = x.status;
     txs[i].type = x.type;
     txs[i].creator = x.creator_out;
-    txs[i].endorse_first = (uint32_t)k;
-    txs[i].endorse_count = (uint32_t)x.ends.size();
-    txs[i].valid_endorsers = x.valid_endorsers;
-    for (const EndRec& e : x.ends) endorse[k++] = e.out;
+    txs[i].endorse_first = (uint32_t)x.end_first;
+    txs[i].endorse_count = (uint32_t)x.end_count;
+    txs[i].valid_endorsers = valid[i];
+    for (size_t k = 0; k < x.end_count; k++) endorse[x.end_first + k] = ends[x.end_first + k].out;
   }
+  return BH_OK;
+}
+
+// SignatureSetToValidIdentities over many signature sets in one device batch.
+extern "C" int bh_signature_sets_verify(const bh_sd_batch* b, size_t n, const uint32_t* set_first,
+                                        size_t n_sets, uint32_t flags, uint8_t* result,
+                                        uint32_t* valid_identities) {
+  if (!b || (n && (!b->identity || !b->identity_off || !b->identity_len || !b->data_off ||
+                   !b->data_len || !b->sig_off || !b->sig_len || !result)) ||
+      (n_sets && (!set_first || !valid_identities)))
+    return bh::host_fail(BH_E_INVALID, "null argument");
+  if (flags & ~(uint32_t)(BH_FAB_F_SHA3 | BH_FAB_F_KEEP_KEYS | BH_FAB_F_DECODE_ONLY))
+    return bh::host_fail(BH_E_INVALID, "unknown flag");
+  std::vector<SetRange> sets;
+  for (size_t k = 0; k < n_sets; k++) {
+    const size_t f = set_first[k], l = k + 1 < n_sets ? set_first[k + 1] : n;
+    if (f > l || l > n) return bh::host_fail(BH_E_INVALID, "set_first not ascending within n");
+    sets.push_back(SetRange{f, l - f});
+  }
+  std::vector<SdEntry> e(n);
+  for (size_t i = 0; i < n; i++) {
+    e[i].id = ident_cache().get(Span{b->identity + b->identity_off[i], b->identity_len[i], true});
+    e[i].seg[0] = Span{b->data ? b->data + b->data_off[i] : nullptr, b->data_len[i], true};
+    e[i].nseg = 1;
+    e[i].sig = Span{b->sig ? b->sig + b->sig_off[i] : nullptr, b->sig_len[i], true};
+  }
+  std::vector<uint32_t> valid;
+  if (int rc = verify_sets(e, sets, verify_flags(flags), (flags & BH_FAB_F_DECODE_ONLY) != 0,
+                           &valid, nullptr))
+    return rc;
+  for (size_t i = 0; i < n; i++) result[i] = e[i].out;
+  for (size_t k = 0; k < n_sets; k++) valid_identities[k] = valid[k];
+  return BH_OK;
+}
+
+// Orderer broadcast SigFilter (orderer/common/msgprocessor/sigfilter.go:50-80)
+// for n serialized envelopes: protoutil.EnvelopeAsSignedData
+// (protoutil/signeddata.go:60-86: payload, "Missing Header", signature
+// header) then the one-entry signature set of the policy evaluation.
+extern "C" int bh_envelopes_preverify(const uint8_t* envs, const uint64_t* env_off,
+                                      const uint32_t* env_len, size_t n, uint32_t flags,
+                                      int32_t* status, uint8_t* reason) {
+  if (n && (!envs || !env_off || !env_len || !status || !reason))
+    return bh::host_fail(BH_E_INVALID, "null argument");
+  if (flags & ~(uint32_t)(BH_FAB_F_SHA3 | BH_FAB_F_KEEP_KEYS | BH_FAB_F_DECODE_ONLY))
+    return bh::host_fail(BH_E_INVALID, "unknown flag");
+  std::vector<SdEntry> e(n);
+  std::vector<SetRange> sets;
+  for (size_t i = 0; i < n; i++) {
+    status[i] = BH_FAB_OK;
+    Envelope env;
+    Payload pl;
+    SignatureHeader sh;
+    if (!dec_envelope(Span{envs + env_off[i], env_len[i], true}, &env)) {
+      status[i] = BH_FAB_ENVELOPE;
+    } else if (!dec_payload(env.payload, &pl)) {
+      status[i] = BH_FAB_PAYLOAD;
+    } else if (!pl.has_header || !dec_signature_header(pl.header.signature_header, &sh)) {
+      status[i] = BH_FAB_HEADER;  // "Missing Header" / GetSignatureHeaderFromBytes failed
+    } else {
+      e[i].id = ident_cache().get(sh.creator);
+      e[i].seg[0] = env.payload;
+      e[i].nseg = 1;
+      e[i].sig = env.signature;
+      if (!e[i].id->ok) status[i] = BH_FAB_CREATOR_IDENTITY;
+      sets.push_back(SetRange{i, 1});
+    }
+  }
+  std::vector<uint32_t> valid;
+  if (int rc = verify_sets(e, sets, verify_flags(flags), (flags & BH_FAB_F_DECODE_ONLY) != 0,
+                           &valid, nullptr))
+    return rc;
+  for (size_t i = 0; i < n; i++) {
+    reason[i] = status[i] == BH_FAB_OK ? e[i].out : (uint8_t)BH_SP_NOT_VERIFIED;
+    if (status[i] == BH_FAB_OK && reason[i] != BH_R_OK && reason[i] != BH_SP_NOT_VERIFIED)
+      status[i] = BH_FAB_CREATOR_SIGNATURE;
+  }
+  return BH_OK;
+}
+
+namespace {
+
+// encoding/asn1 Marshal of protoutil's asn1Header{Number *big.Int,
+// PreviousHash, DataHash []byte} (protoutil/blockutils.go:42-62)
+void asn1_len(std::vector<uint8_t>* o, size_t n) {
+  if (n < 0x80) {
+    o->push_back((uint8_t)n);
+    return;
+  }
+  uint8_t b[8];
+  int k = 0;
+  while (n) {
+    b[k++] = (uint8_t)n;
+    n >>= 8;
+  }
+  o->push_back((uint8_t)(0x80 | k));
+  while (k) o->push_back(b[--k]);
+}
+
+std::vector<uint8_t> block_header_bytes(uint64_t number, Span prev, Span data_hash) {
+  std::vector<uint8_t> num;  // big.Int two's complement, minimal
+  for (int i = 7; i >= 0; i--) {
+    const uint8_t v = (uint8_t)(number >> (8 * i));
+    if (num.empty() && v == 0) continue;
+    if (num.empty() && (v & 0x80)) num.push_back(0);
+    num.push_back(v);
+  }
+  if (num.empty()) num.push_back(0);
+  std::vector<uint8_t> body;
+  body.push_back(0x02);
+  asn1_len(&body, num.size());
+  body.insert(body.end(), num.begin(), num.end());
+  body.push_back(0x04);
+  asn1_len(&body, prev.n);
+  if (prev.n) body.insert(body.end(), prev.p, prev.p + prev.n);
+  body.push_back(0x04);
+  asn1_len(&body, data_hash.n);
+  if (data_hash.n) body.insert(body.end(), data_hash.p, data_hash.p + data_hash.n);
+  std::vector<uint8_t> out;
+  out.push_back(0x30);
+  asn1_len(&out, body.size());
+  out.insert(out.end(), body.begin(), body.end());
+  return out;
+}
+
+}  // namespace
+
+// Block signatures (protoutil/blockutils.go:245-300 BlockSignatureVerifier,
+// non-BFT form; called by orderer/common/cluster/util.go:300
+// VerifyBlockSignature and the peer's gossip MCS) for n serialized blocks in
+// one device batch.
+extern "C" int bh_block_signatures_preverify(const uint8_t* blocks, const uint64_t* block_off,
+                                             const uint32_t* block_len, size_t n, uint32_t flags,
+                                             bh_blocksig_result* res, uint8_t* sig_reason,
+                                             size_t sig_cap, size_t* sig_total) {
+  if (!sig_total || (n && (!blocks || !block_off || !block_len || !res)))
+    return bh::host_fail(BH_E_INVALID, "null argument");
+  if (flags & ~(uint32_t)(BH_FAB_F_SHA3 | BH_FAB_F_KEEP_KEYS | BH_FAB_F_DECODE_ONLY))
+    return bh::host_fail(BH_E_INVALID, "unknown flag");
+  std::vector<SdEntry> e;
+  std::vector<SetRange> sets;
+  std::vector<std::vector<uint8_t>> hdr_der(n);  // BlockHeaderBytes per block (kept alive)
+  std::vector<size_t> set_of(n, SIZE_MAX);
+  for (size_t i = 0; i < n; i++) {
+    res[i] = bh_blocksig_result{BH_BLK_OK, 0, 0, 0};
+    Span header, metadata;
+    bool has_header = false, has_meta = false;
+    std::vector<Span> mds;
+    uint64_t number = 0;
+    Span prev, dhash;
+    const bool ok = pb_walk(blocks + block_off[i], block_len[i], [&](const Field& f) {
+      if (is_bytes(f, 1)) {
+        has_header = true;
+        return pb_walk(f.s.p, f.s.n, [&](const Field& g) {
+          if (is_varint(g, 1)) number = g.v;
+          else if (is_bytes(g, 2)) prev = g.s;
+          else if (is_bytes(g, 3)) dhash = g.s;
+          return true;
+        });
+      }
+      if (is_bytes(f, 2)) return pb_walk(f.s.p, f.s.n, [&](const Field&) { return true; });
+      if (is_bytes(f, 3)) {
+        has_meta = true;
+        return pb_walk(f.s.p, f.s.n, [&](const Field& g) {
+          if (is_bytes(g, 1)) mds.push_back(g.s);
+          return true;
+        });
+      }
+      return true;
+    });
+    (void)header;
+    (void)metadata;
+    (void)has_meta;
+    if (!ok || !has_header) {  // Go dereferences the nil header
+      res[i].status = BH_BLK_DECODE;
+      continue;
+    }
+    if (mds.size() < 1) {  // "no signatures in block metadata"
+      res[i].status = BH_BLK_NO_SIGNATURES;
+      continue;
+    }
+    // cb.Metadata{1 value, 2 signatures: MetadataSignature{1 signature_header,
+    // 2 signature, 3 identifier_header}}
+    Span value;
+    struct MSig {
+      Span sh, sig, idh;
+    };
+    std::vector<MSig> sigs;
+    const bool mok = pb_walk(mds[0].p, mds[0].n, [&](const Field& f) {
+      if (is_bytes(f, 1)) {
+        value = f.s;
+      } else if (is_bytes(f, 2)) {
+        MSig m;
+        bool k = pb_walk(f.s.p, f.s.n, [&](const Field& g) {
+          if (is_bytes(g, 1)) m.sh = g.s;
+          else if (is_bytes(g, 2)) m.sig = g.s;
+          else if (is_bytes(g, 3)) m.idh = g.s;
+          return true;
+        });
+        sigs.push_back(m);
+        return k;
+      }
+      return true;
+    });
+    if (!mok) {
+      res[i].status = BH_BLK_METADATA;
+      continue;
+    }
+    hdr_der[i] = block_header_bytes(number, prev, dhash);
+    const size_t first = e.size();
+    bool bad = false;
+    for (const MSig& m : sigs) {
+      SignatureHeader sh;
+      if (!dec_signature_header(m.sh, &sh)) {  // fails the whole verifier
+        res[i].status = BH_BLK_SIGNATURE_HEADER;
+        bad = true;
+        break;
+      }
+      SdEntry x;
+      x.id = ident_cache().get(sh.creator);
+      x.seg[0] = value;
+      x.seg[1] = m.sh;
+      x.seg[2] = Span{hdr_der[i].data(), hdr_der[i].size(), true};
+      x.nseg = 3;
+      x.sig = m.sig;
+      e.push_back(x);
+    }
+    if (bad) {
+      e.resize(first);
+      continue;
+    }
+    res[i].sig_first = (uint32_t)first;
+    res[i].sig_count = (uint32_t)(e.size() - first);
+    set_of[i] = sets.size();
+    sets.push_back(SetRange{first, e.size() - first});
+  }
+  *sig_total = e.size();
+  if (e.size() && (!sig_reason || sig_cap < e.size()))
+    return bh::host_fail(BH_E_INVALID, "sig_reason too small (see *sig_total)");
+  std::vector<uint32_t> valid;
+  if (int rc = verify_sets(e, sets, verify_flags(flags), (flags & BH_FAB_F_DECODE_ONLY) != 0,
+                           &valid, nullptr))
+    return rc;
+  for (size_t i = 0; i < n; i++)
+    if (set_of[i] != SIZE_MAX) res[i].valid_identities = valid[set_of[i]];
+  for (size_t k = 0; k < e.size(); k++) sig_reason[k] = e[k].out;
   return BH_OK;
 }

@@ -61,3 +61,85 @@ def block_preverify(block: bytes, sha3: bool = False, keep_keys: bool = False,
                             [int(x) for x in end[t.endorse_first:t.endorse_first + t.endorse_count]],
                             t.valid_endorsers))
     return out
+
+
+def _concat(items):
+    ln = np.array([len(x) for x in items], np.uint32)
+    off = np.zeros(len(items), np.uint64)
+    if len(items):
+        off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(items) + b"\0", np.uint8)
+    return buf, off, ln
+
+
+def _flags(sha3, keep_keys, decode_only):
+    return ((_lib.BH_FAB_F_SHA3 if sha3 else 0) | (_lib.BH_FAB_F_KEEP_KEYS if keep_keys else 0)
+            | (_lib.BH_FAB_F_DECODE_ONLY if decode_only else 0))
+
+
+def signature_sets_verify(sets, sha3: bool = False, keep_keys: bool = False,
+                          decode_only: bool = False):
+    """common/policies/policy.go:363-395 SignatureSetToValidIdentities for many
+    sets of (identity, data, signature) in one device batch. Returns
+    [(per-entry results, valid identities)] per set."""
+    L = _lib.lib()
+    if not decode_only:
+        _lib.ensure_init()
+    flat = [sd for s in sets for sd in s]
+    first = np.zeros(max(1, len(sets)), np.uint32)
+    k = 0
+    for i, s in enumerate(sets):
+        first[i] = k
+        k += len(s)
+    ib, io, il = _concat([x[0] for x in flat])
+    db, do, dl = _concat([x[1] for x in flat])
+    sb, so, sl = _concat([x[2] for x in flat])
+    b = _lib.BhSdBatch(ib.ctypes.data, io.ctypes.data, il.ctypes.data, db.ctypes.data,
+                       do.ctypes.data, dl.ctypes.data, sb.ctypes.data, so.ctypes.data,
+                       sl.ctypes.data)
+    res = np.zeros(max(1, len(flat)), np.uint8)
+    valid = np.zeros(max(1, len(sets)), np.uint32)
+    _lib.check(L.bh_signature_sets_verify(ctypes.byref(b), len(flat), first.ctypes.data, len(sets),
+                                          _flags(sha3, keep_keys, decode_only), res.ctypes.data,
+                                          valid.ctypes.data))
+    out, k = [], 0
+    for i, s in enumerate(sets):
+        out.append(([int(x) for x in res[k:k + len(s)]], int(valid[i])))
+        k += len(s)
+    return out
+
+
+def envelopes_preverify(envs, sha3: bool = False, keep_keys: bool = False,
+                        decode_only: bool = False):
+    """SigFilter over n serialized envelopes: [(status, reason)]."""
+    L = _lib.lib()
+    if not decode_only:
+        _lib.ensure_init()
+    buf, off, ln = _concat(envs)
+    n = len(envs)
+    st = np.zeros(max(1, n), np.int32)
+    rs = np.zeros(max(1, n), np.uint8)
+    _lib.check(L.bh_envelopes_preverify(buf.ctypes.data, off.ctypes.data, ln.ctypes.data, n,
+                                        _flags(sha3, keep_keys, decode_only), st.ctypes.data,
+                                        rs.ctypes.data))
+    return [(int(st[i]), int(rs[i])) for i in range(n)]
+
+
+def block_signatures_preverify(blocks, sha3: bool = False, keep_keys: bool = False,
+                               decode_only: bool = False):
+    """Block signature sets of n serialized blocks: [(status, per-signature,
+    valid identities)]."""
+    L = _lib.lib()
+    if not decode_only:
+        _lib.ensure_init()
+    buf, off, ln = _concat(blocks)
+    n = len(blocks)
+    res = (_lib.BhBlocksigResult * max(1, n))()
+    total = ctypes.c_size_t()
+    cap = sum(len(b) for b in blocks) // 8 + 64
+    sr = np.zeros(cap, np.uint8)
+    _lib.check(L.bh_block_signatures_preverify(buf.ctypes.data, off.ctypes.data, ln.ctypes.data, n,
+                                               _flags(sha3, keep_keys, decode_only), res,
+                                               sr.ctypes.data, cap, ctypes.byref(total)))
+    return [(res[i].status, [int(x) for x in sr[res[i].sig_first:res[i].sig_first + res[i].sig_count]],
+             res[i].valid_identities) for i in range(n)]

@@ -374,3 +374,70 @@ def generate_fabric_block(ntx: int = 500, endorsements: int = 3, norgs: int = 4,
     metadata = b"".join(pb_bytes(1, b"") for _ in range(5))
     fb.block = pb_bytes(1, header) + pb_bytes(2, data) + pb_bytes(3, metadata)
     return fb
+
+
+# ---------------------------------------------------------------- block signatures
+def block_header_der(number: int, prev: bytes, data_hash: bytes) -> bytes:
+    """protoutil.BlockHeaderBytes: ASN.1 DER of (number, previous_hash, data_hash)."""
+    num = number.to_bytes(max(1, (number.bit_length() + 8) // 8), "big")
+    return der(0x30, der(0x02, num) + der(0x04, prev) + der(0x04, data_hash))
+
+
+BLOCKSIG_CORRUPTIONS = ["none", "sig_flip", "dup_signer", "bad_identity", "high_s",
+                        "bad_sig_header", "no_metadata", "header_number"]
+
+
+def generate_signed_blocks(nblocks: int = 16, norderers: int = 4, seed: int = 21,
+                           classes: list[str] | None = None):
+    """Blocks as an orderer cluster delivers them: the SIGNATURES metadata
+    entry carries one MetadataSignature per orderer over Metadata.value ||
+    signature_header || BlockHeaderBytes(header) (protoutil/blockutils.go
+    :245-300). Returns (blocks, expected) with expected[i] = (status,
+    per-signature BH_R_* / 253 dup / 254 bad identity, valid identities)."""
+    L = _gen()
+    st = [seed * 0x2545F4914F6CDD1D + 5]
+    _, orderers, _ = make_identities(L, seed, norderers, 0)
+    bad_ident = serialized_identity("OrdererMSP", b"-----BEGIN CERTIFICATE-----\n!!\n"
+                                                  b"-----END CERTIFICATE-----\n")
+    blocks, expected = [], []
+    prev = b"\x00" * 32
+    for bi in range(nblocks):
+        cls = classes[bi % len(classes)] if classes else "none"
+        data = b"".join(pb_bytes(1, _rand_bytes(st, 100)) for _ in range(3))
+        dhash = hashlib.sha256(data).digest()
+        number = 1000 + bi
+        hdr_pb = pb_varint(1, number) + pb_bytes(2, prev) + pb_bytes(3, dhash)
+        hder = block_header_der(number, prev, dhash)
+        value = pb_bytes(1, pb_varint(1, number - 1))  # OrdererBlockMetadata-like value
+        sigs, want = [], []
+        for k, o in enumerate(orderers):
+            shdr = pb_bytes(1, bad_ident if (cls == "bad_identity" and k == 0) else o.serialized) \
+                + pb_bytes(2, _rand_bytes(st, 24))
+            sg = sign(L, o.priv, value + shdr + hder, seed + 100 * bi + k,
+                      high_s=(cls == "high_s" and k == 1))
+            if cls == "sig_flip" and k == 2:
+                sg = sg[:-1] + bytes([sg[-1] ^ 1])
+            sigs.append(pb_bytes(1, shdr) + pb_bytes(2, sg))
+            want.append(254 if (cls == "bad_identity" and k == 0) else
+                        6 if (cls == "high_s" and k == 1) else
+                        9 if (cls == "sig_flip" and k == 2) else 0)
+        if cls == "dup_signer":
+            sigs.append(sigs[0])
+            want.append(253)
+        if cls == "bad_sig_header":
+            sigs.append(pb_bytes(1, b"\x0a\xff") + pb_bytes(2, b"\x30\x00"))
+        md = pb_bytes(1, value) + b"".join(pb_bytes(2, x) for x in sigs)
+        meta = b"" if cls == "no_metadata" else pb_bytes(1, md) + pb_bytes(1, b"") + pb_bytes(1, b"")
+        hdr_used = hdr_pb if cls != "header_number" else (pb_varint(1, number + 1) + pb_bytes(2, prev)
+                                                          + pb_bytes(3, dhash))
+        blocks.append(pb_bytes(1, hdr_used) + pb_bytes(2, data) + pb_bytes(3, meta))
+        if cls == "bad_sig_header":
+            expected.append((4, [], 0))
+        elif cls == "no_metadata":
+            expected.append((2, [], 0))
+        elif cls == "header_number":
+            expected.append((0, [9] * len(orderers), 0))
+        else:
+            expected.append((0, want, sum(1 for w in want if w == 0)))
+        prev = hashlib.sha256(hder).digest()
+    return blocks, expected

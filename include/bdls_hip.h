@@ -330,6 +330,65 @@ int bh_fabric_block_preverify(const uint8_t *block, size_t len, uint32_t flags, 
                               size_t tx_cap, size_t *n_tx, uint8_t *endorse, size_t endorse_cap,
                               size_t *n_endorse);
 
+/* ---- signature sets: SignatureSetToValidIdentities as a batch ------------------
+ * common/policies/policy.go:363-395, the batch point of every policy
+ * evaluation (cauthdsl, implicit-meta sub-policies, the endorsement policy,
+ * SigFilter, block signatures): for each signature set, in order, an entry
+ * whose identity does not deserialize is skipped, an entry of an identity
+ * already validated earlier in the set is skipped (de-duplication by Mspid +
+ * Id, Id over the sanitized certificate), every other entry is verified with
+ * identity.Verify (hash of data, then Verify, low-S). Sets are [set_first[k],
+ * set_first[k+1]) (the last ends at n). result[i]: BH_R_* when verified,
+ * BH_FAB_E_DUPLICATE, BH_FAB_E_BAD_IDENTITY, or BH_SP_NOT_VERIFIED;
+ * valid_identities[k] = the number of identities the set yields. Flags:
+ * BH_FAB_F_SHA3 / BH_FAB_F_KEEP_KEYS / BH_FAB_F_DECODE_ONLY. */
+typedef struct bh_sd_batch { /* protoutil.SignedData {Identity, Data, Signature}, SoA */
+  const uint8_t *identity;   /* msp.SerializedIdentity bytes */
+  const uint64_t *identity_off;
+  const uint32_t *identity_len;
+  const uint8_t *data;       /* the signed bytes */
+  const uint64_t *data_off;
+  const uint32_t *data_len;
+  const uint8_t *sig;        /* DER signatures */
+  const uint64_t *sig_off;
+  const uint32_t *sig_len;
+} bh_sd_batch;
+int bh_signature_sets_verify(const bh_sd_batch *b, size_t n, const uint32_t *set_first,
+                             size_t n_sets, uint32_t flags, uint8_t *result,
+                             uint32_t *valid_identities);
+
+/* Orderer broadcast SigFilter (orderer/common/msgprocessor/sigfilter.go:50-80)
+ * for n serialized common.Envelopes: EnvelopeAsSignedData
+ * (protoutil/signeddata.go:60-86) then the one-signature set of the policy.
+ * status[i]: BH_FAB_OK, BH_FAB_ENVELOPE, BH_FAB_PAYLOAD, BH_FAB_HEADER
+ * ("Missing Header" / signature header), BH_FAB_CREATOR_IDENTITY,
+ * BH_FAB_CREATOR_SIGNATURE; reason[i]: BH_R_* or BH_SP_NOT_VERIFIED. */
+int bh_envelopes_preverify(const uint8_t *envs, const uint64_t *env_off, const uint32_t *env_len,
+                           size_t n, uint32_t flags, int32_t *status, uint8_t *reason);
+
+/* Block signatures (protoutil/blockutils.go:245-300 BlockSignatureVerifier,
+ * non-BFT form, as orderer/common/cluster/util.go:300 VerifyBlockSignature and
+ * the peer's gossip MCS run it) for n serialized blocks: per block the
+ * SIGNATURES metadata's signature set, signed data = Metadata.value ||
+ * signature_header || BlockHeaderBytes(header) (ASN.1 DER of number,
+ * previous_hash, data_hash), de-duplicated as above. sig_reason[]:
+ * one byte per MetadataSignature, block i's at [sig_first, +sig_count). */
+#define BH_BLK_OK 0
+#define BH_BLK_DECODE 1            /* block does not unmarshal or has no header */
+#define BH_BLK_NO_SIGNATURES 2     /* "no signatures in block metadata" */
+#define BH_BLK_METADATA 3          /* Metadata does not unmarshal */
+#define BH_BLK_SIGNATURE_HEADER 4  /* a signature header does not unmarshal */
+typedef struct bh_blocksig_result {
+  int32_t status;            /* BH_BLK_* */
+  uint32_t sig_first;
+  uint32_t sig_count;
+  uint32_t valid_identities; /* identities the policy evaluation receives */
+} bh_blocksig_result;
+int bh_block_signatures_preverify(const uint8_t *blocks, const uint64_t *block_off,
+                                  const uint32_t *block_len, size_t n, uint32_t flags,
+                                  bh_blocksig_result *res, uint8_t *sig_reason, size_t sig_cap,
+                                  size_t *sig_total);
+
 /* ---- X.509 certificate signatures ---------------------------------------------
  * Certificate i's signature against issuer key i (X || Y): Go crypto/x509
  * Certificate.CheckSignatureFrom for an ECDSA issuer (checkSignature: SHA-256

@@ -477,3 +477,116 @@ def validate_block(block: bytes, verify, decode_only: bool = False) -> list[TxOu
                 id_map.add(ident.key)
         t.valid_endorsers = len(id_map)
     return out
+
+
+# ---------------------------------------------------------------- policy batch point
+def signature_set_to_valid_identities(entries, verify, decode_only: bool = False):
+    """common/policies/policy.go:363-395 over one set of (identity, data, sig):
+    per entry BH_R_* / E_DUP / E_BAD_IDENTITY / NOT_VERIFIED, and the number
+    of valid (de-duplicated) identities."""
+    from . import ecdsa_ref as O
+    n, half = O.P256.n, O.P256.n >> 1
+    id_map, out = set(), []
+    for ident_bytes, data, sig in entries:
+        ident = deserialize(ident_bytes, half, n)
+        if ident is None:
+            out.append(E_BAD_IDENTITY)
+            continue
+        if ident.key in id_map:
+            out.append(E_DUP)
+            continue
+        if decode_only:
+            out.append(NOT_VERIFIED)
+            continue
+        r = verify(ident.x, ident.y, data, sig)
+        out.append(r)
+        if r == 0:
+            id_map.add(ident.key)
+    return out, len(id_map)
+
+
+def envelope_as_signed_data(env_bytes: bytes):
+    """protoutil/signeddata.go:60-86 -> (status, (identity, data, sig) or None)."""
+    try:
+        env = unmarshal(env_bytes, ENVELOPE_SPEC)
+    except DecodeError:
+        return ENVELOPE, None
+    try:
+        pl = unmarshal(env["payload"] or b"", PAYLOAD_SPEC)
+    except DecodeError:
+        return PAYLOAD, None
+    if pl["header"] is None:
+        return HEADER, None  # "Missing Header"
+    try:
+        sh = unmarshal(pl["header"]["signature_header"] or b"", SIGNATURE_HEADER_SPEC)
+    except DecodeError:
+        return HEADER, None
+    return OK, (sh["creator"] or b"", env["payload"] or b"", env["signature"] or b"")
+
+
+def sigfilter(env_bytes: bytes, verify, decode_only: bool = False):
+    """orderer/common/msgprocessor/sigfilter.go:50-80 -> (status, reason)."""
+    st, sd = envelope_as_signed_data(env_bytes)
+    if st != OK:
+        return st, NOT_VERIFIED
+    res, _ = signature_set_to_valid_identities([sd], verify, decode_only)
+    r = res[0]
+    if r == E_BAD_IDENTITY:
+        return CREATOR_IDENTITY, NOT_VERIFIED
+    if r not in (0, NOT_VERIFIED):
+        return CREATOR_SIGNATURE, r
+    return OK, r
+
+
+# block signatures
+BLK_OK, BLK_DECODE, BLK_NO_SIGNATURES, BLK_METADATA, BLK_SIGNATURE_HEADER = range(5)
+METADATA_SPEC = {1: ("value", "bytes"),
+                 2: ("signatures", ("rep", {1: ("signature_header", "bytes"),
+                                            2: ("signature", "bytes"),
+                                            3: ("identifier_header", "bytes")}))}
+
+
+def _der(tag: int, content: bytes) -> bytes:
+    n = len(content)
+    if n < 0x80:
+        return bytes([tag, n]) + content
+    b = n.to_bytes((n.bit_length() + 7) // 8, "big")
+    return bytes([tag, 0x80 | len(b)]) + b + content
+
+
+def block_header_bytes(number: int, prev: bytes, data_hash: bytes) -> bytes:
+    """protoutil/blockutils.go:42-62: asn1.Marshal(asn1Header{Number *big.Int,
+    PreviousHash, DataHash})."""
+    num = number.to_bytes(max(1, (number.bit_length() + 8) // 8), "big")
+    return _der(0x30, _der(0x02, num) + _der(0x04, prev) + _der(0x04, data_hash))
+
+
+def block_signatures(block: bytes, verify, decode_only: bool = False):
+    """protoutil/blockutils.go:245-300 BlockSignatureVerifier (non-BFT) ->
+    (status, per-signature results, valid identities)."""
+    try:
+        blk = unmarshal(block, BLOCK_SPEC)
+    except DecodeError:
+        return BLK_DECODE, [], 0
+    if blk["header"] is None:
+        return BLK_DECODE, [], 0
+    mds = (blk["metadata"] or {"metadata": []})["metadata"]
+    if len(mds) < 1:
+        return BLK_NO_SIGNATURES, [], 0
+    try:
+        md = unmarshal(mds[0], METADATA_SPEC)
+    except DecodeError:
+        return BLK_METADATA, [], 0
+    h = blk["header"]
+    hdr = block_header_bytes(h["number"], h["previous_hash"] or b"", h["data_hash"] or b"")
+    entries = []
+    for ms in md["signatures"]:
+        try:
+            sh = unmarshal(ms["signature_header"] or b"", SIGNATURE_HEADER_SPEC)
+        except DecodeError:
+            return BLK_SIGNATURE_HEADER, [], 0
+        entries.append((sh["creator"] or b"",
+                        (md["value"] or b"") + (ms["signature_header"] or b"") + hdr,
+                        ms["signature"] or b""))
+    res, nvalid = signature_set_to_valid_identities(entries, verify, decode_only)
+    return BLK_OK, res, nvalid

@@ -186,3 +186,84 @@ def test_gpu_config3_block():
     for keep in (False, True, True):
         got = fabric.block_preverify(fb.block, keep_keys=keep)
         assert [_got(t) for t in got] == want
+
+
+# ---------------------------------------------------------------- orderer callers
+@pytest.fixture(scope="module")
+def signed_blocks():
+    return F.generate_signed_blocks(nblocks=2 * len(F.BLOCKSIG_CORRUPTIONS),
+                                    classes=F.BLOCKSIG_CORRUPTIONS)
+
+
+def test_blocksig_oracle_matches_construction(signed_blocks):
+    blocks, exp = signed_blocks
+    assert [R.block_signatures(b, _py_verify) for b in blocks] == exp
+
+
+def test_blocksig_decode_matches_oracle(signed_blocks):
+    blocks, _ = signed_blocks
+    rng = random.Random(5)
+    cases = list(blocks) + [_mutate(rng, rng.choice(blocks)) for _ in range(1500)]
+    py = [R.block_signatures(b, None, decode_only=True) for b in cases]
+    cc = fabric.block_signatures_preverify(cases, decode_only=True)
+    assert py == [tuple(c) for c in cc]
+
+
+def test_sigfilter_decode_matches_oracle(classes_block):
+    rng = random.Random(6)
+    envs = _envelopes(classes_block.block)
+    cases = list(envs) + [_nested_mutation(rng, rng.choice(envs[:5])) for _ in range(1500)]
+    py = [R.sigfilter(e, None, decode_only=True) for e in cases]
+    cc = fabric.envelopes_preverify(cases, decode_only=True)
+    assert py == cc
+
+
+def _sets_case(seed=8):
+    """Signature sets drawn from a block's endorsements: duplicates, bad
+    identities, failed-then-valid identities, empty sets."""
+    fb = F.generate_fabric_block(ntx=12, corrupt_den=0, classes=F.CORRUPTIONS, seed=seed)
+    sds = []
+    for env in _envelopes(fb.block):
+        try:
+            e = R.unmarshal(env, R.ENVELOPE_SPEC)
+            pl = R.unmarshal(e["payload"], R.PAYLOAD_SPEC)
+            tx = R.unmarshal(pl["data"], R.TRANSACTION_SPEC)
+            cap = R.unmarshal(tx["actions"][0]["payload"], R.CC_ACTION_PAYLOAD_SPEC)
+        except (R.DecodeError, IndexError, TypeError):
+            continue
+        prp = cap["action"]["proposal_response_payload"]
+        for x in cap["action"]["endorsements"]:
+            sds.append((x["endorser"], prp + x["endorser"], x["signature"]))
+    rng = random.Random(seed)
+    sets = [[]]
+    for _ in range(40):
+        sets.append([rng.choice(sds) for _ in range(rng.randrange(1, 7))])
+    return sets
+
+
+def test_sets_decode_matches_oracle():
+    sets = _sets_case()
+    py = [R.signature_set_to_valid_identities(s, None, decode_only=True) for s in sets]
+    cc = fabric.signature_sets_verify(sets, decode_only=True)
+    assert py == cc
+
+
+@pytest.mark.gpu
+def test_gpu_signature_sets():
+    sets = _sets_case()
+    want = [R.signature_set_to_valid_identities(s, _orc_verify) for s in sets]
+    assert fabric.signature_sets_verify(sets) == want
+
+
+@pytest.mark.gpu
+def test_gpu_sigfilter(classes_block):
+    envs = _envelopes(classes_block.block)
+    want = [R.sigfilter(e, _orc_verify) for e in envs]
+    assert fabric.envelopes_preverify(envs) == want
+
+
+@pytest.mark.gpu
+def test_gpu_block_signatures(signed_blocks):
+    blocks, exp = signed_blocks
+    got = fabric.block_signatures_preverify(blocks)
+    assert [tuple(g) for g in got] == exp
