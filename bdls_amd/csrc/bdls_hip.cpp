@@ -134,10 +134,10 @@ struct HostBuf {
   }
 };
 
-// One of the double-buffered host-API pipeline slots of a device: its own
+// One of the host-API pipeline slots of a device (triple-buffered): its own
 // device staging for the inputs, device and pinned-host buffers for the
 // outputs, and the events that order upload -> verify -> download. While the
-// compute stream verifies slot k's batch, the copy stream uploads slot k^1's.
+// compute stream verifies one slot's batch, the copy stream uploads the next.
 struct Slot {
   DevBuf stage;     // inputs (H2D on the copy stream)
   DevBuf out;       // bitmap words + reasons (device)
@@ -146,7 +146,7 @@ struct Slot {
   bh_job* owner = nullptr;  // job whose results are in flight / sit in host_out
   size_t owner_part = 0;
 };
-constexpr int kSlots = 2;
+constexpr int kSlots = 3;  // up to 3 host batches in flight per device
 
 struct Dev {
   int id = -1;

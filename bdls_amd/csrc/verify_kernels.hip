@@ -245,14 +245,35 @@ __global__ __launch_bounds__(256) void k_key_insert(Work w, Plan pl, KeyReg g, u
 }
 
 // Full-key check against the slot's representative (fingerprint collisions
-// fall back to the ladder), then count.
-__global__ __launch_bounds__(256) void k_key_count(Work w, Plan pl, uint32_t n) {
+// fall back to the ladder), then count. Keys compare as their 64 input bytes
+// X || Y: prep admitted only coordinates < p, so equal bytes <=> equal point,
+// and the representative's key is one contiguous 64-byte read instead of 18
+// scattered limb-major words. A16: the key array is 16-byte aligned.
+template <bool A16>
+__global__ __launch_bounds__(256) void k_key_count(Work w, Plan pl, const uint8_t* __restrict__ pub,
+                                                   uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t p = pl.rec_slot[i];
   if (p == kNone) return;
   const uint32_t rep = pl.slot_rep[p];
-  if (rep == i || same_key(w, i, rep)) {
+  bool same = rep == i;
+  if (!same) {
+    uint32_t d = 0;
+    if constexpr (A16) {
+      const uint4* a = reinterpret_cast<const uint4*>(pub + (size_t)i * 64);
+      const uint4* b = reinterpret_cast<const uint4*>(pub + (size_t)rep * 64);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint4 x = a[k], y = b[k];
+        d |= (x.x ^ y.x) | (x.y ^ y.y) | (x.z ^ y.z) | (x.w ^ y.w);
+      }
+    } else {
+      for (int k = 0; k < 64; k++) d |= pub[(size_t)i * 64 + k] ^ pub[(size_t)rep * 64 + k];
+    }
+    same = d == 0;
+  }
+  if (same) {
     atomicAdd(&pl.slot_cnt[p], 1u);
   } else {
     pl.rec_slot[i] = kNone;
@@ -304,8 +325,22 @@ __global__ __launch_bounds__(256) void k_split(Work w, Plan pl, uint32_t n,
     if (p != kNone) t = pl.slot_tab[p];
     pl.rec_tab[i] = t;
   }
-  if (t != kNone) pl.comb_list[atomicAdd(&pl.counters[0], 1u)] = i;
-  else pl.ladder_list[atomicAdd(&pl.counters[1], 1u)] = i;
+  // one atomic per wave and list: lanes take consecutive slots by their rank
+  // among the wave's lanes bound for the same list (contended per-record
+  // atomics on two counters cost more than the rest of the routing)
+  const bool comb = t != kNone;
+  const uint64_t m_comb = __ballot(comb), m_lad = __ballot(!comb);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint32_t leader_c = __ffsll((unsigned long long)m_comb) - 1;
+  const uint32_t leader_l = __ffsll((unsigned long long)m_lad) - 1;
+  uint32_t base_c = 0, base_l = 0;
+  if (comb && lane == leader_c) base_c = atomicAdd(&pl.counters[0], (uint32_t)__popcll(m_comb));
+  if (!comb && lane == leader_l) base_l = atomicAdd(&pl.counters[1], (uint32_t)__popcll(m_lad));
+  base_c = __shfl(base_c, (int)leader_c, 64);
+  base_l = __shfl(base_l, (int)leader_l, 64);
+  if (comb) pl.comb_list[base_c + __popcll(m_comb & below)] = i;
+  else pl.ladder_list[base_l + __popcll(m_lad & below)] = i;
 }
 
 // Blocks [0, tab_blocks) build key tables (`parts` lanes per table); the rest run
@@ -465,6 +500,17 @@ hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s) {
   return hipGetLastError();
 }
 
+static const uint8_t* key_bytes(const BatchIn& in) { return in.pub; }
+static const uint8_t* key_bytes(const BdlsIn& in) { return in.xy; }
+
+static void launch_key_count(const Work& w, const Plan& pl, const uint8_t* pub, uint32_t n,
+                             dim3 grd, dim3 blk, hipStream_t s) {
+  if (((uintptr_t)pub & 15u) == 0)
+    hipLaunchKernelGGL(k_key_count<true>, grd, blk, 0, s, w, pl, pub, n);
+  else
+    hipLaunchKernelGGL(k_key_count<false>, grd, blk, 0, s, w, pl, pub, n);
+}
+
 static hipError_t plan_reset(const Plan& pl, hipStream_t s) {
   hipError_t e;
   if ((e = hipMemsetAsync(pl.slot_hash, 0, (size_t)pl.hc * 8, s))) return e;
@@ -551,7 +597,7 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   hipLaunchKernelGGL((k_inv<N>), grc, blk, 0, s, w, n, nlanes);
   REC(2);
   hipLaunchKernelGGL(k_key_insert, grd, blk, 0, s, w, pl, g, n);
-  hipLaunchKernelGGL(k_key_count, grd, blk, 0, s, w, pl, n);
+  launch_key_count(w, pl, key_bytes(in), n, grd, blk, s);
   hipLaunchKernelGGL(k_key_plan, grd, blk, 0, s, w, pl, g, n, o.min_uses, o.min_batch,
                      o.keep ? 1u : 0u, 0u);
   hipLaunchKernelGGL(k_split, grd, blk, 0, s, w, pl, n, reason);
@@ -617,7 +663,7 @@ static hipError_t reg_seq(const uint8_t* pub, const Work& w, const Plan& pl, con
   if ((e = plan_reset(pl, s))) return e;
   hipLaunchKernelGGL((k_reg_prep<P, C>), grd, blk, 0, s, pub, w, n);
   hipLaunchKernelGGL(k_key_insert, grd, blk, 0, s, w, pl, g, n);
-  hipLaunchKernelGGL(k_key_count, grd, blk, 0, s, w, pl, n);
+  launch_key_count(w, pl, pub, n, grd, blk, s);
   hipLaunchKernelGGL(k_key_plan, grd, blk, 0, s, w, pl, g, n, 1u, 0u, 1u, 1u);
   const uint32_t parts = pl.max_tables <= kSplitBuildMax ? 2u : 1u;
   const uint32_t tab_blocks = (parts * pl.max_tables + 255) / 256;
