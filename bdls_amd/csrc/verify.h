@@ -677,6 +677,141 @@ BH_HD void q_ladder(J30& A, bool& a_inf, const Work& w, uint32_t i, uint32_t wav
   }
 }
 
+// ---- secp256k1: GLV endomorphism (the split btcec uses to halve the
+// doublings, vendor/github.com/BDLS-bft/bdls/crypto/btcec/btcec.go:765-865
+// splitK). phi(x, y) = (beta x, y) = lambda (x, y); u2 = k1 + k2 lambda (mod n)
+// with |k1|, |k2| < 2^128, so u2 Q = k1 Q + k2 phi(Q): 125 doublings instead
+// of 255. The split is libsecp256k1's secp256k1_scalar_split_lambda (c_i =
+// round(u2 g_i / 2^384), k2 = c1 (-b1) + c2 (-b2), k1 = u2 - k2 lambda); any
+// valid split gives the same point, hence the same verdict, as btcec's.
+struct GlvK1 {
+  static constexpr uint32_t g1[8] = {0x45dbb031u, 0xe893209au, 0x71e8ca7fu, 0x3daa8a14u,
+                                     0x9284eb15u, 0xe86c90e4u, 0xa7d46bcdu, 0x3086d221u};
+  static constexpr uint32_t g2[8] = {0x8ac47f71u, 0x1571b4aeu, 0x9df506c6u, 0x221208acu,
+                                     0x0abfe4c4u, 0x6f547fa9u, 0x010e8828u, 0xe4437ed6u};
+  // -b1, -b2, -lambda times 2^256 mod n (a Montgomery product with them is a
+  // plain product mod n)
+  static constexpr uint32_t mb1R[8] = {0x0ad9263cu, 0xc50468d0u, 0xfaa6ed42u, 0x1b1c8205u,
+                                       0x8ac47f71u, 0x1571b4aeu, 0x9df506c6u, 0x221208acu};
+  static constexpr uint32_t mb2R[8] = {0x6a144696u, 0x0cac5e50u, 0xf3ba5939u, 0x1e8a8dc5u,
+                                       0xba244fceu, 0x176cdf65u, 0x8e173580u, 0xc25575ebu};
+  static constexpr uint32_t mlamR[8] = {0x06a3d4a3u, 0xcf54734fu, 0x2b820beeu, 0x8e1af539u,
+                                        0xad96826du, 0x8c5699f9u, 0x7aa729c6u, 0xacd7bfe8u};
+  // beta 2^270 mod p, radix 2^30 (canonical)
+  static constexpr uint32_t beta_m[9] = {0x22c82b32u, 0x361d08c9u, 0x02bd6290u,
+                                         0x1631c4b8u, 0x0140ff78u, 0x38d02e39u,
+                                         0x0fe3a625u, 0x2bcbb3d5u, 0x00008dabu};
+};
+
+// (k g) >> 384 rounded to nearest (bit 383 added); k, g < 2^256, result < 2^129
+BH_HD void mul_shift384(uint32_t out[8], const uint32_t k[8], const uint32_t g[8]) {
+  uint32_t t[16];
+#pragma unroll
+  for (int q = 0; q < 16; q++) t[q] = 0;
+#pragma unroll
+  for (int a = 0; a < 8; a++) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      c += (uint64_t)k[a] * g[b] + t[a + b];
+      t[a + b] = (uint32_t)c;
+      c >>= 32;
+    }
+    t[a + 8] = (uint32_t)c;
+  }
+  uint64_t c = t[11] >> 31;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    c += t[12 + q];
+    out[q] = (uint32_t)c;
+    c >>= 32;
+  }
+  out[4] = (uint32_t)c;
+  out[5] = out[6] = out[7] = 0;
+}
+
+// bits [b, b + 6) of a 160-bit value (5 limbs); b compile-time after unrolling
+BH_HD uint32_t bits6(const uint32_t v[5], uint32_t b) {
+  const uint32_t q = b >> 5, sh = b & 31u;
+  uint32_t x = v[q] >> sh;
+  if (sh > 26 && q + 1 < 5) x |= v[q + 1] << (32 - sh);
+  return x & 63u;
+}
+
+template <class P>
+BH_HD void j_acc(J30& A, bool& a_inf, const J30& T, bool t_inf);  // below
+
+template <class P>
+BH_HD void q_ladder_glv(J30& A, bool& a_inf, const Work& w, uint32_t i, uint32_t wave,
+                        uint32_t lane) {
+  uint32_t u2[8], qx[9], qy[9], one[9];
+  ld8(u2, w.r, i, w.ns);
+  ld9(qx, w.qx, i, w.ns);
+  ld9(qy, w.qy, i, w.ns);
+  f_const(one, P::r1);
+  J30 T;
+  f_copy(T.X, qx);
+  f_copy(T.Y, qy);
+  f_copy(T.Z, one);
+  qtab_store(w.qtab, wave, 0, lane, T);
+  j_dbl<P>(T, T);
+  qtab_store(w.qtab, wave, 1, lane, T);
+  for (uint32_t k = 2; k < kQTab; k++) {
+    bool same;
+    j_madd<P>(T, T, qx, qy, &same);  // (k+1) Q = k Q + Q, never degenerate for 2 <= k < 16
+    qtab_store(w.qtab, wave, k, lane, T);
+  }
+  // u2 = k1 + k2 lambda (mod n), then |k1|, |k2| with their signs
+  uint32_t c1[8], c2[8], k1[8], k2[8], t[8], cst[8];
+  mul_shift384(c1, u2, GlvK1::g1);
+  mul_shift384(c2, u2, GlvK1::g2);
+  load_const8(cst, GlvK1::mb1R);
+  mont_mul<Fn_k1>(k2, c1, cst);
+  load_const8(cst, GlvK1::mb2R);
+  mont_mul<Fn_k1>(t, c2, cst);
+  mod_add<Fn_k1>(k2, k2, t);
+  load_const8(cst, GlvK1::mlamR);
+  mont_mul<Fn_k1>(k1, k2, cst);
+  mod_add<Fn_k1>(k1, k1, u2);
+  load_const8(cst, Cv_k1::half_n);
+  const bool s1 = !geq8(cst, k1), s2 = !geq8(cst, k2);  // "negative": > n/2
+  if (s1) mod_neg<Fn_k1>(k1, k1);
+  if (s2) mod_neg<Fn_k1>(k2, k2);
+  // Booth windows read bits [5 win - 1, 5 win + 4]: K = k << 1 (k < 2^128,
+  // so windows 0..25 suffice and the top digit is non-negative)
+  uint32_t K1[5], K2[5];
+  K1[0] = k1[0] << 1;
+  K2[0] = k2[0] << 1;
+#pragma unroll
+  for (int q = 1; q < 5; q++) {
+    K1[q] = (k1[q] << 1) | (k1[q - 1] >> 31);
+    K2[q] = (k2[q] << 1) | (k2[q - 1] >> 31);
+  }
+  uint32_t beta[9];
+  f_const(beta, GlvK1::beta_m);
+  f_copy(A.X, one);
+  f_copy(A.Y, one);
+  f_copy(A.Z, one);
+  a_inf = true;
+  for (int win = 25; win >= 0; win--) {
+    if (win != 25)
+      for (int d = 0; d < 5; d++) j_dbl<P>(A, A);
+    uint32_t mag;
+    bool neg;
+    booth5(bits6(K1, 5u * (uint32_t)win), &mag, &neg);
+    J30 T1;
+    qtab_load(T1, w.qtab, wave, mag ? mag - 1 : 0, lane);
+    if (neg != s1) f_neg<P, 64>(T1.Y, T1.Y);
+    j_acc<P>(A, a_inf, T1, mag == 0);
+    booth5(bits6(K2, 5u * (uint32_t)win), &mag, &neg);
+    J30 T2;
+    qtab_load(T2, w.qtab, wave, mag ? mag - 1 : 0, lane);
+    f_mul<P>(T2.X, T2.X, beta);  // phi: (beta X, Y, Z)
+    if (neg != s2) f_neg<P, 64>(T2.Y, T2.Y);
+    j_acc<P>(A, a_inf, T2, mag == 0);
+  }
+}
+
 // Returns true iff the signature equation holds (valid). Lanes whose prep
 // failed run on placeholder inputs (Q = G, u1 = u2 = 1) and are masked by the
 // caller.
@@ -685,7 +820,8 @@ BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_
                         uint32_t lane) {
   J30 A, B;
   bool a_inf, b_inf;
-  q_ladder<P>(A, a_inf, w, i, wave, lane);
+  if constexpr (P::a_is_minus3) q_ladder<P>(A, a_inf, w, i, wave, lane);
+  else q_ladder_glv<P>(A, a_inf, w, i, wave, lane);
   uint32_t u1[8];
   ld8(u1, w.e, i, w.ns);
   g_comb<P>(B, b_inf, gtab, u1);

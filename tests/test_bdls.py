@@ -106,6 +106,24 @@ def _k1_edge_records():
         s = 2 * r * d * pow(k, -1, c.n) % c.n
         add("k1_u1G_eq_u2Q", qx, qy, r, s, e.to_bytes(32, "big"))
         add("k1_u1G_eq_u2Q_high_s", qx, qy, r, c.n - s, e.to_bytes(32, "big"))
+    # GLV split edges (verify.h q_ladder_glv): valid signatures built for a
+    # chosen u2 -- R = u1 G + u2 Q, r = x(R) mod n, s = r / u2, e = u1 s
+    lam = 0x5363AD4CC05C30E0A5261C028812645A122E22EA20816678DF02967C1B23BD72
+    n = c.n
+    u2s = [1, 2, 3, 15, 16, 17, 31, 32, 33, lam, n - lam, lam * lam % n, 2**127, 2**128 - 1,
+           2**128, 2**128 + 1, n - 1, n - 2, n // 2, n // 2 + 1, (2**128 * lam) % n,
+           (12345 * lam) % n, (n - 12345 * lam % n) % n, (2**64 + 5 * lam) % n]
+    u2s += [rng.randrange(1, n) for _ in range(8)] + [rng.randrange(1, 2**128) for _ in range(4)]
+    for u2 in u2s:
+        u1 = rng.randrange(1, n)
+        R = O.point_add(c, O.scalar_mult(c, u1, (c.gx, c.gy)), O.scalar_mult(c, u2, (qx, qy)))
+        if R is None or R[0] % n == 0:
+            continue
+        r = R[0] % n
+        s = r * pow(u2, -1, n) % n
+        e = u1 * s % n
+        add("k1_glv_u2", qx, qy, r, s, e.to_bytes(32, "big"))
+        add("k1_glv_u2_flip", qx, qy, r, s, (e ^ 1).to_bytes(32, "big"))
     for _ in range(6):  # plain valid / invalid, high-S accepted (no low-S rule)
         msgd = bytes(rng.getrandbits(8) for _ in range(32))
         r, s = O.sign_digest(c, d, msgd, rng.randrange(1, c.n), low_s=False)
@@ -138,6 +156,7 @@ def test_k1_curve_edges_hostsim(hs, min_uses, wide):
     bad = [(t[0], int(o), t[5]) for t, o in zip(recs, out) if o != t[5]]
     assert not bad
     assert any(t[0] == "k1_xwrap_accept" and t[5] == 0 for t in recs)
+    assert sum(t[0] == "k1_glv_u2" and t[5] == 0 for t in recs) >= 30
 
 
 @pytest.mark.gpu
