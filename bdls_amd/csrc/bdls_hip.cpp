@@ -181,6 +181,10 @@ size_t max_tables_for(size_t ns, bool reg = false) {
   return std::min<size_t>(reg ? ns : ns / 2, size_t(1) << 16);
 }
 
+// Q-table slots: one per record, two for batches small enough to run the
+// 2-lane secp256k1 ladder (launch_opts: wide > 1).
+size_t qtab_slots(size_t ns) { return ns <= 8192 ? 2 * ns : ns; }
+
 size_t work_bytes(size_t ns) {
   // 4 scalar SoA arrays (8 limbs) + 4 base-field SoA arrays (9 limbs) + status
   // + per-lane Q tables; then the key plan (fingerprint table, per-record
@@ -188,7 +192,7 @@ size_t work_bytes(size_t ns) {
   // rounded to 256 bytes.
   const size_t hc = pow2_at_least(2 * ns);
   const size_t mt = max_tables_for(ns);
-  return 4 * 32 * ns + 4 * 36 * ns + ns + (ns / 64) * 64 * bh::kQTab * bh::kQPt * 4 +
+  return 4 * 32 * ns + 4 * 36 * ns + ns + qtab_slots(ns) * bh::kQTab * bh::kQPt * 4 +
          hc * (8 + 4 + 4 + 4) + ns * 16 + 16 + mt * 8 + mt * (size_t)bh::kKTabWords * 4 +
          256 * 26;
 }
@@ -213,7 +217,7 @@ int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl, bool reg = false) {
   w->rm = (uint32_t*)take(36 * ns);
   w->r2m = (uint32_t*)take(36 * ns);
   w->st = (uint8_t*)take(ns);
-  w->qtab = (uint32_t*)take((ns / 64) * 64 * bh::kQTab * bh::kQPt * 4);
+  w->qtab = (uint32_t*)take(qtab_slots(ns) * bh::kQTab * bh::kQPt * 4);
   const size_t hc = pow2_at_least(2 * ns);
   const size_t mt = max_tables_for(ns, reg);
   pl->hc = (uint32_t)hc;

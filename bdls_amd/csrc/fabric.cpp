@@ -625,23 +625,52 @@ Ident resolve(Span ser) {
 // Long-lived cache of resolved identities (the device-side twin of the MSP's
 // deserializer cache, msp/cache/cache.go): serialized bytes -> Ident.
 using IdentP = std::shared_ptr<const Ident>;
+
+// 64-bit hash of a byte span (8 bytes per step, no copy): identities are
+// ~0.9 KB PEM certificates looked up twice or more per transaction.
+uint64_t span_hash(const uint8_t* p, size_t n) {
+  uint64_t h = 0x9e3779b97f4a7c15ull ^ n;
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t v;
+    memcpy(&v, p + i, 8);
+    h = (h ^ v) * 0xff51afd7ed558ccdull;
+    h ^= h >> 32;
+  }
+  uint64_t v = 0;
+  memcpy(&v, p + i, n - i);
+  h = (h ^ v) * 0xc4ceb9fe1a85ec53ull;
+  return h ^ (h >> 29);
+}
+
+struct IdentEntry {
+  std::string bytes;  // the serialized identity (full compare on every hit)
+  IdentP id;
+};
+
+// Long-lived cache of resolved identities (the device-side twin of the MSP's
+// deserializer cache, msp/cache/cache.go): serialized bytes -> Ident. Callers
+// hold one Session for a whole block / batch: one lock, no copies on a hit.
 struct IdentCache {
   std::mutex mu;
-  std::unordered_map<std::string, IdentP> m;
+  std::unordered_multimap<uint64_t, IdentEntry> m;
   static constexpr size_t kCap = 1 << 16;
-  IdentP get(Span ser) {
-    std::string k((const char*)ser.p, ser.n);
-    {
-      std::lock_guard<std::mutex> g(mu);
-      auto it = m.find(k);
-      if (it != m.end()) return it->second;
+  struct Session {
+    IdentCache& c;
+    std::lock_guard<std::mutex> g;
+    explicit Session(IdentCache& cc) : c(cc), g(cc.mu) {}
+    IdentP get(Span ser) {
+      const uint64_t h = span_hash(ser.p, ser.n);
+      auto r = c.m.equal_range(h);
+      for (auto it = r.first; it != r.second; ++it)
+        if (it->second.bytes.size() == ser.n && !memcmp(it->second.bytes.data(), ser.p, ser.n))
+          return it->second.id;
+      if (c.m.size() >= kCap) c.m.clear();
+      IdentP id = std::make_shared<const Ident>(resolve(ser));
+      c.m.emplace(h, IdentEntry{std::string((const char*)ser.p, ser.n), id});
+      return id;
     }
-    IdentP id = std::make_shared<const Ident>(resolve(ser));
-    std::lock_guard<std::mutex> g(mu);
-    if (m.size() >= kCap) m.clear();
-    m.emplace(std::move(k), id);
-    return id;
-  }
+  };
 };
 
 IdentCache& ident_cache() {
@@ -681,6 +710,16 @@ struct Batch {
     dst.push_back(out);
   }
   void add(SdEntry& e) { add(e.id->pub, e.sig, e.seg, e.nseg, &e.out); }
+  void reserve(size_t n, size_t msg_bytes, size_t sig_bytes) {
+    pub.reserve(64 * n);
+    sig_off.reserve(n);
+    sig_len.reserve(n);
+    msg_off.reserve(n);
+    msg_len.reserve(n);
+    dst.reserve(n);
+    msg.reserve(msg_bytes + 1);
+    sig.reserve(sig_bytes + 1);
+  }
   size_t size() const { return dst.size(); }
   int run(uint32_t flags) {
     const size_t n = size();
@@ -712,6 +751,14 @@ int verify_sets(std::vector<SdEntry>& e, const std::vector<SetRange>& sets, uint
                 bool decode_only, std::vector<uint32_t>* valid, Batch* extra) {
   Batch b;
   if (extra) b = std::move(*extra);
+  {
+    size_t bytes = 0, sig_bytes = 0;
+    for (const SdEntry& x : e) {
+      for (int k = 0; k < x.nseg; k++) bytes += x.seg[k].n;
+      sig_bytes += x.sig.n;
+    }
+    b.reserve(b.size() + e.size(), b.msg.size() + bytes, b.sig.size() + sig_bytes);
+  }
   for (const SetRange& r : sets) {
     std::vector<const std::string*> seen;
     for (size_t i = r.first; i < r.first + r.count; i++) {
@@ -778,7 +825,7 @@ struct TxRec {
 // validateEndorserTransaction). Checks that do not gate which signatures are
 // verified (CheckTxID, the proposal hash, ledger / channel state) are left to
 // the unchanged validator.
-void decode_tx(Span env_bytes, TxRec* t, std::vector<SdEntry>* ends) {
+void decode_tx(Span env_bytes, TxRec* t, std::vector<SdEntry>* ends, IdentCache::Session& ic) {
   t->end_first = ends->size();
   Envelope env;
   if (!dec_envelope(env_bytes, &env)) {
@@ -808,7 +855,7 @@ void decode_tx(Span env_bytes, TxRec* t, std::vector<SdEntry>* ends) {
   if (!env.signature.set || !env.payload.set) {
     t->status = BH_FAB_CREATOR_SIGNATURE;  // "nil arguments"
   } else {
-    t->creator = ident_cache().get(sh.creator);
+    t->creator = ic.get(sh.creator);
     if (!t->creator->ok) t->status = BH_FAB_CREATOR_IDENTITY;
     else t->creator_check = true;
   }
@@ -840,7 +887,7 @@ void decode_tx(Span env_bytes, TxRec* t, std::vector<SdEntry>* ends) {
     // SignedData{data: prp || endorser, identity: endorser, signature}
     // (validator_keylevel.go:246-260)
     SdEntry x;
-    x.id = ident_cache().get(en.endorser);
+    x.id = ic.get(en.endorser);
     x.seg[0] = ap.action.prp;
     x.seg[1] = en.endorser;
     x.nseg = 2;
@@ -1028,7 +1075,11 @@ extern "C" int bh_fabric_block_preverify(const uint8_t* block, size_t len, uint3
     return bh::host_fail(BH_E_INVALID, "block does not unmarshal (common.Block)");
   std::vector<TxRec> t(data.size());
   std::vector<SdEntry> ends;
-  for (size_t i = 0; i < data.size(); i++) decode_tx(data[i], &t[i], &ends);
+  ends.reserve(data.size() * 4);
+  {
+    IdentCache::Session ic(ident_cache());
+    for (size_t i = 0; i < data.size(); i++) decode_tx(data[i], &t[i], &ends, ic);
+  }
   *n_tx = t.size();
   *n_endorse = ends.size();
   if ((t.size() && (!txs || tx_cap < t.size())) ||
@@ -1038,6 +1089,15 @@ extern "C" int bh_fabric_block_preverify(const uint8_t* block, size_t len, uint3
   // one device batch: every creator signature and the first round of every
   // transaction's endorsement set
   Batch creators;
+  {
+    size_t bytes = 0, sig_bytes = 0;
+    for (const TxRec& x : t) {
+      bytes += x.payload.n;
+      sig_bytes += x.signature.n;
+    }
+    creators.reserve(t.size() + ends.size(), bytes + 2 * 1700 * ends.size(),
+                     sig_bytes + 80 * ends.size());
+  }
   std::vector<SetRange> sets;
   for (TxRec& x : t) {
     if (x.creator_check) creators.add(x.creator->pub, x.signature, &x.payload, 1, &x.creator_out);
@@ -1080,11 +1140,14 @@ extern "C" int bh_signature_sets_verify(const bh_sd_batch* b, size_t n, const ui
     sets.push_back(SetRange{f, l - f});
   }
   std::vector<SdEntry> e(n);
-  for (size_t i = 0; i < n; i++) {
-    e[i].id = ident_cache().get(Span{b->identity + b->identity_off[i], b->identity_len[i], true});
-    e[i].seg[0] = Span{b->data ? b->data + b->data_off[i] : nullptr, b->data_len[i], true};
-    e[i].nseg = 1;
-    e[i].sig = Span{b->sig ? b->sig + b->sig_off[i] : nullptr, b->sig_len[i], true};
+  {
+    IdentCache::Session ic(ident_cache());  // released before the device work
+    for (size_t i = 0; i < n; i++) {
+      e[i].id = ic.get(Span{b->identity + b->identity_off[i], b->identity_len[i], true});
+      e[i].seg[0] = Span{b->data ? b->data + b->data_off[i] : nullptr, b->data_len[i], true};
+      e[i].nseg = 1;
+      e[i].sig = Span{b->sig ? b->sig + b->sig_off[i] : nullptr, b->sig_len[i], true};
+    }
   }
   std::vector<uint32_t> valid;
   if (int rc = verify_sets(e, sets, verify_flags(flags), (flags & BH_FAB_F_DECODE_ONLY) != 0,
@@ -1108,6 +1171,7 @@ extern "C" int bh_envelopes_preverify(const uint8_t* envs, const uint64_t* env_o
     return bh::host_fail(BH_E_INVALID, "unknown flag");
   std::vector<SdEntry> e(n);
   std::vector<SetRange> sets;
+  std::unique_ptr<IdentCache::Session> ic(new IdentCache::Session(ident_cache()));
   for (size_t i = 0; i < n; i++) {
     status[i] = BH_FAB_OK;
     Envelope env;
@@ -1120,7 +1184,7 @@ extern "C" int bh_envelopes_preverify(const uint8_t* envs, const uint64_t* env_o
     } else if (!pl.has_header || !dec_signature_header(pl.header.signature_header, &sh)) {
       status[i] = BH_FAB_HEADER;  // "Missing Header" / GetSignatureHeaderFromBytes failed
     } else {
-      e[i].id = ident_cache().get(sh.creator);
+      e[i].id = ic->get(sh.creator);
       e[i].seg[0] = env.payload;
       e[i].nseg = 1;
       e[i].sig = env.signature;
@@ -1128,6 +1192,7 @@ extern "C" int bh_envelopes_preverify(const uint8_t* envs, const uint64_t* env_o
       sets.push_back(SetRange{i, 1});
     }
   }
+  ic.reset();  // release the cache before device work
   std::vector<uint32_t> valid;
   if (int rc = verify_sets(e, sets, verify_flags(flags), (flags & BH_FAB_F_DECODE_ONLY) != 0,
                            &valid, nullptr))
@@ -1203,6 +1268,7 @@ extern "C" int bh_block_signatures_preverify(const uint8_t* blocks, const uint64
   std::vector<SetRange> sets;
   std::vector<std::vector<uint8_t>> hdr_der(n);  // BlockHeaderBytes per block (kept alive)
   std::vector<size_t> set_of(n, SIZE_MAX);
+  std::unique_ptr<IdentCache::Session> ic(new IdentCache::Session(ident_cache()));
   for (size_t i = 0; i < n; i++) {
     res[i] = bh_blocksig_result{BH_BLK_OK, 0, 0, 0};
     Span header, metadata;
@@ -1279,7 +1345,7 @@ extern "C" int bh_block_signatures_preverify(const uint8_t* blocks, const uint64
         break;
       }
       SdEntry x;
-      x.id = ident_cache().get(sh.creator);
+      x.id = ic->get(sh.creator);
       x.seg[0] = value;
       x.seg[1] = m.sh;
       x.seg[2] = Span{hdr_der[i].data(), hdr_der[i].size(), true};
@@ -1296,6 +1362,7 @@ extern "C" int bh_block_signatures_preverify(const uint8_t* blocks, const uint64
     set_of[i] = sets.size();
     sets.push_back(SetRange{first, e.size() - first});
   }
+  ic.reset();
   *sig_total = e.size();
   if (e.size() && (!sig_reason || sig_cap < e.size()))
     return bh::host_fail(BH_E_INVALID, "sig_reason too small (see *sig_total)");

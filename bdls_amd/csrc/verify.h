@@ -741,9 +741,11 @@ BH_HD uint32_t bits6(const uint32_t v[5], uint32_t b) {
 template <class P>
 BH_HD void j_acc(J30& A, bool& a_inf, const J30& T, bool t_inf);  // below
 
+// parts: bit 0 = the k1 Q half, bit 1 = the k2 phi(Q) half (3 = all of u2 Q;
+// the 2-lane ladder runs one half per lane and adds the two results).
 template <class P>
 BH_HD void q_ladder_glv(J30& A, bool& a_inf, const Work& w, uint32_t i, uint32_t wave,
-                        uint32_t lane) {
+                        uint32_t lane, uint32_t parts = 3) {
   uint32_t u2[8], qx[9], qy[9], one[9];
   ld8(u2, w.r, i, w.ns);
   ld9(qx, w.qx, i, w.ns);
@@ -798,17 +800,21 @@ BH_HD void q_ladder_glv(J30& A, bool& a_inf, const Work& w, uint32_t i, uint32_t
       for (int d = 0; d < 5; d++) j_dbl<P>(A, A);
     uint32_t mag;
     bool neg;
-    booth5(bits6(K1, 5u * (uint32_t)win), &mag, &neg);
-    J30 T1;
-    qtab_load(T1, w.qtab, wave, mag ? mag - 1 : 0, lane);
-    if (neg != s1) f_neg<P, 64>(T1.Y, T1.Y);
-    j_acc<P>(A, a_inf, T1, mag == 0);
-    booth5(bits6(K2, 5u * (uint32_t)win), &mag, &neg);
-    J30 T2;
-    qtab_load(T2, w.qtab, wave, mag ? mag - 1 : 0, lane);
-    f_mul<P>(T2.X, T2.X, beta);  // phi: (beta X, Y, Z)
-    if (neg != s2) f_neg<P, 64>(T2.Y, T2.Y);
-    j_acc<P>(A, a_inf, T2, mag == 0);
+    if (parts & 1u) {
+      booth5(bits6(K1, 5u * (uint32_t)win), &mag, &neg);
+      J30 T1;
+      qtab_load(T1, w.qtab, wave, mag ? mag - 1 : 0, lane);
+      if (neg != s1) f_neg<P, 64>(T1.Y, T1.Y);
+      j_acc<P>(A, a_inf, T1, mag == 0);
+    }
+    if (parts & 2u) {
+      booth5(bits6(K2, 5u * (uint32_t)win), &mag, &neg);
+      J30 T2;
+      qtab_load(T2, w.qtab, wave, mag ? mag - 1 : 0, lane);
+      f_mul<P>(T2.X, T2.X, beta);  // phi: (beta X, Y, Z)
+      if (neg != s2) f_neg<P, 64>(T2.Y, T2.Y);
+      j_acc<P>(A, a_inf, T2, mag == 0);
+    }
   }
 }
 
@@ -1149,6 +1155,10 @@ BH_HD void j_acc_aff(J30& A, bool& a_inf, const uint32_t tx[9], const uint32_t t
   if (use_t) a_inf = false;
 }
 
+template <class P, int L>
+BH_HD void g_comb_part(J30& C, bool& c_inf, const uint32_t* gtab, const uint32_t u1[8],
+                       uint32_t l);  // below
+
 // Lane l's partial sum C = sum over its windows of (key-table digit points
 // + G-comb digit points).
 template <class P, int L>
@@ -1177,7 +1187,16 @@ BH_HD void keycomb_part(J30& C, bool& c_inf, const Work& w, const uint32_t* gtab
   }
   // u1 G: kGW-bit windows win = l + m L over the affine G comb
   ld8(k, w.e, i, w.ns);
-  recode_goff(v, k);
+  g_comb_part<P, L>(C, c_inf, gtab, k, l);
+}
+
+// C += the G-comb windows win = l, l + L, ... of u1 G (kGW-bit signed digits
+// from one offset addition, recode_goff).
+template <class P, int L>
+BH_HD void g_comb_part(J30& C, bool& c_inf, const uint32_t* gtab, const uint32_t u1[8],
+                       uint32_t l) {
+  uint32_t v[9], sv[9];
+  recode_goff(v, u1);
   shr288(sv, v, (uint32_t)kGW * l);
   uint32_t one[9];
   f_const(one, P::r1);
@@ -1198,6 +1217,18 @@ BH_HD void keycomb_part(J30& C, bool& c_inf, const Work& w, const uint32_t* gtab
       j_acc_aff<P>(C, c_inf, tx, ty, one, mag == 0);
     }
   }
+}
+
+// One lane's half of the 2-lane secp256k1 ladder (small, latency-bound
+// batches): lane `part` computes k1 Q (part 0) or k2 phi(Q) (part 1) and every
+// other G-comb window; the caller adds the two halves and runs finish_check.
+template <class P>
+BH_HD void ladder2_part(J30& C, bool& c_inf, const Work& w, const uint32_t* gtab, uint32_t i,
+                        uint32_t wave, uint32_t lane, uint32_t part) {
+  q_ladder_glv<P>(C, c_inf, w, i, wave, lane, 1u << part);
+  uint32_t u1[8];
+  ld8(u1, w.e, i, w.ns);
+  g_comb_part<P, 2>(C, c_inf, gtab, u1, part);
 }
 
 }  // namespace bh

@@ -370,6 +370,38 @@ __global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
   if (active) reason[i] = ok ? R_OK : R_MATH;
 }
 
+// secp256k1 ladder on 2 lanes per record (small, latency-bound batches): lane
+// pair (2j, 2j+1) takes the k1 Q / k2 phi(Q) halves of the GLV split and
+// alternate G-comb windows (verify.h ladder2_part); lane 0 adds the halves.
+// Each lane owns a Q-table slot (the workspace reserves 2 per record for
+// batches this small). Waves past the list length exit whole.
+template <class P>
+__global__ __launch_bounds__(256) void k_ladder2(Work w, Plan pl,
+                                                 const uint32_t* __restrict__ gtab,
+                                                 uint8_t* __restrict__ reason) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j0 = gid >> 1, part = gid & 1u;
+  const uint32_t cnt = pl.counters[1];
+  if ((j0 & ~31u) >= cnt) return;
+  const bool active = j0 < cnt;
+  const uint32_t i = pl.ladder_list[active ? j0 : cnt - 1];
+  J30 C;
+  bool c_inf;
+  ladder2_part<P>(C, c_inf, w, gtab, i, gid >> 6, threadIdx.x & 63u, part);
+  J30 T;
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    T.X[q] = __shfl_xor(C.X[q], 1, 64);
+    T.Y[q] = __shfl_xor(C.Y[q], 1, 64);
+    T.Z[q] = __shfl_xor(C.Z[q], 1, 64);
+  }
+  const bool t_inf = __shfl_xor((int)c_inf, 1, 64) != 0;
+  if (part != 0) return;
+  j_acc<P>(C, c_inf, T, t_inf);
+  const bool ok = finish_check<P>(w, i, C, c_inf, C, true);
+  if (active) reason[i] = ok ? R_OK : R_MATH;
+}
+
 // Publish registry tables built in this batch (after the builds completed).
 __global__ __launch_bounds__(256) void k_reg_publish(Work w, Plan pl, KeyReg g) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -611,8 +643,20 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   const uint32_t parts = pl.max_tables <= kSplitBuildMax ? 2u : 1u;
   const uint32_t tab_blocks = (parts * pl.max_tables + 255) / 256;
   // from here on only plc (rec_slot consumed by the sort)
-  hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x), blk, 0, s, w, plc, g, gtab,
-                     reason, tab_blocks, parts);
+  if constexpr (!P::a_is_minus3) {
+    if (o.wide > 1) {  // small secp256k1 batch: 2-lane GLV ladder
+      hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, plc, g, gtab,
+                         reason, tab_blocks, parts);
+      hipLaunchKernelGGL((k_ladder2<P>), dim3((2 * n + 255) / 256), blk, 0, s, w, plc, gtab,
+                         reason);
+    } else {
+      hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x), blk, 0, s, w, plc, g,
+                         gtab, reason, tab_blocks, parts);
+    }
+  } else {
+    hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x), blk, 0, s, w, plc, g, gtab,
+                       reason, tab_blocks, parts);
+  }
   REC(4);
   if (o.keep) hipLaunchKernelGGL(k_reg_publish, dim3(tab_blocks), blk, 0, s, w, plc, g);
   REC(5);

@@ -78,8 +78,9 @@ def parse(argv=None):
     ap.add_argument("--n", type=int, default=1 << 20, help="config 2: records per GPU")
     ap.add_argument("--n-total", type=int, default=CONFIG5_TOTAL,
                     help="config 5: records of the one batch split over all GPUs")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
-                    help="2/5: throughput; 3 (block) / 4 (BDLS round): latency")
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
+                    help="1: host-CPU reference proxy; 2/5: throughput; 3 (block) / 4 (BDLS "
+                         "round): latency")
     ap.add_argument("--curve", type=int, default=1, help="config 4: 1 secp256k1 (as wired), 0 P-256")
     ap.add_argument("--validators", type=int, default=100, help="config 4")
     ap.add_argument("--nkeys", type=int, default=65536)
@@ -703,6 +704,72 @@ def bench_throughput(a, rank, world, local):
     return 0 if parity_ok else 3
 
 
+def bench_config1(a):
+    """BASELINE config 1: 10k synthetic P-256 verifies through bccsp/sw on the
+    host CPU (go test -bench, plumbing, no GPU). No Go toolchain exists here or
+    on the GPU box, so the measured figure is the labelled proxy SURVEY 8(d)
+    prescribes: oracle/orc.c (Fabric's DER + low-S rules in C, the ECDSA core in
+    OpenSSL's P-256 assembly -- the class of Go's crypto/internal/nistec asm)
+    with every usable CPU and with os.cpu_count() threads. 10,000 records,
+    1,000 keys, SHA-256 digests of 256-byte messages, all valid, seed 1. The
+    same batch through the engine is reported beside it (one bh_verify call,
+    host buffers, digests given as in bccsp.Verify)."""
+    import hashlib
+    from bdls_amd import _lib, workload
+    from oracle import orc
+    w = workload.generate(10_000, 1_000, 256, 0, seed=1)
+    dg = np.frombuffer(b"".join(hashlib.sha256(bytes(w.msg[o:o + l])).digest()
+                                for o, l in zip(w.msg_off, w.msg_len)), np.uint8)
+    doff = np.arange(w.n, dtype=np.uint64) * 32
+    dlen = np.full(w.n, 32, np.uint32)
+    cpus = host_cpus()
+    usable = int(min(cpus.get("affinity", cpus["nproc"]),
+                     cpus.get("cgroup_quota_cpus", cpus["nproc"]))) or 1
+    runs = {}
+    for threads in sorted({1, usable, cpus["nproc"]}):
+        best = 0.0
+        for _ in range(max(1, a.steps)):
+            t = time.perf_counter()
+            got = orc.batch_verify(w.pub.reshape(-1, 64), dg, doff, dlen, w.sig, w.sig_off,
+                                   w.sig_len, fused=False, nthreads=threads)
+            best = max(best, w.n / (time.perf_counter() - t))
+        assert (got == 0).all()
+        runs[str(threads)] = round(best, 1)
+    top = max(runs, key=lambda k: runs[k])
+    out = {
+        "metric": "P-256 ECDSA verifies/sec, host CPU (bccsp/sw proxy)",
+        "value": runs[top], "unit": "verifies/s", "n_gpus": 0, "steps": a.steps,
+        "warmup": 0, "ms_per_step": round(w.n / runs[top] * 1e3, 3), "higher_is_better": True,
+        "scaling": "none", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (seeded P-256 keys/signatures, workload/gen.c)",
+        "config": {"workload": "BASELINE config 1: 10,000 P-256 records, 1,000 keys, SHA-256 "
+                               "digests of 256 B messages, all valid, seed 1",
+                   "kind": "port (no Go toolchain: OpenSSL-backed restatement of "
+                           "bccsp/sw Verify, labelled proxy per SURVEY 8(d))"},
+        "cpu": {"threads": int(top), "by_threads": runs, "host_cpus": cpus},
+        "parity": True,
+    }
+    try:  # the same 10k records through the engine (digest mode), if a GPU is there
+        _lib.check(_lib.lib().bh_init(1, 0))
+        b = _lib.BhBatch(w.pub.ctypes.data, w.sig.ctypes.data, w.sig_off.ctypes.data,
+                         w.sig_len.ctypes.data, dg.ctypes.data, doff.ctypes.data, dlen.ctypes.data)
+        bm = np.zeros((w.n + 7) // 8, np.uint8)
+        rs = np.zeros(w.n, np.uint8)
+        ms = []
+        for _ in range(max(3, a.steps)):
+            t = time.perf_counter()
+            _lib.check(_lib.lib().bh_verify(0, ctypes.byref(b), w.n, 0, bm.ctypes.data,
+                                            rs.ctypes.data))
+            ms.append((time.perf_counter() - t) * 1e3)
+        out["gpu_same_batch"] = {"p50_ms": round(percentile(ms, 50), 4),
+                                 "verifies_per_s": round(w.n / percentile(ms, 50) * 1e3, 1),
+                                 "parity": bool((rs == 0).all())}
+    except _lib.EngineError as e:
+        out["gpu_same_batch"] = {"skipped": str(e)}
+    print(json.dumps(out), flush=True)
+    return 0
+
+
 def dry_run(a, rank, world):
     """Launcher + rank plumbing without a GPU (tests/test_bench_launch.py)."""
     from bdls_amd import dist
@@ -721,6 +788,8 @@ def dry_run(a, rank, world):
 def main(argv=None):
     a = parse(argv)
     from bdls_amd import dist
+    if a.config == 1:
+        return bench_config1(a)
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(a.gpus)
     rank, world, local = dist.env_rank()

@@ -71,7 +71,7 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
                    uint32_t* n_comb) {
   const uint32_t* gtab = gtab_for<P>();
   const uint32_t ns = (n + 63) & ~63u;
-  std::vector<uint32_t> buf((size_t)9 * 9 * ns + (size_t)(ns / 64) * 64 * kQTab * kQPt);
+  std::vector<uint32_t> buf((size_t)9 * 9 * ns + (size_t)2 * ns * kQTab * kQPt);
   std::vector<uint8_t> st(ns);
   Work w;
   w.ns = ns;
@@ -136,6 +136,15 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
       }
       ok = keycomb_any<P>(w, gtab, i, tables[tab_of[r]].data());
       combs++;
+    } else if (!P::a_is_minus3 && g_wide > 1) {
+      // the 2-lane secp256k1 ladder (verify_kernels.hip k_ladder2): the two
+      // GLV halves in two Q-table slots, added as the kernel's lane 0 does
+      J30 C0, C1;
+      bool i0, i1;
+      ladder2_part<P>(C0, i0, w, gtab, i, (2 * i) / 64, (2 * i) % 64, 0);
+      ladder2_part<P>(C1, i1, w, gtab, i, (2 * i + 1) / 64, (2 * i + 1) % 64, 1);
+      j_acc<P>(C0, i0, C1, i1);
+      ok = finish_check<P>(w, i, C0, i0, C0, true);
     } else {
       ok = stage_ladder<P>(w, gtab, i, i / 64, i % 64);
     }

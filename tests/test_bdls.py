@@ -132,7 +132,7 @@ def _k1_edge_records():
     return recs
 
 
-@pytest.mark.parametrize("min_uses,wide", [(1, 1), (1000, 1), (1, 16), (1, 4)])
+@pytest.mark.parametrize("min_uses,wide", [(1, 1), (1000, 1), (1, 16), (1, 4), (1000, 4)])
 def test_k1_curve_edges_hostsim(hs, min_uses, wide):
     recs = _k1_edge_records()
     pub = np.frombuffer(b"".join(qx.to_bytes(32, "big") + qy.to_bytes(32, "big")
