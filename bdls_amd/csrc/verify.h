@@ -881,43 +881,46 @@ BH_HD void ktab_load(J30& P, const uint32_t* tab, uint32_t win, uint32_t j) {
   }
 }
 
-// Build one key table from the canonical Montgomery (qx, qy) of record `rec`,
-// by one lane (parts = 1) or two (parts = 2: part 0 = windows [0, kKSplit),
-// part 1 = windows [kKSplit, 65) after 4 kKSplit doublings of Q). kKSplit
-// balances the two serial chains (88 F_p ops per window vs 8 per doubling:
-// 3,520 vs 3,480 instead of 5,720). Two lanes only pay when a few tables are
-// built (key registration: latency-bound); with tens of thousands of tables
-// the +18% work costs more than the shorter chain saves (measured at config
-// 2: 3.34 -> 4.64 ms), so verify batches use one lane per table.
-constexpr uint32_t kKSplit = 40;
+// Two-wave table build (k_ktab_ladder build blocks, round 2). One build lane
+// per table left one wave per SIMD at 65,536 tables, with nothing to hide the
+// v_mad_u64_u32 dependency latency (0.57 of the counter-based VALU rate). The
+// work of a window is split between two waves of a workgroup, 64 tables per
+// wave pair, synchronised once per window:
+//   chain wave : B -> 2B -> 4B -> 8B -> 16B (next base) and 5B = 4B + B
+//                (4 doublings + 1 addition; stores B, 2B, 4B, 5B, 8B)
+//   side wave  : one window behind, loads B and 2B back and makes
+//                3B = 2B + B, 6B = 2 (3B), 7B = 6B + B (2 additions + 1 doubling)
+// Same points and total work as one lane doing both (round 1's ktab_build:
+// a two-lane split by window ranges cost +18 % doublings and was slower at
+// 65,536 tables), twice the waves. Entry j of window w = (j+1) 16^w Q.
 template <class P>
-BH_HD void ktab_build(uint32_t* tab, const Work& w, uint32_t rec, uint32_t part, uint32_t parts) {
-  J30 B, E2, E3, E4, T;
-  ld9(B.X, w.qx, rec, w.ns);
-  ld9(B.Y, w.qy, rec, w.ns);
-  f_const(B.Z, P::r1);
+BH_HD void ktab_chain_step(J30& B, uint32_t* tab, uint32_t win) {
+  J30 E2, E4, T;
   bool same;
-  const uint32_t w0 = part ? kKSplit : 0u;
-  const uint32_t w1 = (part || parts == 1) ? (uint32_t)kKWin : kKSplit;
-  for (uint32_t d = 0; d < 4u * w0; d++) j_dbl<P>(B, B);
-  for (uint32_t win = w0; win < w1; win++) {
-    ktab_store(tab, win, 0, B);                 // 1 B
-    j_dbl<P>(E2, B);
-    ktab_store(tab, win, 1, E2);                // 2 B
-    j_add<P>(E3, E2, B, &same);
-    ktab_store(tab, win, 2, E3);                // 3 B
-    j_dbl<P>(E4, E2);
-    ktab_store(tab, win, 3, E4);                // 4 B
-    j_add<P>(T, E4, B, &same);
-    ktab_store(tab, win, 4, T);                 // 5 B
-    j_dbl<P>(T, E3);
-    ktab_store(tab, win, 5, T);                 // 6 B
-    j_add<P>(T, T, B, &same);
-    ktab_store(tab, win, 6, T);                 // 7 B
-    j_dbl<P>(T, E4);
-    ktab_store(tab, win, 7, T);                 // 8 B
-    j_dbl<P>(B, T);                             // next window base: 16 B
-  }
+  ktab_store(tab, win, 0, B);          // 1 B
+  j_dbl<P>(E2, B);
+  ktab_store(tab, win, 1, E2);         // 2 B
+  j_dbl<P>(E4, E2);
+  ktab_store(tab, win, 3, E4);         // 4 B
+  j_add<P>(T, E4, B, &same);
+  ktab_store(tab, win, 4, T);          // 5 B
+  j_dbl<P>(T, E4);
+  ktab_store(tab, win, 7, T);          // 8 B
+  j_dbl<P>(B, T);                      // 16 B: the next window's base
+}
+
+template <class P>
+BH_HD void ktab_side_step(uint32_t* tab, uint32_t win) {
+  J30 B, E2, T;
+  bool same;
+  ktab_load(B, tab, win, 0);
+  ktab_load(E2, tab, win, 1);
+  j_add<P>(T, E2, B, &same);
+  ktab_store(tab, win, 2, T);          // 3 B
+  j_dbl<P>(T, T);
+  ktab_store(tab, win, 5, T);          // 6 B
+  j_add<P>(T, T, B, &same);
+  ktab_store(tab, win, 6, T);          // 7 B
 }
 
 // u2 Q from a key table: 4-bit signed windows (least significant first).

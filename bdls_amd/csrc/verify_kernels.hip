@@ -309,55 +309,91 @@ __global__ __launch_bounds__(256) void k_key_plan(Work w, Plan pl, KeyReg g, uin
 }
 
 // Route every record: failed prep -> reason now; key table -> comb list;
-// otherwise -> ladder list.
-__global__ __launch_bounds__(256) void k_split(Work w, Plan pl, uint32_t n,
-                                               uint8_t* __restrict__ reason) {
+// otherwise -> ladder list. List slots come from one atomic per 1024-thread
+// block and list: same-address atomics serialise in L2, so a per-wave (let
+// alone per-record) atomic costs more than the rest of the routing.
+constexpr uint32_t kSplitBlock = 1024;
+__global__ __launch_bounds__(kSplitBlock) void k_split(Work w, Plan pl, uint32_t n,
+                                                       uint8_t* __restrict__ reason) {
+  __shared__ uint32_t wave_cnt[2][kSplitBlock / 64];
+  __shared__ uint32_t block_base[2];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint8_t st = w.st[i] & 0x7fu;
-  if (st != R_OK) {
-    reason[i] = st;
-    return;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  int list = -1;  // 0 comb, 1 ladder, -1 none
+  if (i < n) {
+    const uint8_t st = w.st[i] & 0x7fu;
+    if (st != R_OK) {
+      reason[i] = st;
+    } else {
+      uint32_t t = pl.rec_tab[i];
+      if (t == kNone) {
+        const uint32_t p = pl.rec_slot[i];
+        if (p != kNone) t = pl.slot_tab[p];
+        pl.rec_tab[i] = t;
+      }
+      list = t != kNone ? 0 : 1;
+    }
   }
-  uint32_t t = pl.rec_tab[i];
-  if (t == kNone) {
-    const uint32_t p = pl.rec_slot[i];
-    if (p != kNone) t = pl.slot_tab[p];
-    pl.rec_tab[i] = t;
+  const uint64_t m0 = __ballot(list == 0), m1 = __ballot(list == 1);
+  if (lane == 0) {
+    wave_cnt[0][wv] = (uint32_t)__popcll(m0);
+    wave_cnt[1][wv] = (uint32_t)__popcll(m1);
   }
-  // one atomic per wave and list: lanes take consecutive slots by their rank
-  // among the wave's lanes bound for the same list (contended per-record
-  // atomics on two counters cost more than the rest of the routing)
-  const bool comb = t != kNone;
-  const uint64_t m_comb = __ballot(comb), m_lad = __ballot(!comb);
-  const uint32_t lane = threadIdx.x & 63u;
+  __syncthreads();
+  if (threadIdx.x < 2) {  // exclusive prefix over the block's waves, one atomic per list
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < kSplitBlock / 64; k++) {
+      const uint32_t c = wave_cnt[threadIdx.x][k];
+      wave_cnt[threadIdx.x][k] = sum;
+      sum += c;
+    }
+    block_base[threadIdx.x] = sum ? atomicAdd(&pl.counters[threadIdx.x], sum) : 0u;
+  }
+  __syncthreads();
+  if (list < 0) return;
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  const uint32_t leader_c = __ffsll((unsigned long long)m_comb) - 1;
-  const uint32_t leader_l = __ffsll((unsigned long long)m_lad) - 1;
-  uint32_t base_c = 0, base_l = 0;
-  if (comb && lane == leader_c) base_c = atomicAdd(&pl.counters[0], (uint32_t)__popcll(m_comb));
-  if (!comb && lane == leader_l) base_l = atomicAdd(&pl.counters[1], (uint32_t)__popcll(m_lad));
-  base_c = __shfl(base_c, (int)leader_c, 64);
-  base_l = __shfl(base_l, (int)leader_l, 64);
-  if (comb) pl.comb_list[base_c + __popcll(m_comb & below)] = i;
-  else pl.ladder_list[base_l + __popcll(m_lad & below)] = i;
+  const uint64_t m = list == 0 ? m0 : m1;
+  const uint32_t slot = block_base[list] + wave_cnt[list][wv] + (uint32_t)__popcll(m & below);
+  if (list == 0) pl.comb_list[slot] = i;
+  else pl.ladder_list[slot] = i;
 }
 
-// Blocks [0, tab_blocks) build key tables (`parts` lanes per table); the rest run
-// the ladder list. Ladder waves past the list length exit whole (the Q-table
-// scratch slot is the list position).
+// Blocks [0, tab_blocks) build key tables, 128 per block: waves 2q / 2q+1
+// are the chain / side waves of tables [128 b + 64 q, +64) (verify.h
+// ktab_chain_step / ktab_side_step), one __syncthreads per window; the rest
+// run the ladder list. Ladder waves past the list length exit whole (the
+// Q-table scratch slot is the list position).
+constexpr uint32_t kBuildPerBlock = 128;
 template <class P>
 __global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
                                                      const uint32_t* __restrict__ gtab,
                                                      uint8_t* __restrict__ reason,
-                                                     uint32_t tab_blocks, uint32_t parts) {
+                                                     uint32_t tab_blocks) {
   if (blockIdx.x < tab_blocks) {
-    const uint32_t t2 = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t t = t2 / parts;
     const uint32_t nt = min(pl.counters[2], pl.max_tables);
-    if (t >= nt) return;
-    ktab_build<P>(const_cast<uint32_t*>(tab_ptr(pl, g, pl.tab_dst[t])), w, pl.tab_rec[t],
-                  t2 % parts, parts);
+    const uint32_t base = blockIdx.x * kBuildPerBlock;
+    if (base >= nt) return;  // uniform over the block: no barrier is skipped
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t role = wv & 1u, t = base + (wv >> 1) * 64u + lane;
+    const bool active = t < nt;
+    uint32_t* tab = active ? const_cast<uint32_t*>(tab_ptr(pl, g, pl.tab_dst[t])) : nullptr;
+    J30 B;
+    if (role == 0 && active) {
+      const uint32_t rec = pl.tab_rec[t];
+      ld9(B.X, w.qx, rec, w.ns);
+      ld9(B.Y, w.qy, rec, w.ns);
+      f_const(B.Z, P::r1);
+    }
+    for (uint32_t step = 0; step <= (uint32_t)kKWin; step++) {
+      if (active) {
+        if (role == 0) {
+          if (step < (uint32_t)kKWin) ktab_chain_step<P>(B, tab, step);
+        } else if (step > 0) {
+          ktab_side_step<P>(tab, step - 1);
+        }
+      }
+      __syncthreads();  // window `step`'s B, 2B are visible to the side wave
+    }
     return;
   }
   const uint32_t j0 = (blockIdx.x - tab_blocks) * blockDim.x + threadIdx.x;
@@ -603,9 +639,6 @@ static hipError_t comb_sort(const Plan& pl, const KeyReg& g, uint32_t n, hipStre
   return hipSuccess;
 }
 
-// Table builds run two lanes per table when at most this many can be built
-// (far below one wave per SIMD: latency-bound), else one (see ktab_build).
-constexpr uint32_t kSplitBuildMax = 8192;
 
 // Full launch sequence. ev (optional, 7 events) brackets: prep | inv | plan
 // (lookup + dedup + split) | key tables + ladder | publish | key comb + bitmap.
@@ -632,7 +665,8 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   launch_key_count(w, pl, key_bytes(in), n, grd, blk, s);
   hipLaunchKernelGGL(k_key_plan, grd, blk, 0, s, w, pl, g, n, o.min_uses, o.min_batch,
                      o.keep ? 1u : 0u, 0u);
-  hipLaunchKernelGGL(k_split, grd, blk, 0, s, w, pl, n, reason);
+  hipLaunchKernelGGL(k_split, dim3((n + kSplitBlock - 1) / kSplitBlock), dim3(kSplitBlock), 0, s,
+                     w, pl, n, reason);
   Plan plc;
   if (o.wide <= 1) {
     if ((e = comb_sort(pl, g, n, s, &plc))) return e;
@@ -640,25 +674,25 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
     plc = pl;
   }
   REC(3);
-  const uint32_t parts = pl.max_tables <= kSplitBuildMax ? 2u : 1u;
-  const uint32_t tab_blocks = (parts * pl.max_tables + 255) / 256;
+  const uint32_t tab_blocks = (pl.max_tables + kBuildPerBlock - 1) / kBuildPerBlock;
   // from here on only plc (rec_slot consumed by the sort)
   if constexpr (!P::a_is_minus3) {
     if (o.wide > 1) {  // small secp256k1 batch: 2-lane GLV ladder
       hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, plc, g, gtab,
-                         reason, tab_blocks, parts);
+                         reason, tab_blocks);
       hipLaunchKernelGGL((k_ladder2<P>), dim3((2 * n + 255) / 256), blk, 0, s, w, plc, gtab,
                          reason);
     } else {
       hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x), blk, 0, s, w, plc, g,
-                         gtab, reason, tab_blocks, parts);
+                         gtab, reason, tab_blocks);
     }
   } else {
     hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x), blk, 0, s, w, plc, g, gtab,
-                       reason, tab_blocks, parts);
+                       reason, tab_blocks);
   }
   REC(4);
-  if (o.keep) hipLaunchKernelGGL(k_reg_publish, dim3(tab_blocks), blk, 0, s, w, plc, g);
+  if (o.keep)
+    hipLaunchKernelGGL(k_reg_publish, dim3((pl.max_tables + 255) / 256), blk, 0, s, w, plc, g);
   REC(5);
   switch (o.wide) {
     case 4:
@@ -709,11 +743,10 @@ static hipError_t reg_seq(const uint8_t* pub, const Work& w, const Plan& pl, con
   hipLaunchKernelGGL(k_key_insert, grd, blk, 0, s, w, pl, g, n);
   launch_key_count(w, pl, pub, n, grd, blk, s);
   hipLaunchKernelGGL(k_key_plan, grd, blk, 0, s, w, pl, g, n, 1u, 0u, 1u, 1u);
-  const uint32_t parts = pl.max_tables <= kSplitBuildMax ? 2u : 1u;
-  const uint32_t tab_blocks = (parts * pl.max_tables + 255) / 256;
+  const uint32_t tab_blocks = (pl.max_tables + kBuildPerBlock - 1) / kBuildPerBlock;
   hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, pl, g,
-                     (const uint32_t*)nullptr, (uint8_t*)nullptr, tab_blocks, parts);
-  hipLaunchKernelGGL(k_reg_publish, dim3(tab_blocks), blk, 0, s, w, pl, g);
+                     (const uint32_t*)nullptr, (uint8_t*)nullptr, tab_blocks);
+  hipLaunchKernelGGL(k_reg_publish, dim3((pl.max_tables + 255) / 256), blk, 0, s, w, pl, g);
   hipLaunchKernelGGL(k_reg_status, grd, blk, 0, s, w, pl, n, status);
   return hipGetLastError();
 }

@@ -127,11 +127,15 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
       if (tab_of[r] == kNone) {
         tab_of[r] = (uint32_t)tables.size();
         tables.emplace_back(kKTabWords);
-        if (r & 1) {  // both build shapes (the device picks per launch)
-          ktab_build<P>(tables.back().data(), w, r, 0, 2);
-          ktab_build<P>(tables.back().data(), w, r, 1, 2);
-        } else {
-          ktab_build<P>(tables.back().data(), w, r, 0, 1);
+        // the device's two-wave schedule: chain window s, side window s - 1
+        uint32_t* tab = tables.back().data();
+        J30 B;
+        ld9(B.X, w.qx, r, w.ns);
+        ld9(B.Y, w.qy, r, w.ns);
+        f_const(B.Z, P::r1);
+        for (uint32_t step = 0; step <= (uint32_t)kKWin; step++) {
+          if (step < (uint32_t)kKWin) ktab_chain_step<P>(B, tab, step);
+          if (step > 0) ktab_side_step<P>(tab, step - 1);
         }
       }
       ok = keycomb_any<P>(w, gtab, i, tables[tab_of[r]].data());
