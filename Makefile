@@ -42,6 +42,15 @@ tests/native/build/libhostsim.so: tests/native/hostsim.cpp $(HDRS)
 	@mkdir -p tests/native/build
 	$(CLANGXX) -O2 -std=c++17 -shared -fPIC -o $@ $<
 
+# build-kernel experiments (profiles/r02/exp_build): not part of `all`
+EXP_VARIANTS := base:
+exp:
+	@mkdir -p build/exp
+	@for v in $(EXP_VARIANTS); do n=$${v%%:*}; f=$$(echo $${v#*:} | tr '+' ' '); \
+	  $(HIPCC) $(HIPFLAGS) $$f -c $(CSRC)/verify_kernels.hip -o build/exp/vk_$$n.o && \
+	  $(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/exp/libbdlship_$$n.so build/exp/vk_$$n.o \
+	    $(LIB)/bdls_hip.o $(LIB)/bdls_msg.o $(LIB)/fabric.o -lpthread || exit 1; done
+
 clean:
 	rm -rf $(LIB) tests/native/build
 	$(MAKE) -C oracle clean

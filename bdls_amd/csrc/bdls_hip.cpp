@@ -193,8 +193,9 @@ size_t work_bytes(size_t ns) {
   const size_t hc = pow2_at_least(2 * ns);
   const size_t mt = max_tables_for(ns);
   return 4 * 32 * ns + 4 * 36 * ns + ns + qtab_slots(ns) * bh::kQTab * bh::kQPt * 4 +
+         bh::kGPartWords * 4 * ns +
          hc * (8 + 4 + 4 + 4) + ns * 16 + 16 + mt * 8 + mt * (size_t)bh::kKTabWords * 4 +
-         256 * 26;
+         256 * 27;
 }
 
 int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl, bool reg = false) {
@@ -218,6 +219,7 @@ int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl, bool reg = false) {
   w->r2m = (uint32_t*)take(36 * ns);
   w->st = (uint8_t*)take(ns);
   w->qtab = (uint32_t*)take(qtab_slots(ns) * bh::kQTab * bh::kQPt * 4);
+  w->gpart = (uint32_t*)take(bh::kGPartWords * 4 * ns);
   const size_t hc = pow2_at_least(2 * ns);
   const size_t mt = max_tables_for(ns, reg);
   pl->hc = (uint32_t)hc;

@@ -89,6 +89,89 @@ BH_HD void j_dbl(J30& r, const J30& p) {
   }
 }
 
+// Co-Z doubling (DBLU): r = 2p and pp = p rescaled to r's Z, i.e.
+// (X (2Y)^2, Y (2Y)^3, 2YZ) = (4 X Y^2, 8 Y^4, Z3), both intermediates of the
+// doubling. Requires beta(X) <= 63, beta(Y) + beta(Z) <= 128. Output r as
+// j_dbl (a = -3: (34, 34, 34); a = 0: (34, 34, 4)); pp beta (8, 16) / (2, 16).
+template <class F>
+BH_HD void j_dblu(J30& r, J30& pp, const J30& p) {
+  if constexpr (F::a_is_minus3) {
+    uint32_t delta[9], gamma[9], bt[9], t0[9], t1[9], u[9], alpha[9];
+    f_sqr<F>(delta, p.Z);                 // [b2]
+    f_sqr<F>(gamma, p.Y);                 // [b2]
+    f_mul<F>(bt, p.X, gamma);             // [b2]
+    f_sub<F, 32>(t0, p.X, delta);         // [bX+32]
+    f_add(t1, p.X, delta);                // [bX+2]
+    f_mul<F>(u, t0, t1);                  // [b2]
+    f_mulc<3>(alpha, u);                  // [b6]
+    f_add(t0, p.Y, p.Z);                  // [bY+bZ]
+    f_sqr<F>(t0, t0);                     // [b2]
+    f_add(t1, gamma, delta);              // [b4]
+    f_sub<F, 32>(r.Z, t0, t1);            // [b34]  2YZ
+    f_sqr<F>(u, alpha);                   // [b2]
+    f_mulc<8>(t0, bt);                    // [b16]
+    f_sub<F, 32>(r.X, u, t0);             // [b34]
+    f_mulc<4>(pp.X, bt);                  // [b8]   4 X Y^2
+    f_mulc<12>(t0, bt);                   // [b24]
+    f_sub<F, 32>(t0, t0, u);              // [b56]
+    f_mul<F>(t0, alpha, t0);              // [b2]
+    f_sqr<F>(gamma, gamma);               // [b2]
+    f_mulc<8>(pp.Y, gamma);               // [b16]  8 Y^4
+    f_sub<F, 32>(r.Y, t0, pp.Y);          // [b34]
+    f_copy(pp.Z, r.Z);
+  } else {
+    uint32_t A[9], B[9], Cc[9], D[9], E[9], t[9], t2[9];
+    f_sqr<F>(A, p.X);                     // [b2]
+    f_sqr<F>(B, p.Y);                     // [b2]
+    f_mul<F>(t, p.Y, p.Z);                // [b2]
+    f_sqr<F>(Cc, B);                      // [b2]
+    f_add(t2, p.X, B);                    // [bX+2]
+    f_sqr<F>(t2, t2);                     // [b2]
+    f_mulc<2>(r.Z, t);                    // [b4]   2YZ
+    f_add(t, A, Cc);                      // [b4]
+    f_sub<F, 32>(t2, t2, t);              // [b34]
+    f_mulc<2>(D, t2);                     // [b68]  D = 4 X Y^2
+    f_reduce<F>(D, D);                    // [b1]
+    f_copy(pp.X, D);                      // [b1]
+    f_mulc<3>(E, A);                      // [b6]
+    f_sqr<F>(t, E);                       // [b2]   F = E^2
+    f_mulc<3>(t2, D);                     // [b3]
+    f_sub<F, 32>(t2, t2, t);              // [b35]  3D - F
+    f_mulc<2>(D, D);                      // [b2]
+    f_sub<F, 32>(r.X, t, D);              // [b34]  X3 = F - 2D
+    f_mul<F>(t, E, t2);                   // [b2]   6*35
+    f_mulc<8>(pp.Y, Cc);                  // [b16]  8 Y^4
+    f_sub<F, 32>(r.Y, t, pp.Y);           // [b34]
+    f_copy(pp.Z, r.Z);
+  }
+}
+
+// Co-Z addition (ZADDU, Meloni 2007): p, q share Z; r = p + q and p is
+// rescaled in place to r's Z (5M + 2S instead of 12M + 4S). Requires
+// beta(X1), beta(Y1) <= 64, beta(X2), beta(Y2) <= 63, beta(Z) <= 34.
+// Output r beta (34, 34, 2), p beta (2, 2, 2). Incomplete: p = +-q is not
+// detected (callers guarantee it cannot happen).
+template <class F>
+BH_HD void j_zaddu(J30& r, J30& p, const J30& q) {
+  uint32_t t1[9], c[9], w1[9], w2[9], t2[9], d[9], t3[9];
+  f_sub<F, 64>(t1, p.X, q.X);             // [b128]
+  f_sqr<F>(c, t1);                        // [b2]   C = (X1 - X2)^2
+  f_mul<F>(w1, p.X, c);                   // [b2]   W1 = X1 C
+  f_mul<F>(w2, q.X, c);                   // [b2]   W2 = X2 C
+  f_sub<F, 64>(t2, p.Y, q.Y);             // [b128]
+  f_sqr<F>(d, t2);                        // [b2]   D = (Y1 - Y2)^2
+  f_sub<F, 32>(t3, w1, w2);               // [b34]
+  f_mul<F>(p.Y, p.Y, t3);                 // [b2]   A1 = Y1 (W1 - W2)
+  f_add(t3, w1, w2);                      // [b4]
+  f_sub<F, 32>(r.X, d, t3);               // [b34]  X3 = D - W1 - W2
+  f_sub<F, 64>(t3, w1, r.X);              // [b66]
+  f_mul<F>(t3, t2, t3);                   // [b2]   128*66
+  f_sub<F, 32>(r.Y, t3, p.Y);             // [b34]  Y3 = (Y1 - Y2)(W1 - X3) - A1
+  f_mul<F>(r.Z, p.Z, t1);                 // [b2]   Z3 = Z (X1 - X2): 34*128
+  f_copy(p.X, w1);                        // [b2]
+  f_copy(p.Z, r.Z);
+}
+
 // r = p + q (Jacobian, neither at infinity). Requires beta <= 63 on X1, Y1,
 // X2, Y2 and beta <= 34 on Z1, Z2... (products below stay <= 16384).
 // Output beta (34, 34, 2). Returns true iff x(p) == x(q) (degenerate); then r

@@ -54,17 +54,17 @@ BH_HD void f_const(uint32_t r[9], const C& c) {
 // (critical path ~2 instructions per column). Column bound: <= 9 products
 // < 2^60 plus reduction terms < 2^60 + 2^46 + 2^42 + 2^36 and the carry, < 2^64.
 // c += m * k as ONE v_mad_u64_u32. For power-of-two k hipcc otherwise emits a
-// 64-bit shift of the whole column plus two masks and an add (4 instructions).
-// k must be wave-uniform (an SGPR or an inline constant); the carry-out goes to
-// VCC, which is declared clobbered.
+// 64-bit shift of the whole column plus two masks and an add (4 instructions),
+// so k is hidden behind an empty asm that claims to rewrite it in an SGPR:
+// the multiply stays a multiply (k in an SGPR operand). An inline-asm mad with
+// an explicit VCC carry-out instead made the hazard recognizer put an s_nop
+// between consecutive mads (1,414 in k_ktab_ladder).
 template <uint32_t K>
 BH_HD void mac_k(uint64_t& c, uint32_t m) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (K <= 64) {
-    asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c) : "v"(m), "i"(K) : "vcc");
-  } else {
-    asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c) : "v"(m), "s"(K) : "vcc");
-  }
+  uint32_t k = K;
+  asm("" : "+s"(k));
+  c += (uint64_t)m * k;
 #else
   c += (uint64_t)m * K;
 #endif

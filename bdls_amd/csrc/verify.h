@@ -77,6 +77,7 @@ struct Work {
   uint32_t* r2m;    // [9][ns]  (r + n) * 2^270 mod p   (valid iff ST_R2OK)
   uint8_t* st;      // [ns]
   uint32_t* qtab;   // [ns/64][64 lanes][16][28]  per-lane Q multiples 1..16 (Jacobian, radix 2^30)
+  uint32_t* gpart;  // [28][ns]  u1 G of key-comb list position j (X, Y, Z, infinity flag)
 };
 
 // Per-batch key plan (device): open-addressed fingerprint table for key
@@ -881,46 +882,34 @@ BH_HD void ktab_load(J30& P, const uint32_t* tab, uint32_t win, uint32_t j) {
   }
 }
 
-// Two-wave table build (k_ktab_ladder build blocks, round 2). One build lane
-// per table left one wave per SIMD at 65,536 tables, with nothing to hide the
-// v_mad_u64_u32 dependency latency (0.57 of the counter-based VALU rate). The
-// work of a window is split between two waves of a workgroup, 64 tables per
-// wave pair, synchronised once per window:
-//   chain wave : B -> 2B -> 4B -> 8B -> 16B (next base) and 5B = 4B + B
-//                (4 doublings + 1 addition; stores B, 2B, 4B, 5B, 8B)
-//   side wave  : one window behind, loads B and 2B back and makes
-//                3B = 2B + B, 6B = 2 (3B), 7B = 6B + B (2 additions + 1 doubling)
-// Same points and total work as one lane doing both (round 1's ktab_build:
-// a two-lane split by window ranges cost +18 % doublings and was slower at
-// 65,536 tables), twice the waves. Entry j of window w = (j+1) 16^w Q.
+// One lane per table: entry j of window w = (j+1) 16^w Q. Per window a co-Z
+// chain (ec30.h j_dblu / j_zaddu): DBLU gives 2B and B on 2B's Z, then six
+// ZADDUs give 3B..8B, each re-basing B onto the new sum's Z, and one doubling
+// of 8B gives the next window's base 16B:
+//   8 + 6 x 7 + 8 = 58 F_p mul/sqr per window (the plain Jacobian sequence,
+//   5 doublings + 3 full additions, is 88).
+// The entries are ordinary Jacobian points (each with its own Z), so the key
+// comb is unchanged. ZADDU cannot degenerate here: k B = +-B would need n to
+// divide (k -+ 1) 16^w with k - 1 <= 7, and n is a prime of 256 bits.
 template <class P>
-BH_HD void ktab_chain_step(J30& B, uint32_t* tab, uint32_t win) {
-  J30 E2, E4, T;
-  bool same;
-  ktab_store(tab, win, 0, B);          // 1 B
-  j_dbl<P>(E2, B);
-  ktab_store(tab, win, 1, E2);         // 2 B
-  j_dbl<P>(E4, E2);
-  ktab_store(tab, win, 3, E4);         // 4 B
-  j_add<P>(T, E4, B, &same);
-  ktab_store(tab, win, 4, T);          // 5 B
-  j_dbl<P>(T, E4);
-  ktab_store(tab, win, 7, T);          // 8 B
-  j_dbl<P>(B, T);                      // 16 B: the next window's base
-}
-
-template <class P>
-BH_HD void ktab_side_step(uint32_t* tab, uint32_t win) {
-  J30 B, E2, T;
-  bool same;
-  ktab_load(B, tab, win, 0);
-  ktab_load(E2, tab, win, 1);
-  j_add<P>(T, E2, B, &same);
-  ktab_store(tab, win, 2, T);          // 3 B
-  j_dbl<P>(T, T);
-  ktab_store(tab, win, 5, T);          // 6 B
-  j_add<P>(T, T, B, &same);
-  ktab_store(tab, win, 6, T);          // 7 B
+BH_HD void ktab_build(uint32_t* tab, const Work& w, uint32_t rec) {
+  J30 B, Bz, S;
+  ld9(B.X, w.qx, rec, w.ns);
+  ld9(B.Y, w.qy, rec, w.ns);
+  f_const(B.Z, P::r1);
+  for (uint32_t win = 0; win < (uint32_t)kKWin; win++) {
+    ktab_store(tab, win, 0, B);               // 1 B
+    j_dblu<P>(S, Bz, B);                      // S = 2B, Bz = B on S's Z
+    ktab_store(tab, win, 1, S);               // 2 B
+#pragma unroll 1  // one ZADDU body (~10 KB of code; unrolled: same speed, 5x the code)
+    for (uint32_t j = 2; j < (uint32_t)kKEnt; j++) {
+      J30 T;
+      j_zaddu<P>(T, Bz, S);                   // T = (j+1) B; Bz onto T's Z
+      ktab_store(tab, win, j, T);
+      j_copy(S, T);
+    }
+    j_dbl<P>(B, S);                           // 16 B: the next window's base
+  }
 }
 
 // u2 Q from a key table: 4-bit signed windows (least significant first).
@@ -977,6 +966,45 @@ BH_HD bool stage_keycomb(const Work& w, const uint32_t* gtab, uint32_t i, const 
   uint32_t u1[8];
   ld8(u1, w.e, i, w.ns);
   g_comb<P>(B, b_inf, gtab, u1);
+  return finish_check<P>(w, i, A, a_inf, B, b_inf);
+}
+
+// Split key comb (large batches). The u1 G half does not need the key tables,
+// so k_ktab_ladder computes it for every key-comb record WHILE the tables are
+// built (the build runs one wave per SIMD and leaves issue slots free), and
+// k_keycomb then only adds the 65 table points and the stored u1 G. Stored by
+// list position j, SoA, so both sides are coalesced.
+constexpr uint32_t kGPartWords = 28;
+template <class P>
+BH_HD void stage_gpart(const Work& w, const uint32_t* gtab, uint32_t i, uint32_t j) {
+  J30 B;
+  bool b_inf;
+  uint32_t u1[8];
+  ld8(u1, w.e, i, w.ns);
+  g_comb<P>(B, b_inf, gtab, u1);
+  uint32_t* o = w.gpart + j;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    o[(size_t)k * w.ns] = B.X[k];
+    o[(size_t)(9 + k) * w.ns] = B.Y[k];
+    o[(size_t)(18 + k) * w.ns] = B.Z[k];
+  }
+  o[(size_t)27 * w.ns] = b_inf ? 1u : 0u;
+}
+
+template <class P>
+BH_HD bool stage_keycomb_q(const Work& w, uint32_t i, uint32_t j, const uint32_t* tab) {
+  J30 A, B;
+  bool a_inf;
+  q_keycomb<P>(A, a_inf, w, i, tab);
+  const uint32_t* o = w.gpart + j;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    B.X[k] = o[(size_t)k * w.ns];
+    B.Y[k] = o[(size_t)(9 + k) * w.ns];
+    B.Z[k] = o[(size_t)(18 + k) * w.ns];
+  }
+  const bool b_inf = o[(size_t)27 * w.ns] != 0;
   return finish_check<P>(w, i, A, a_inf, B, b_inf);
 }
 

@@ -358,42 +358,28 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(Work w, Plan pl, uint32_t
   else pl.ladder_list[slot] = i;
 }
 
-// Blocks [0, tab_blocks) build key tables, 128 per block: waves 2q / 2q+1
-// are the chain / side waves of tables [128 b + 64 q, +64) (verify.h
-// ktab_chain_step / ktab_side_step), one __syncthreads per window; the rest
-// run the ladder list. Ladder waves past the list length exit whole (the
-// Q-table scratch slot is the list position).
-constexpr uint32_t kBuildPerBlock = 128;
+// Blocks [0, tab_blocks) build key tables (one lane per table, verify.h
+// ktab_build), the next lad_blocks run the ladder list (waves past the list
+// length exit whole; the Q-table scratch slot is the list position), the last
+// gp_blocks compute the u1 G half of the key-comb list (verify.h stage_gpart)
+// while the builds run: one build wave per SIMD leaves issue slots free.
+constexpr uint32_t kBuildPerBlock = 256;
 template <class P>
 __global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
                                                      const uint32_t* __restrict__ gtab,
                                                      uint8_t* __restrict__ reason,
-                                                     uint32_t tab_blocks) {
+                                                     uint32_t tab_blocks,
+                                                     uint32_t lad_blocks) {
+  if (blockIdx.x >= tab_blocks + lad_blocks) {
+    const uint32_t j = (blockIdx.x - tab_blocks - lad_blocks) * blockDim.x + threadIdx.x;
+    if (j < pl.counters[0]) stage_gpart<P>(w, gtab, pl.comb_order[j], j);
+    return;
+  }
   if (blockIdx.x < tab_blocks) {
     const uint32_t nt = min(pl.counters[2], pl.max_tables);
     const uint32_t base = blockIdx.x * kBuildPerBlock;
-    if (base >= nt) return;  // uniform over the block: no barrier is skipped
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t role = wv & 1u, t = base + (wv >> 1) * 64u + lane;
-    const bool active = t < nt;
-    uint32_t* tab = active ? const_cast<uint32_t*>(tab_ptr(pl, g, pl.tab_dst[t])) : nullptr;
-    J30 B;
-    if (role == 0 && active) {
-      const uint32_t rec = pl.tab_rec[t];
-      ld9(B.X, w.qx, rec, w.ns);
-      ld9(B.Y, w.qy, rec, w.ns);
-      f_const(B.Z, P::r1);
-    }
-    for (uint32_t step = 0; step <= (uint32_t)kKWin; step++) {
-      if (active) {
-        if (role == 0) {
-          if (step < (uint32_t)kKWin) ktab_chain_step<P>(B, tab, step);
-        } else if (step > 0) {
-          ktab_side_step<P>(tab, step - 1);
-        }
-      }
-      __syncthreads();  // window `step`'s B, 2B are visible to the side wave
-    }
+    const uint32_t t = base + threadIdx.x;
+    if (t < nt) ktab_build<P>(const_cast<uint32_t*>(tab_ptr(pl, g, pl.tab_dst[t])), w, pl.tab_rec[t]);
     return;
   }
   const uint32_t j0 = (blockIdx.x - tab_blocks) * blockDim.x + threadIdx.x;
@@ -472,7 +458,7 @@ __global__ __launch_bounds__(256) BH_KEYCOMB_ATTR void k_keycomb(Work w, Plan pl
   const uint32_t cnt = pl.counters[0];
   if (j >= cnt) return;
   const uint32_t i = pl.comb_order[j];
-  const bool ok = stage_keycomb<P>(w, gtab, i, tab_ptr(pl, g, pl.rec_tab[i]));
+  const bool ok = stage_keycomb_q<P>(w, i, j, tab_ptr(pl, g, pl.rec_tab[i]));
   reason[i] = ok ? R_OK : R_MATH;
 }
 
@@ -675,20 +661,22 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   }
   REC(3);
   const uint32_t tab_blocks = (pl.max_tables + kBuildPerBlock - 1) / kBuildPerBlock;
+  // u1 G of the key-comb list runs inside k_ktab_ladder for the 1-lane comb
+  const uint32_t gp_blocks = o.wide <= 1 ? grd.x : 0u;
   // from here on only plc (rec_slot consumed by the sort)
   if constexpr (!P::a_is_minus3) {
     if (o.wide > 1) {  // small secp256k1 batch: 2-lane GLV ladder
       hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, plc, g, gtab,
-                         reason, tab_blocks);
+                         reason, tab_blocks, 0u);
       hipLaunchKernelGGL((k_ladder2<P>), dim3((2 * n + 255) / 256), blk, 0, s, w, plc, gtab,
                          reason);
     } else {
-      hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x), blk, 0, s, w, plc, g,
-                         gtab, reason, tab_blocks);
+      hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x + gp_blocks), blk, 0, s, w,
+                         plc, g, gtab, reason, tab_blocks, grd.x);
     }
   } else {
-    hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x), blk, 0, s, w, plc, g, gtab,
-                       reason, tab_blocks);
+    hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x + gp_blocks), blk, 0, s, w,
+                       plc, g, gtab, reason, tab_blocks, grd.x);
   }
   REC(4);
   if (o.keep)
@@ -745,7 +733,7 @@ static hipError_t reg_seq(const uint8_t* pub, const Work& w, const Plan& pl, con
   hipLaunchKernelGGL(k_key_plan, grd, blk, 0, s, w, pl, g, n, 1u, 0u, 1u, 1u);
   const uint32_t tab_blocks = (pl.max_tables + kBuildPerBlock - 1) / kBuildPerBlock;
   hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, pl, g,
-                     (const uint32_t*)nullptr, (uint8_t*)nullptr, tab_blocks);
+                     (const uint32_t*)nullptr, (uint8_t*)nullptr, tab_blocks, 0u);
   hipLaunchKernelGGL(k_reg_publish, dim3((pl.max_tables + 255) / 256), blk, 0, s, w, pl, g);
   hipLaunchKernelGGL(k_reg_status, grd, blk, 0, s, w, pl, n, status);
   return hipGetLastError();

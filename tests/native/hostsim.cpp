@@ -58,7 +58,10 @@ static bool keycomb_any(const Work& w, const uint32_t* gtab, uint32_t i, const u
     case 4: return wide_keycomb<P, 4>(w, gtab, i, tab);
     case 8: return wide_keycomb<P, 8>(w, gtab, i, tab);
     case 16: return wide_keycomb<P, 16>(w, gtab, i, tab);
-    default: return stage_keycomb<P>(w, gtab, i, tab);
+    case 0: return stage_keycomb<P>(w, gtab, i, tab);
+    default:  // the device's split: u1 G stored by list position, then the table half
+      stage_gpart<P>(w, gtab, i, i);
+      return stage_keycomb_q<P>(w, i, i, tab);
   }
 }
 
@@ -71,7 +74,8 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
                    uint32_t* n_comb) {
   const uint32_t* gtab = gtab_for<P>();
   const uint32_t ns = (n + 63) & ~63u;
-  std::vector<uint32_t> buf((size_t)9 * 9 * ns + (size_t)2 * ns * kQTab * kQPt);
+  std::vector<uint32_t> buf((size_t)9 * 9 * ns + (size_t)2 * ns * kQTab * kQPt +
+                            (size_t)kGPartWords * ns);
   std::vector<uint8_t> st(ns);
   Work w;
   w.ns = ns;
@@ -86,6 +90,8 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
   w.r2m = p; p += 9 * ns;
   p += 9 * ns;
   w.qtab = p;
+  p += (size_t)2 * ns * kQTab * kQPt;
+  w.gpart = p;
   w.st = st.data();
   for (uint32_t i = 0; i < n; i++) {
     if constexpr (std::is_same_v<IN, BatchIn>) {
@@ -127,16 +133,7 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
       if (tab_of[r] == kNone) {
         tab_of[r] = (uint32_t)tables.size();
         tables.emplace_back(kKTabWords);
-        // the device's two-wave schedule: chain window s, side window s - 1
-        uint32_t* tab = tables.back().data();
-        J30 B;
-        ld9(B.X, w.qx, r, w.ns);
-        ld9(B.Y, w.qy, r, w.ns);
-        f_const(B.Z, P::r1);
-        for (uint32_t step = 0; step <= (uint32_t)kKWin; step++) {
-          if (step < (uint32_t)kKWin) ktab_chain_step<P>(B, tab, step);
-          if (step > 0) ktab_side_step<P>(tab, step - 1);
-        }
+        ktab_build<P>(tables.back().data(), w, r);  // the device's co-Z chain
       }
       ok = keycomb_any<P>(w, gtab, i, tables[tab_of[r]].data());
       combs++;
