@@ -44,14 +44,18 @@ sys.path.insert(0, ROOT)
 
 # Algorithmic work per verify in SURVEY.md 8(d) units: F_p mul/sqr x 128 u32
 # MACs (64 product + 64 reduction). The variable-base ladder is schedule S0
-# (3.2e3 F_p ops = 4.1e5 MACs). The per-key comb path does 65 Jacobian adds
-# (16 ops) + G_WINDOWS mixed adds (11 ops) + ~23 for the final add/x check
-# (= 1,349 F_p ops per verify with the 10-bit G comb: BH_GCOMB_BITS in
-# verify.h), plus 65 x (5 dbl x 8 + 3 add x 16) = 5,720 per key table.
+# (3.2e3 F_p ops = 4.1e5 MACs). The per-key comb path is split over two
+# kernels: k_ktab_ladder builds the key tables (co-Z chain, 65 windows x 58 F_p
+# ops = 3,770 per table) and, beside them, the u1 G half of every key-comb
+# record (G_WINDOWS mixed adds of 11 ops over the 10-bit G comb: BH_GCOMB_BITS
+# in verify.h); k_keycomb adds the 65 key-table points (KTAB_ADD ops each) and
+# the stored u1 G and checks x (~23 ops).
 MAC_PER_FP = 128
 G_COMB_BITS = 10
 G_WINDOWS = (257 + G_COMB_BITS - 1) // G_COMB_BITS
-FP_LADDER, FP_KEYCOMB, FP_KTAB = 3200, 65 * 16 + G_WINDOWS * 11 + 23, 5720
+KTAB_ADD = 16  # Jacobian addition (12M + 4S): the key tables are Jacobian
+FP_LADDER, FP_GPART, FP_KTAB = 3200, G_WINDOWS * 11, 65 * 58
+FP_KEYCOMB = 65 * KTAB_ADD + 23
 MACS_PER_VERIFY = FP_LADDER * MAC_PER_FP
 KERNELS = {"build_ladder_ms": "k_ktab_ladder", "keycomb_ms": "k_keycomb"}
 CONFIG5_TOTAL = 1 << 26
@@ -60,7 +64,8 @@ CONFIG5_TOTAL = 1 << 26
 def kernel_fp_ops(stage: str, routes: dict) -> float:
     """Algorithmic F_p ops of one launch of the stage's kernel."""
     if stage == "build_ladder_ms":
-        return routes["ladder"] * FP_LADDER + routes["key_tables"] * FP_KTAB
+        return (routes["ladder"] * FP_LADDER + routes["key_tables"] * FP_KTAB
+                + routes["keycomb"] * FP_GPART)
     return routes["keycomb"] * FP_KEYCOMB
 
 
@@ -664,7 +669,8 @@ def bench_throughput(a, rank, world, local):
             "unit": "TMAC/s (u32 x u32 -> u64)",
             "frac": achieved / peak if peak else None,
             "work_per_launch": (f"{routes['ladder']} ladder verifies x {FP_LADDER} + "
-                                f"{routes['key_tables']} key tables x {FP_KTAB}"
+                                f"{routes['key_tables']} key tables x {FP_KTAB} + "
+                                f"{routes['keycomb']} u1 G halves x {FP_GPART}"
                                 if dom == "build_ladder_ms" else
                                 f"{routes['keycomb']} key-table verifies x {FP_KEYCOMB}")
                                + f" F_p mul/sqr x {MAC_PER_FP} u32 MACs (SURVEY 8(d) units)",

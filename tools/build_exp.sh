@@ -1,0 +1,20 @@
+#!/bin/bash
+# Build library variants for A/B runs on the GPU (tools/gpu_check.sh STEPS=exp):
+#   tools/build_exp.sh name:-DFLAG=1+-DOTHER=2 name2:...
+# Each variant recompiles verify_kernels.hip with its flags and links it with
+# the default host objects into build/exp/libbdlship_<name>.so. Parallel.
+set -eu
+cd "$(dirname "$0")/.."
+make -s bdls_amd/lib/bdls_hip.o bdls_amd/lib/bdls_msg.o bdls_amd/lib/fabric.o
+mkdir -p build/exp  # variants accumulate; rm -rf build/exp to start over
+HIPCC=/opt/rocm/bin/hipcc
+one() {
+  n=${1%%:*}; f=$(echo "${1#*:}" | tr '+' ' ')
+  $HIPCC -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function $f \
+    -c bdls_amd/csrc/verify_kernels.hip -o build/exp/vk_$n.o &&
+  $HIPCC --offload-arch=gfx950 -shared -fPIC -o build/exp/libbdlship_$n.so build/exp/vk_$n.o \
+    bdls_amd/lib/bdls_hip.o bdls_amd/lib/bdls_msg.o bdls_amd/lib/fabric.o -lpthread &&
+  echo "built $n"
+}
+export -f one; export HIPCC
+printf '%s\n' "$@" | xargs -P 4 -I{} bash -c 'one "$@"' _ {}
