@@ -152,6 +152,8 @@ struct Dev {
   int id = -1;
   hipStream_t stream = nullptr;  // compute (+ result download)
   hipStream_t copy = nullptr;    // host-API input upload
+  hipStream_t aux = nullptr;     // BDLS digests beside the rest of a pass
+  hipEvent_t fork = nullptr, join = nullptr;
   uint32_t* gtab[2] = {nullptr, nullptr};
   DevBuf ws;     // Work + Plan
   DevBuf stage;  // key registration input
@@ -182,8 +184,8 @@ size_t max_tables_for(size_t ns, bool reg = false) {
 }
 
 // Q-table slots: one per record, two for batches small enough to run the
-// 2-lane secp256k1 ladder (launch_opts: wide > 1).
-size_t qtab_slots(size_t ns) { return ns <= 8192 ? 2 * ns : ns; }
+// 2-lane secp256k1 ladder (launch_opts: wide > 1, i.e. up to kWide4Max).
+size_t qtab_slots(size_t ns) { return ns <= bh::kWide4Max ? 2 * ns : ns; }
 
 size_t work_bytes(size_t ns) {
   // 4 scalar SoA arrays (8 limbs) + 4 base-field SoA arrays (9 limbs) + status
@@ -193,7 +195,7 @@ size_t work_bytes(size_t ns) {
   const size_t hc = pow2_at_least(2 * ns);
   const size_t mt = max_tables_for(ns);
   return 4 * 32 * ns + 4 * 36 * ns + ns + qtab_slots(ns) * bh::kQTab * bh::kQPt * 4 +
-         bh::kGPartWords * 4 * ns +
+         bh::kGPartWords * 4 * bh::gpart_slots(ns) +
          hc * (8 + 4 + 4 + 4) + ns * 16 + 16 + mt * 8 + mt * (size_t)bh::kKTabWords * 4 +
          256 * 27;
 }
@@ -219,7 +221,7 @@ int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl, bool reg = false) {
   w->r2m = (uint32_t*)take(36 * ns);
   w->st = (uint8_t*)take(ns);
   w->qtab = (uint32_t*)take(qtab_slots(ns) * bh::kQTab * bh::kQPt * 4);
-  w->gpart = (uint32_t*)take(bh::kGPartWords * 4 * ns);
+  w->gpart = (uint32_t*)take(bh::kGPartWords * 4 * bh::gpart_slots(ns));
   const size_t hc = pow2_at_least(2 * ns);
   const size_t mt = max_tables_for(ns, reg);
   pl->hc = (uint32_t)hc;
@@ -283,6 +285,9 @@ int dev_init(Dev& d, int id) {
                                 prop.gcnArchName + ", this build targets gfx950 only");
   HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&d.fork, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&d.join, hipEventDisableTiming));
   for (Slot& sl : d.slot) {
     HIPCHK(hipEventCreateWithFlags(&sl.uploaded, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
@@ -315,6 +320,12 @@ void dev_free(Dev& d) {
     if (sl.done) (void)hipEventDestroy(sl.done);
   }
   if (d.copy) (void)hipStreamDestroy(d.copy);
+  if (d.aux) {
+    (void)hipStreamSynchronize(d.aux);
+    (void)hipStreamDestroy(d.aux);
+  }
+  if (d.fork) (void)hipEventDestroy(d.fork);
+  if (d.join) (void)hipEventDestroy(d.join);
   for (auto& r : d.reg) r.mem.release();
   for (auto& e : d.ev)
     if (e) (void)hipEventDestroy(e);
@@ -354,7 +365,7 @@ bh::LaunchOpts launch_opts(size_t m, uint32_t flags) {
   o.min_uses = o.keep ? 2u : bh::kMinUses;
   o.min_batch = o.keep ? 0u : bh::kKeyTableMinBatch;
   // below chip size, spread each key-table record over 16 or 4 lanes
-  o.wide = m <= 8192 ? 16 : m <= 32768 ? 4 : 1;
+  o.wide = bh::wide_for(m);
   return o;
 }
 
@@ -399,7 +410,10 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
     bh::Plan pl;
     int rc = carve_work(d, m, &w, &pl);
     if (rc) return rc;
-    const bh::LaunchOpts o = launch_opts(m, flags);
+    bh::LaunchOpts o = launch_opts(m, flags);
+    o.aux = d.aux;
+    o.ev_fork = d.fork;
+    o.ev_join = d.join;
     hipEvent_t* ev = t ? d.ev : nullptr;
     if (!t && d.defer) {
       if (d.ev_used == d.ev_pool.size()) {

@@ -110,7 +110,26 @@ struct LaunchOpts {
   uint32_t min_batch;  // no per-batch tables below this batch size
   bool keep;           // BH_F_KEEP_KEYS: new tables go to the key registry
   int wide;            // lanes per record on the key-table path (1, 4, 16)
+  // BDLS batches: the BLAKE2b digests run on a second stream (hipStream_t)
+  // beside prep / inverse / plan / the u2 Q halves; fork and join are
+  // hipEvent_t. Opaque here so the host harness compiles this header.
+  void* aux = nullptr;
+  void* ev_fork = nullptr;
+  void* ev_join = nullptr;
 };
+
+// Lanes per record on the key-table path by batch size (records far below
+// chip size are spread over 16 or 4 lanes; the secp256k1 ladder then runs on
+// 2 lanes per record).
+constexpr uint32_t kWide16Max = 8192, kWide4Max = 32768;
+BH_HD int wide_for(size_t m) { return m <= kWide16Max ? 16 : m <= kWide4Max ? 4 : 1; }
+// Partial-sum slots of w.gpart: one per record (stage_gpart), or for wide
+// batches the split kernels' ladder pairs [0, 2 ns) + key-comb groups
+// [2 ns, (2 + wide) ns).
+BH_HD size_t gpart_slots(size_t ns) {
+  const int wide = wide_for(ns);
+  return wide > 1 ? (2 + (size_t)wide) * ns : ns;
+}
 
 // G comb table: kGW-bit signed windows. Window w in [0, kCombWindows), entry
 // j in [0, kCombEntries): (j+1) * 2^(kGW w) * G, affine, canonical radix-2^30
@@ -304,7 +323,7 @@ BH_HD void stage_bdls_hash(const BdlsIn& in, const Work& w, uint32_t i) {
 template <class P, class N, class C>
 BH_HD void stage_prep(const BdlsIn& in, const Work& w, uint32_t i) {
   uint8_t reason = R_OK;
-  uint32_t r[8], s[8], e[8], nn[8];
+  uint32_t r[8], s[8], nn[8];
   uint32_t qx30[9], qy30[9];
   load_const8(nn, C::n);
   bool rbig, rzero, sbig, szero;
@@ -316,7 +335,8 @@ BH_HD void stage_prep(const BdlsIn& in, const Work& w, uint32_t i) {
   if (reason == R_OK && !key_import<P, C>(q, qx30, qy30)) reason = R_BAD_KEY;
   if (reason == R_OK && (rbig || geq8(r, nn))) reason = R_R_RANGE;
   if (reason == R_OK && (sbig || geq8(s, nn))) reason = R_S_RANGE;
-  if (reason == R_OK) ld8(e, w.e, i, w.ns);  // stage_bdls_hash (or k_bdls_hash) ran first
+  // e (w.e) is written by stage_bdls_hash / k_bdls_hash, possibly concurrently:
+  // prep never touches it (a rejected record's e is any scalar < n)
   uint8_t st = reason;
   if (reason == R_OK) {
     uint32_t pmn[8], rn[8], rm[9], r2m[9];
@@ -337,13 +357,12 @@ BH_HD void stage_prep(const BdlsIn& in, const Work& w, uint32_t i) {
     st9(w.r2m, i, w.ns, r2m);
     to_mont<N>(s, s);
   } else {
-    for (int k = 0; k < 8; k++) { e[k] = r[k] = 0; }
-    e[0] = r[0] = 1;
+    for (int k = 0; k < 8; k++) r[k] = 0;
+    r[0] = 1;
     load_const8(s, N::r1);
     f_const(qx30, P::gx_m);
     f_const(qy30, P::gy_m);
   }
-  st8(w.e, i, w.ns, e);
   st8(w.r, i, w.ns, r);
   st8(w.sm, i, w.ns, s);
   st9(w.qx, i, w.ns, qx30);
@@ -353,8 +372,9 @@ BH_HD void stage_prep(const BdlsIn& in, const Work& w, uint32_t i) {
 
 // ------------------------------------------------------------ batch inverse
 // One lane's records (strided). Montgomery's trick: one safegcd inversion per
-// lane, 3 multiplications per record.
-template <class N>
+// lane, 3 multiplications per record. U1 = false (BDLS batches whose digests
+// are still being hashed): w = s^-1 R goes to w.sm for stage_u1, u1 later.
+template <class N, bool U1 = true>
 BH_HD void stage_inv(const Work& w, uint32_t c, uint32_t stride, uint32_t n) {
   // lane c owns records c, c + stride, c + 2 stride, ... (< n): consecutive
   // lanes touch consecutive records, so every limb access is coalesced
@@ -376,14 +396,27 @@ BH_HD void stage_inv(const Work& w, uint32_t c, uint32_t stride, uint32_t n) {
     mont_mul<N>(wi, inv, pre);  // s_i^-1 * R
     ld8(x, w.sm, i, w.ns);
     mont_mul<N>(inv, inv, x);
-    ld8(t, w.e, i, w.ns);
-    mont_mul<N>(t, t, wi);      // u1 = e * w (plain)
-    st8(w.e, i, w.ns, t);
+    if constexpr (U1) {
+      ld8(t, w.e, i, w.ns);
+      mont_mul<N>(t, t, wi);    // u1 = e * w (plain)
+      st8(w.e, i, w.ns, t);
+    } else {
+      st8(w.sm, i, w.ns, wi);
+    }
     ld8(t, w.r, i, w.ns);
     mont_mul<N>(t, t, wi);      // u2 = r * w (plain)
     st8(w.r, i, w.ns, t);
     if (i < c + stride) break;
   }
+}
+
+// u1 = e w for the U1 = false inverse (after the digests are in w.e).
+template <class N>
+BH_HD void calc_u1(uint32_t u1[8], const Work& w, uint32_t i) {
+  uint32_t wi[8];
+  ld8(u1, w.e, i, w.ns);
+  ld8(wi, w.sm, i, w.ns);
+  mont_mul<N>(u1, u1, wi);
 }
 
 // ------------------------------------------------------------------ ladder
@@ -1190,17 +1223,15 @@ template <class P, int L>
 BH_HD void g_comb_part(J30& C, bool& c_inf, const uint32_t* gtab, const uint32_t u1[8],
                        uint32_t l);  // below
 
-// Lane l's partial sum C = sum over its windows of (key-table digit points
-// + G-comb digit points).
+// Lane l's u2 Q windows (win = l, l + L, ...) of the key table.
 template <class P, int L>
-BH_HD void keycomb_part(J30& C, bool& c_inf, const Work& w, const uint32_t* gtab, uint32_t i,
-                        const uint32_t* tab, uint32_t l) {
+BH_HD void keycomb_q_part(J30& C, bool& c_inf, const Work& w, uint32_t i, const uint32_t* tab,
+                          uint32_t l) {
   uint32_t k[8], v[9], sv[9];
   f_const(C.X, P::r1);
   f_const(C.Y, P::r1);
   f_const(C.Z, P::r1);
   c_inf = true;
-  // u2 Q: 4-bit windows win = l + m L
   ld8(k, w.r, i, w.ns);
   recode_offset(v, k, 0x88888888u, 0x8u);
   shr288(sv, v, 4u * l);
@@ -1216,9 +1247,17 @@ BH_HD void keycomb_part(J30& C, bool& c_inf, const Work& w, const uint32_t* gtab
       j_acc<P>(C, c_inf, T, mag == 0);
     }
   }
-  // u1 G: kGW-bit windows win = l + m L over the affine G comb
+}
+
+// Lane l's partial sum C = sum over its windows of (key-table digit points
+// + G-comb digit points).
+template <class P, int L>
+BH_HD void keycomb_part(J30& C, bool& c_inf, const Work& w, const uint32_t* gtab, uint32_t i,
+                        const uint32_t* tab, uint32_t l) {
+  keycomb_q_part<P, L>(C, c_inf, w, i, tab, l);  // u2 Q: 4-bit windows win = l + m L
+  uint32_t k[8];
   ld8(k, w.e, i, w.ns);
-  g_comb_part<P, L>(C, c_inf, gtab, k, l);
+  g_comb_part<P, L>(C, c_inf, gtab, k, l);        // u1 G: kGW-bit windows win = l + m L
 }
 
 // C += the G-comb windows win = l, l + L, ... of u1 G (kGW-bit signed digits
@@ -1260,6 +1299,31 @@ BH_HD void ladder2_part(J30& C, bool& c_inf, const Work& w, const uint32_t* gtab
   uint32_t u1[8];
   ld8(u1, w.e, i, w.ns);
   g_comb_part<P, 2>(C, c_inf, gtab, u1, part);
+}
+
+// Partial-sum scratch for the split wide kernels (BDLS batches: the u2 Q
+// halves run while the digests are hashed, the u1 G halves after): slot g of
+// a lane, SoA with stride `stride` (>= lanes), 28 words (X, Y, Z, infinity).
+BH_HD void part_store(const Work& w, uint32_t g, uint32_t stride, const J30& C, bool c_inf) {
+  uint32_t* o = w.gpart + g;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    o[(size_t)k * stride] = C.X[k];
+    o[(size_t)(9 + k) * stride] = C.Y[k];
+    o[(size_t)(18 + k) * stride] = C.Z[k];
+  }
+  o[(size_t)27 * stride] = c_inf ? 1u : 0u;
+}
+
+BH_HD void part_load(const Work& w, uint32_t g, uint32_t stride, J30& C, bool& c_inf) {
+  const uint32_t* o = w.gpart + g;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    C.X[k] = o[(size_t)k * stride];
+    C.Y[k] = o[(size_t)(9 + k) * stride];
+    C.Z[k] = o[(size_t)(18 + k) * stride];
+  }
+  c_inf = o[(size_t)27 * stride] != 0;
 }
 
 }  // namespace bh

@@ -198,18 +198,26 @@ __global__ __launch_bounds__(256) void k_bdls_hash(BdlsIn in, Work w, uint32_t n
   st8(w.e, i, w.ns, e);
 }
 
-template <class P, class N, class C>
-void launch_prep(const BdlsIn& in, const Work& w, uint32_t n, dim3 grd, dim3 blk, hipStream_t s) {
-  hipLaunchKernelGGL((k_bdls_hash<C>), dim3((n * 4 + 255) / 256), blk, 0, s, in, w, n);
-  hipLaunchKernelGGL((k_prep<P, N, C, BdlsIn, 0>), grd, blk, 0, s, in, w, n);
-}
 
-template <class N>
+template <class N, bool U1>
 __global__ __launch_bounds__(256) void k_inv(Work w, uint32_t n, uint32_t lanes) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= lanes) return;
-  stage_inv<N>(w, c, lanes, n);
+  stage_inv<N, U1>(w, c, lanes, n);
 }
+
+// u1 = e w into w.e (the U1 = false inverse, for kernels that read u1 there).
+// Every other u1 reader of a split pass computes it inline (calc_u1).
+template <class N>
+__global__ __launch_bounds__(256) void k_u1(Work w, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t u1[8];
+  calc_u1<N>(u1, w, i);
+  st8(w.e, i, w.ns, u1);
+}
+
+
 
 // ---- key lookup / dedup / plan ----------------------------------------------
 // Registry hit -> rec_tab; otherwise insert the fingerprint into the batch's
@@ -392,6 +400,23 @@ __global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
   if (active) reason[i] = ok ? R_OK : R_MATH;
 }
 
+// Butterfly over groups of L adjacent lanes: every lane ends with the group's
+// sum (L partial sums of one record).
+template <class P, int L>
+__device__ __forceinline__ void group_sum(J30& C, bool& c_inf) {
+  for (int off = 1; off < L; off <<= 1) {
+    J30 T;
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+      T.X[q] = __shfl_xor(C.X[q], off, 64);
+      T.Y[q] = __shfl_xor(C.Y[q], off, 64);
+      T.Z[q] = __shfl_xor(C.Z[q], off, 64);
+    }
+    const bool t_inf = __shfl_xor((int)c_inf, off, 64) != 0;
+    j_acc<P>(C, c_inf, T, t_inf);
+  }
+}
+
 // secp256k1 ladder on 2 lanes per record (small, latency-bound batches): lane
 // pair (2j, 2j+1) takes the k1 Q / k2 phi(Q) halves of the GLV split and
 // alternate G-comb windows (verify.h ladder2_part); lane 0 adds the halves.
@@ -410,18 +435,57 @@ __global__ __launch_bounds__(256) void k_ladder2(Work w, Plan pl,
   J30 C;
   bool c_inf;
   ladder2_part<P>(C, c_inf, w, gtab, i, gid >> 6, threadIdx.x & 63u, part);
-  J30 T;
-#pragma unroll
-  for (int q = 0; q < 9; q++) {
-    T.X[q] = __shfl_xor(C.X[q], 1, 64);
-    T.Y[q] = __shfl_xor(C.Y[q], 1, 64);
-    T.Z[q] = __shfl_xor(C.Z[q], 1, 64);
-  }
-  const bool t_inf = __shfl_xor((int)c_inf, 1, 64) != 0;
+  group_sum<P, 2>(C, c_inf);
   if (part != 0) return;
-  j_acc<P>(C, c_inf, T, t_inf);
   const bool ok = finish_check<P>(w, i, C, c_inf, C, true);
   if (active) reason[i] = ok ? R_OK : R_MATH;
+}
+
+// The same ladder split around the BDLS digests: k_ladder2_q runs the GLV
+// halves (no u1 needed) while k_bdls_hash runs on the second stream, and
+// k_ladder2_g adds the G-comb windows of u1 = e w afterwards. Partial sums
+// live in the gpart scratch (slot gid, stride pstride).
+template <class P>
+__global__ __launch_bounds__(256) void k_ladder2_q(Work w, Plan pl, uint32_t pstride) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j0 = gid >> 1, part = gid & 1u;
+  const uint32_t cnt = pl.counters[1];
+  if ((j0 & ~31u) >= cnt) return;
+  const uint32_t i = pl.ladder_list[j0 < cnt ? j0 : cnt - 1];
+  J30 C;
+  bool c_inf;
+  q_ladder_glv<P>(C, c_inf, w, i, gid >> 6, threadIdx.x & 63u, 1u << part);
+  part_store(w, gid, pstride, C, c_inf);
+}
+
+// 8 lanes per record: lanes 0 / 1 start from the two GLV halves, every lane
+// adds the G-comb windows l, l + 8, ... of u1 = e w (computed per lane), then
+// a 3-level butterfly; lane 0 checks. (2 lanes: 13 serial mixed additions.)
+constexpr int kLadGLanes = 8;
+template <class P, class N>
+__global__ __launch_bounds__(256) void k_ladder2_g(Work w, Plan pl,
+                                                   const uint32_t* __restrict__ gtab,
+                                                   uint8_t* __restrict__ reason,
+                                                   uint32_t pstride) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j0 = gid / kLadGLanes, l = gid % kLadGLanes;
+  const uint32_t cnt = pl.counters[1];
+  if (j0 >= cnt) return;  // whole groups exit together
+  const uint32_t i = pl.ladder_list[j0];
+  J30 C;
+  bool c_inf = true;
+  if (l < 2) {
+    part_load(w, 2 * j0 + l, pstride, C, c_inf);
+  } else {
+    f_const(C.X, P::r1);
+    f_const(C.Y, P::r1);
+    f_const(C.Z, P::r1);
+  }
+  uint32_t u1[8];
+  calc_u1<N>(u1, w, i);
+  g_comb_part<P, kLadGLanes>(C, c_inf, gtab, u1, l);
+  group_sum<P, kLadGLanes>(C, c_inf);
+  if (l == 0) reason[i] = finish_check<P>(w, i, C, c_inf, C, true) ? R_OK : R_MATH;
 }
 
 // Publish registry tables built in this batch (after the builds completed).
@@ -476,17 +540,46 @@ __global__ __launch_bounds__(256) void k_keycomb_wide(Work w, Plan pl, KeyReg g,
   J30 C;
   bool c_inf;
   keycomb_part<P, L>(C, c_inf, w, gtab, i, tab_ptr(pl, g, pl.rec_tab[i]), l);
-  for (int off = 1; off < L; off <<= 1) {
-    J30 T;
-#pragma unroll
-    for (int q = 0; q < 9; q++) {
-      T.X[q] = __shfl_xor(C.X[q], off, 64);
-      T.Y[q] = __shfl_xor(C.Y[q], off, 64);
-      T.Z[q] = __shfl_xor(C.Z[q], off, 64);
-    }
-    const bool t_inf = __shfl_xor((int)c_inf, off, 64) != 0;
-    j_acc<P>(C, c_inf, T, t_inf);
-  }
+  group_sum<P, L>(C, c_inf);
+  if (l == 0) reason[i] = finish_check<P>(w, i, C, c_inf, C, true) ? R_OK : R_MATH;
+}
+
+// k_keycomb_wide split around the BDLS digests like k_ladder2_q / _g: the key
+// table windows first, the u1 G windows once u1 = e w exists. Partial-sum slot
+// pbase + gid.
+template <class P, int L>
+__global__ __launch_bounds__(256) void k_keycomb_wide_q(Work w, Plan pl, KeyReg g,
+                                                        uint32_t pbase, uint32_t pstride) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j = gid / L, l = gid % L;
+  const uint32_t cnt = pl.counters[0];
+  if (j >= cnt) return;
+  const uint32_t i = pl.comb_order[j];
+  J30 C;
+  bool c_inf;
+  keycomb_q_part<P, L>(C, c_inf, w, i, tab_ptr(pl, g, pl.rec_tab[i]), l);
+  part_store(w, pbase + gid, pstride, C, c_inf);
+}
+
+// U1E: u1 is already in w.e (k_u1 ran for the P-256 Booth ladder).
+template <class P, class N, int L, bool U1E>
+__global__ __launch_bounds__(256) void k_keycomb_wide_g(Work w, Plan pl,
+                                                        const uint32_t* __restrict__ gtab,
+                                                        uint8_t* __restrict__ reason,
+                                                        uint32_t pbase, uint32_t pstride) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j = gid / L, l = gid % L;
+  const uint32_t cnt = pl.counters[0];
+  if (j >= cnt) return;
+  const uint32_t i = pl.comb_order[j];
+  J30 C;
+  bool c_inf;
+  part_load(w, pbase + gid, pstride, C, c_inf);
+  uint32_t u1[8];
+  if constexpr (U1E) ld8(u1, w.e, i, w.ns);
+  else calc_u1<N>(u1, w, i);
+  g_comb_part<P, L>(C, c_inf, gtab, u1, l);
+  group_sum<P, L>(C, c_inf);
   if (l == 0) reason[i] = finish_check<P>(w, i, C, c_inf, C, true) ? R_OK : R_MATH;
 }
 
@@ -628,14 +721,23 @@ static hipError_t comb_sort(const Plan& pl, const KeyReg& g, uint32_t n, hipStre
 
 // Full launch sequence. ev (optional, 7 events) brackets: prep | inv | plan
 // (lookup + dedup + split) | key tables + ladder | publish | key comb + bitmap.
+// BDLS batches hash their SignedProtos on the second stream (o.aux): forked
+// after the plan reset, joined before the first kernel that needs u1. Small
+// (wide) BDLS batches run the u2 Q halves of the ladder and key comb before the
+// join and only the u1 G halves after it (the digests of long lock / decide
+// messages are a serial BLAKE2b chain as long as the prep + inverse + plan).
 template <class P, class N, class C, class IN>
 static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg& g,
                       const uint32_t* gtab, uint32_t n, const LaunchOpts& o, uint64_t* bitmap,
                       uint8_t* reason, hipStream_t s, hipEvent_t* ev) {
+  constexpr bool kBdls = std::is_same_v<IN, BdlsIn>;
   const dim3 blk(256);
   const dim3 grd((n + 255) / 256);
   const uint32_t nlanes = (n + o.inv_chunk - 1) / o.inv_chunk;  // records per lane ~ inv_chunk
   const dim3 grc((nlanes + 255) / 256);
+  const bool split = kBdls && o.wide > 1 && o.aux;
+  // partial-sum slots (verify.h gpart_slots): ladder pairs, then key-comb groups
+  const uint32_t pstride = (uint32_t)gpart_slots(w.ns), pbase = 2u * w.ns;
   hipError_t e;
 #define REC(k)                                                 \
   if (ev) {                                                    \
@@ -643,9 +745,34 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   }
   if ((e = plan_reset(pl, s))) return e;
   REC(0);
-  launch_prep<P, N, C>(in, w, n, grd, blk, s);
+  bool joined = true;
+  if constexpr (kBdls) {
+    if (o.aux) {
+      hipStream_t aux = (hipStream_t)o.aux;
+      if ((e = hipEventRecord((hipEvent_t)o.ev_fork, s))) return e;
+      if ((e = hipStreamWaitEvent(aux, (hipEvent_t)o.ev_fork, 0))) return e;
+      hipLaunchKernelGGL((k_bdls_hash<C>), dim3((n * 4 + 255) / 256), blk, 0, aux, in, w, n);
+      if ((e = hipEventRecord((hipEvent_t)o.ev_join, aux))) return e;
+      joined = false;
+    } else {
+      hipLaunchKernelGGL((k_bdls_hash<C>), dim3((n * 4 + 255) / 256), blk, 0, s, in, w, n);
+    }
+    hipLaunchKernelGGL((k_prep<P, N, C, BdlsIn, 0>), grd, blk, 0, s, in, w, n);
+  } else {
+    launch_prep<P, N, C>(in, w, n, grd, blk, s);
+  }
   REC(1);
-  hipLaunchKernelGGL((k_inv<N>), grc, blk, 0, s, w, n, nlanes);
+  auto join = [&]() -> hipError_t {
+    if (joined) return hipSuccess;
+    joined = true;
+    return hipStreamWaitEvent(s, (hipEvent_t)o.ev_join, 0);
+  };
+  if (split) {
+    hipLaunchKernelGGL((k_inv<N, false>), grc, blk, 0, s, w, n, nlanes);
+  } else {
+    if ((e = join())) return e;
+    hipLaunchKernelGGL((k_inv<N, true>), grc, blk, 0, s, w, n, nlanes);
+  }
   REC(2);
   hipLaunchKernelGGL(k_key_insert, grd, blk, 0, s, w, pl, g, n);
   launch_key_count(w, pl, key_bytes(in), n, grd, blk, s);
@@ -664,6 +791,41 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   // u1 G of the key-comb list runs inside k_ktab_ladder for the 1-lane comb
   const uint32_t gp_blocks = o.wide <= 1 ? grd.x : 0u;
   // from here on only plc (rec_slot consumed by the sort)
+  if (split) {
+    // key tables (no u1), then the u2 Q halves; u1 G after the join
+    hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, plc, g, gtab, reason,
+                       tab_blocks, 0u);
+    if constexpr (!P::a_is_minus3)
+      hipLaunchKernelGGL((k_ladder2_q<P>), dim3((2 * n + 255) / 256), blk, 0, s, w, plc,
+                         pstride);
+    if (o.wide == 16)
+      hipLaunchKernelGGL((k_keycomb_wide_q<P, 16>), dim3((n * 16 + 255) / 256), blk, 0, s, w, plc,
+                         g, pbase, pstride);
+    else
+      hipLaunchKernelGGL((k_keycomb_wide_q<P, 4>), dim3((n * 4 + 255) / 256), blk, 0, s, w, plc, g,
+                         pbase, pstride);
+    REC(4);
+    if (o.keep)
+      hipLaunchKernelGGL(k_reg_publish, dim3((pl.max_tables + 255) / 256), blk, 0, s, w, plc, g);
+    if ((e = join())) return e;
+    if constexpr (!P::a_is_minus3) {
+      hipLaunchKernelGGL((k_ladder2_g<P, N>), dim3((kLadGLanes * n + 255) / 256), blk, 0, s, w,
+                         plc, gtab, reason, pstride);
+    } else {  // P-256 BDLS: the Booth ladder, whole (u1 needed from the start)
+      hipLaunchKernelGGL((k_u1<N>), grd, blk, 0, s, w, n);
+      hipLaunchKernelGGL((k_ktab_ladder<P>), grd, blk, 0, s, w, plc, g, gtab, reason, 0u, grd.x);
+    }
+    REC(5);
+    if (o.wide == 16)
+      hipLaunchKernelGGL((k_keycomb_wide_g<P, N, 16, P::a_is_minus3>), dim3((n * 16 + 255) / 256),
+                         blk, 0, s, w, plc, gtab, reason, pbase, pstride);
+    else
+      hipLaunchKernelGGL((k_keycomb_wide_g<P, N, 4, P::a_is_minus3>), dim3((n * 4 + 255) / 256),
+                         blk, 0, s, w, plc, gtab, reason, pbase, pstride);
+    hipLaunchKernelGGL(k_bitmap, grd, blk, 0, s, reason, n, bitmap);
+    REC(6);
+    return hipGetLastError();
+  }
   if constexpr (!P::a_is_minus3) {
     if (o.wide > 1) {  // small secp256k1 batch: 2-lane GLV ladder
       hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, plc, g, gtab,

@@ -255,3 +255,37 @@ def test_c_oracle_bdls_golden(bdls_golden):
         bad = [(r["tag"], int(g), r["reason"]) for r, g in zip(recs, got)
                if g != r["reason"] and not (r["reason"] == 7 and g == 9)]
         assert not bad
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("curve", ["secp256k1", "P-256"])
+@pytest.mark.parametrize("reps", [60, 80])
+def test_bdls_gpu_mixed_wide(bdls_golden, curve, reps):
+    """Batches below chip size (16 lanes per record at <= 8,192 records, 4 at
+    <= 32,768): the golden set repeated (its 4 keys get per-batch key tables)
+    plus a generated 100-validator round (keys used 2-4 times: ladder and key
+    table records mixed). Runs the split kernels -- u2 Q halves while the
+    BLAKE2b digests are hashed on the second stream, u1 G halves after -- and,
+    at 4 lanes, the 2-slots-per-record Q tables of the 2-lane ladder."""
+    from bdls_amd import _lib
+    from bdls_amd.workload import generate_bdls_round
+    _lib.ensure_init()
+    gold = [r for r in bdls_golden if r["curve"] == curve]
+    rb = generate_bdls_round(nval=100, curve=CURVE_ID[curve], seed=23)
+    rnd = [dict(x=d["x"].hex(), y=d["y"].hex(), r=d["r"].hex(), s=d["s"].hex(),
+                msg=d["msg"].hex(), version=d["version"])
+           for d in _round_records(rb, range(rb.n))]
+    recs = gold * reps + rnd
+    n = len(recs)
+    assert (n <= 8192) == (reps == 60) and n <= 32768
+    arrs = pack_bdls(recs)
+    bitmap = np.zeros((n + 7) // 8, np.uint8)
+    reason = np.full(n, 255, np.uint8)
+    b = _lib.BhBdlsBatch(*[a.ctypes.data for a in arrs])
+    _lib.check(_lib.lib().bh_verify_bdls(CURVE_ID[curve], ctypes.byref(b), n,
+                                         bitmap.ctypes.data, reason.ctypes.data))
+    want = [r["reason"] for r in gold] * reps + [0] * rb.n
+    bad = [(k, int(g), w) for k, (g, w) in enumerate(zip(reason, want)) if g != w]
+    assert not bad[:10]
+    valid = np.unpackbits(bitmap, bitorder="little")[:n].astype(bool)
+    assert (valid == (np.array(want) == 0)).all()
