@@ -24,7 +24,7 @@ BH_CURVE_SECP256K1 = 1
 # Every symbol include/bdls_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = (
     "bh_init", "bh_shutdown", "bh_device_count", "bh_last_error", "bh_version",
-    "bh_workspace_bytes", "bh_verify", "bh_verify_dev", "bh_csp_verify_p256",
+    "bh_workspace_bytes", "bh_verify", "bh_verify_2seg", "bh_verify_dev", "bh_csp_verify_p256",
     "bh_parse_der_sig", "bh_dev_alloc", "bh_dev_free", "bh_memcpy_h2d", "bh_memcpy_d2h",
     "bh_sync", "bh_verify_bdls", "bh_verify_bdls_dev", "bh_keys_reserve", "bh_keys_register",
     "bh_keys_clear", "bh_keys_count", "bh_timing_begin", "bh_timing_end", "bh_bdls_preverify",
@@ -121,6 +121,8 @@ def lib() -> ctypes.CDLL:
         L.bh_workspace_bytes.restype = sz
         L.bh_verify.argtypes = [i32, ctypes.POINTER(BhBatch), sz, u32, vp, vp]
         L.bh_verify.restype = i32
+        L.bh_verify_2seg.argtypes = [i32, ctypes.POINTER(BhBatch), vp, vp, sz, u32, vp, vp]
+        L.bh_verify_2seg.restype = i32
         L.bh_verify_submit.argtypes = [i32, ctypes.POINTER(BhBatch), sz, u32, vp, vp,
                                        ctypes.POINTER(vp)]
         L.bh_verify_submit.restype = i32

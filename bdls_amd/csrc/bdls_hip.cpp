@@ -379,6 +379,19 @@ bh::BdlsIn slice(const bh_bdls_batch* b, size_t base, uint32_t flags) {
                     b->s, b->s_off + base, b->s_len + base, b->version + base,
                     b->msg, b->msg_off + base, b->msg_len + base, flags};
 }
+// bh_verify_2seg: a bh_batch whose message i is msg[msg_off, +msg_len) ||
+// msg[msg2_off, +msg2_len) (host representation; device copy has the same shape).
+struct SegBatch {
+  bh_batch b;
+  const uint64_t* msg2_off;
+  const uint32_t* msg2_len;
+};
+bh::BatchIn slice(const SegBatch* b, size_t base, uint32_t flags) {
+  bh::BatchIn in = slice(&b->b, base, flags);
+  in.msg2_off = b->msg2_off + base;
+  in.msg2_len = b->msg2_len + base;
+  return in;
+}
 hipError_t launch(int curve, const bh::BatchIn& in, const bh::Work& w, const bh::Plan& pl,
                   const bh::KeyReg& g, const uint32_t* gtab, uint32_t n, const bh::LaunchOpts& o,
                   uint64_t* bm, uint8_t* rs, hipStream_t s, hipEvent_t* ev) {
@@ -527,6 +540,27 @@ bh_batch upload(Uploader& u, const bh_batch* b, size_t lo, size_t m, const HostF
   d.msg_len = u.put(b->msg_len + lo, m);
   d.sig = u.put(b->sig, f.var[0]);
   d.msg = u.put(b->msg, f.var[1]);
+  return d;
+}
+
+// message bytes of both spans: one staged range [min start, max end)
+HostFields fields(const SegBatch* b, size_t lo, size_t m) {
+  HostFields f = fields(&b->b, lo, m);
+  const VarField v2 = span(b->msg2_off, b->msg2_len, lo, m);
+  VarField& v = f.var[1];
+  const uint64_t a = std::min(v.lo, v2.lo), z = std::max(v.lo + v.bytes, v2.lo + v2.bytes);
+  f.bytes -= round256(v.bytes + 1);
+  v.lo = a;
+  v.bytes = z - a;
+  f.bytes += round256(v.bytes + 1) + 2 * round256(m * 8 + 1);
+  return f;
+}
+
+SegBatch upload(Uploader& u, const SegBatch* b, size_t lo, size_t m, const HostFields& f) {
+  SegBatch d;
+  d.b = upload(u, &b->b, lo, m, f);
+  d.msg2_off = u.put(b->msg2_off + lo, m);
+  d.msg2_len = u.put(b->msg2_len + lo, m);
   return d;
 }
 
@@ -972,6 +1006,22 @@ int bh_verify(int curve, const bh_batch* b, size_t n, uint32_t flags, uint8_t* b
   if (int rc = check_flags(flags)) return rc;
   if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
   return host_verify(curve, b, n, flags, bitmap, reason);
+}
+
+int bh_verify_2seg(int curve, const bh_batch* b, const uint64_t* msg2_off,
+                   const uint32_t* msg2_len, size_t n, uint32_t flags, uint8_t* bitmap,
+                   uint8_t* reason) {
+  if (!b || (n && (!b->pub || !b->sig_off || !b->sig_len || !b->msg_off || !b->msg_len ||
+                   !msg2_off || !msg2_len || !bitmap || !reason)))
+    return fail(BH_E_INVALID, "null pointer in batch");
+  if (curve != BH_CURVE_P256) return fail(BH_E_INVALID, "curve not supported by bh_verify_2seg");
+  if (int rc = check_flags(flags)) return rc;
+  if (!(flags & (BH_F_HASH_SHA256 | BH_F_HASH_SHA3_256)))
+    return fail(BH_E_INVALID, "bh_verify_2seg hashes on the device: pass BH_F_HASH_SHA256 or "
+                              "BH_F_HASH_SHA3_256");
+  if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
+  const SegBatch sb{*b, msg2_off, msg2_len};
+  return host_verify(curve, &sb, n, flags, bitmap, reason);
 }
 
 int bh_verify_submit(int curve, const bh_batch* b, size_t n, uint32_t flags, uint8_t* bitmap,

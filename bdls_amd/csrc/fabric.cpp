@@ -31,11 +31,15 @@
 // public key; an identity this code cannot resolve is reported as such and
 // left to the Go path (the verified set never claims what it did not check).
 #include <algorithm>
+#include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -569,6 +573,7 @@ struct Ident {
   bool ok = false;
   uint8_t pub[64];
   std::string key;
+  uint64_t key_id = 0;  // interned key (IdentCache): equal keys <=> equal ids
 };
 
 constexpr uint32_t kP256HalfN[8] = {0x7e3192a8, 0x79dce561, 0xd38bcf42, 0xde737d56,
@@ -629,17 +634,26 @@ using IdentP = std::shared_ptr<const Ident>;
 // 64-bit hash of a byte span (8 bytes per step, no copy): identities are
 // ~0.9 KB PEM certificates looked up twice or more per transaction.
 uint64_t span_hash(const uint8_t* p, size_t n) {
+  // Serialized identities are ~1 KB PEM certificates that share long
+  // prefixes: hash the length and 16 words spread over the span (the tail
+  // holds the certificate signature) instead of a serial multiply chain over
+  // every byte (4 lookups per transaction made that half the block decode).
+  // Every hit is confirmed by a full compare, so this only spreads buckets.
   uint64_t h = 0x9e3779b97f4a7c15ull ^ n;
-  size_t i = 0;
-  for (; i + 8 <= n; i += 8) {
+  if (n < 8) {
+    uint64_t v = 0;
+    memcpy(&v, p, n);
+    h = (h ^ v) * 0xc4ceb9fe1a85ec53ull;
+    return h ^ (h >> 29);
+  }
+  const size_t step = n <= 128 ? 8 : (n - 8) / 15;
+  const size_t cnt = n <= 128 ? (n - 8) / 8 + 1 : 16;
+  for (size_t k = 0; k < cnt; k++) {
     uint64_t v;
-    memcpy(&v, p + i, 8);
+    memcpy(&v, p + (k == cnt - 1 ? n - 8 : k * step), 8);
     h = (h ^ v) * 0xff51afd7ed558ccdull;
     h ^= h >> 32;
   }
-  uint64_t v = 0;
-  memcpy(&v, p + i, n - i);
-  h = (h ^ v) * 0xc4ceb9fe1a85ec53ull;
   return h ^ (h >> 29);
 }
 
@@ -651,24 +665,40 @@ struct IdentEntry {
 // Long-lived cache of resolved identities (the device-side twin of the MSP's
 // deserializer cache, msp/cache/cache.go): serialized bytes -> Ident. Callers
 // hold one Session for a whole block / batch: one lock, no copies on a hit.
+// Dedup keys are interned to integers (Ident::key_id), so the signature-set
+// replay compares ids instead of ~1 KB strings. Both maps are only cleared
+// when a session starts (never in the middle of one), so the identities one
+// call resolves always agree on their ids.
 struct IdentCache {
   std::mutex mu;
   std::unordered_multimap<uint64_t, IdentEntry> m;
+  std::unordered_map<std::string, uint64_t> keys;
+  uint64_t next_key = 1;
   static constexpr size_t kCap = 1 << 16;
   struct Session {
     IdentCache& c;
     std::lock_guard<std::mutex> g;
-    explicit Session(IdentCache& cc) : c(cc), g(cc.mu) {}
+    explicit Session(IdentCache& cc) : c(cc), g(cc.mu) {
+      if (c.m.size() >= kCap || c.keys.size() >= kCap) {
+        c.m.clear();
+        c.keys.clear();
+      }
+    }
     IdentP get(Span ser) {
       const uint64_t h = span_hash(ser.p, ser.n);
       auto r = c.m.equal_range(h);
       for (auto it = r.first; it != r.second; ++it)
         if (it->second.bytes.size() == ser.n && !memcmp(it->second.bytes.data(), ser.p, ser.n))
           return it->second.id;
-      if (c.m.size() >= kCap) c.m.clear();
-      IdentP id = std::make_shared<const Ident>(resolve(ser));
-      c.m.emplace(h, IdentEntry{std::string((const char*)ser.p, ser.n), id});
-      return id;
+      Ident id = resolve(ser);
+      if (id.ok) {
+        auto k = c.keys.emplace(id.key, c.next_key);
+        if (k.second) c.next_key++;
+        id.key_id = k.first->second;
+      }
+      IdentP p = std::make_shared<const Ident>(std::move(id));
+      c.m.emplace(h, IdentEntry{std::string((const char*)ser.p, ser.n), p});
+      return p;
     }
   };
 };
@@ -683,20 +713,41 @@ IdentCache& ident_cache() {
 // signed bytes (up to three pieces, concatenated) and the signature.
 struct SdEntry {
   IdentP id;  // resolved identity (id->ok false: DeserializeIdentity fails)
+  Span id_ser;  // serialized identity (block decode resolves it after parsing)
   Span seg[3];
   int nseg = 0;
   Span sig;
   uint8_t out = BH_SP_NOT_VERIFIED;
 };
 
-// One device batch of signatures (messages hashed on the device).
+// One device batch of signatures (messages hashed on the device). With `base`
+// set (a serialized block), signatures and the one or two message spans of
+// every record index that buffer directly (bh_verify_2seg): no host copy of
+// the signed bytes, and one upload of the block instead of their
+// concatenation. Otherwise pieces are concatenated into `msg` / `sig`.
 struct Batch {
+  const uint8_t* base = nullptr;
+  size_t base_len = 0;
   std::vector<uint8_t> pub, sig, msg;
-  std::vector<uint64_t> sig_off, msg_off;
-  std::vector<uint32_t> sig_len, msg_len;
+  std::vector<uint64_t> sig_off, msg_off, msg2_off;
+  std::vector<uint32_t> sig_len, msg_len, msg2_len;
   std::vector<uint8_t*> dst;  // where each record's reason goes
+  uint64_t rel(Span x) const {  // offset of a span inside base (empty spans: 0)
+    return x.n ? (uint64_t)(x.p - base) : 0u;
+  }
+  bool inside(Span x) const { return !x.n || (x.p >= base && x.p + x.n <= base + base_len); }
   void add(const uint8_t pub64[64], Span s, const Span* m, int nm, uint8_t* out) {
     pub.insert(pub.end(), pub64, pub64 + 64);
+    dst.push_back(out);
+    if (base) {  // every span of a block's SignedData lies in the block
+      sig_off.push_back(rel(s));
+      sig_len.push_back((uint32_t)s.n);
+      msg_off.push_back(nm > 0 ? rel(m[0]) : 0u);
+      msg_len.push_back(nm > 0 ? (uint32_t)m[0].n : 0u);
+      msg2_off.push_back(nm > 1 ? rel(m[1]) : 0u);
+      msg2_len.push_back(nm > 1 ? (uint32_t)m[1].n : 0u);
+      return;
+    }
     sig_off.push_back(sig.size());
     sig_len.push_back((uint32_t)s.n);
     if (s.n) sig.insert(sig.end(), s.p, s.p + s.n);
@@ -707,7 +758,12 @@ struct Batch {
       L += m[k].n;
     }
     msg_len.push_back((uint32_t)L);
-    dst.push_back(out);
+  }
+  // zero-copy needs every span inside base and at most two message pieces
+  bool fits(const SdEntry& e) const {
+    bool ok = e.nseg <= 2 && inside(e.sig);
+    for (int k = 0; k < e.nseg; k++) ok = ok && inside(e.seg[k]);
+    return ok;
   }
   void add(SdEntry& e) { add(e.id->pub, e.sig, e.seg, e.nseg, &e.out); }
   void reserve(size_t n, size_t msg_bytes, size_t sig_bytes) {
@@ -717,19 +773,32 @@ struct Batch {
     msg_off.reserve(n);
     msg_len.reserve(n);
     dst.reserve(n);
-    msg.reserve(msg_bytes + 1);
-    sig.reserve(sig_bytes + 1);
+    if (base) {
+      msg2_off.reserve(n);
+      msg2_len.reserve(n);
+    } else {
+      msg.reserve(msg_bytes + 1);
+      sig.reserve(sig_bytes + 1);
+    }
   }
   size_t size() const { return dst.size(); }
   int run(uint32_t flags) {
     const size_t n = size();
     if (!n) return BH_OK;
     std::vector<uint8_t> bitmap((n + 7) / 8), reason(n);
-    sig.push_back(0);
-    msg.push_back(0);
-    bh_batch b{pub.data(), sig.data(), sig_off.data(), sig_len.data(),
-               msg.data(), msg_off.data(), msg_len.data()};
-    int rc = bh_verify(BH_CURVE_P256, &b, n, flags, bitmap.data(), reason.data());
+    int rc;
+    if (base) {
+      bh_batch b{pub.data(), base, sig_off.data(), sig_len.data(),
+                 base, msg_off.data(), msg_len.data()};
+      rc = bh_verify_2seg(BH_CURVE_P256, &b, msg2_off.data(), msg2_len.data(), n, flags,
+                          bitmap.data(), reason.data());
+    } else {
+      sig.push_back(0);
+      msg.push_back(0);
+      bh_batch b{pub.data(), sig.data(), sig_off.data(), sig_len.data(),
+                 msg.data(), msg_off.data(), msg_len.data()};
+      rc = bh_verify(BH_CURVE_P256, &b, n, flags, bitmap.data(), reason.data());
+    }
     if (rc) return rc;
     for (size_t i = 0; i < n; i++) *dst[i] = reason[i];
     return BH_OK;
@@ -751,6 +820,10 @@ int verify_sets(std::vector<SdEntry>& e, const std::vector<SetRange>& sets, uint
                 bool decode_only, std::vector<uint32_t>* valid, Batch* extra) {
   Batch b;
   if (extra) b = std::move(*extra);
+  if (b.base)  // a record that does not index the block goes the copying way
+    for (const SdEntry& x : e)
+      if (x.id && x.id->ok && !b.fits(x))
+        return bh::host_fail(BH_E_INVALID, "span outside the block");
   {
     size_t bytes = 0, sig_bytes = 0;
     for (const SdEntry& x : e) {
@@ -759,18 +832,17 @@ int verify_sets(std::vector<SdEntry>& e, const std::vector<SetRange>& sets, uint
     }
     b.reserve(b.size() + e.size(), b.msg.size() + bytes, b.sig.size() + sig_bytes);
   }
+  std::vector<uint64_t> seen, ok;
   for (const SetRange& r : sets) {
-    std::vector<const std::string*> seen;
+    seen.clear();
     for (size_t i = r.first; i < r.first + r.count; i++) {
       SdEntry& x = e[i];
       if (!x.id || !x.id->ok) {
         x.out = BH_FAB_E_BAD_IDENTITY;
         continue;
       }
-      bool dup = false;
-      for (const std::string* k : seen) dup |= (*k == x.id->key);
-      if (dup) continue;
-      seen.push_back(&x.id->key);
+      if (std::find(seen.begin(), seen.end(), x.id->key_id) != seen.end()) continue;
+      seen.push_back(x.id->key_id);
       b.add(x);
     }
   }
@@ -779,15 +851,15 @@ int verify_sets(std::vector<SdEntry>& e, const std::vector<SetRange>& sets, uint
   valid->assign(sets.size(), 0);
   for (int round = 0; round < 256; round++) {
     Batch more;
+    more.base = b.base;
+    more.base_len = b.base_len;
     for (size_t k = 0; k < sets.size(); k++) {
       const SetRange& r = sets[k];
-      std::vector<const std::string*> ok;
+      ok.clear();
       for (size_t i = r.first; i < r.first + r.count; i++) {
         SdEntry& x = e[i];
         if (!x.id || !x.id->ok) continue;
-        bool dup = false;
-        for (const std::string* key : ok) dup |= (*key == x.id->key);
-        if (dup) {
+        if (std::find(ok.begin(), ok.end(), x.id->key_id) != ok.end()) {
           x.out = BH_FAB_E_DUPLICATE;
           continue;
         }
@@ -795,7 +867,7 @@ int verify_sets(std::vector<SdEntry>& e, const std::vector<SetRange>& sets, uint
           if (!decode_only) more.add(x);
           break;  // later entries of this set depend on its result
         }
-        if (x.out == BH_R_OK) ok.push_back(&x.id->key);
+        if (x.out == BH_R_OK) ok.push_back(x.id->key_id);
       }
       (*valid)[k] = (uint32_t)ok.size();
     }
@@ -815,6 +887,9 @@ struct TxRec {
   int32_t status = BH_FAB_OK;
   int32_t type = 0;
   bool creator_check = false;  // creator signature goes to the device
+  bool resolve_creator = false;  // creator identity still to be resolved
+  int32_t post_status = BH_FAB_OK;  // status if the creator identity resolves
+  Span creator_ser;
   IdentP creator;
   Span payload, signature;
   uint8_t creator_out = BH_SP_NOT_VERIFIED;
@@ -824,8 +899,9 @@ struct TxRec {
 // Go's order of checks up to the signatures (validateTx, ValidateTransaction,
 // validateEndorserTransaction). Checks that do not gate which signatures are
 // verified (CheckTxID, the proposal hash, ledger / channel state) are left to
-// the unchanged validator.
-void decode_tx(Span env_bytes, TxRec* t, std::vector<SdEntry>* ends, IdentCache::Session& ic) {
+// the unchanged validator. Pure parsing (no identity lookups), so transactions
+// decode in parallel; resolve_tx then applies the identity outcomes in order.
+void decode_tx(Span env_bytes, TxRec* t, std::vector<SdEntry>* ends) {
   t->end_first = ends->size();
   Envelope env;
   if (!dec_envelope(env_bytes, &env)) {
@@ -849,18 +925,18 @@ void decode_tx(Span env_bytes, TxRec* t, std::vector<SdEntry>* ends, IdentCache:
     return;
   }
   t->type = ch.type;
-  // checkSignatureFromCreator: nil arguments, then DeserializeIdentity, Verify
+  // checkSignatureFromCreator: nil arguments, then DeserializeIdentity (in
+  // resolve_tx: BH_FAB_CREATOR_IDENTITY overrides everything below), Verify
   t->payload = env.payload;
   t->signature = env.signature;
   if (!env.signature.set || !env.payload.set) {
     t->status = BH_FAB_CREATOR_SIGNATURE;  // "nil arguments"
   } else {
-    t->creator = ic.get(sh.creator);
-    if (!t->creator->ok) t->status = BH_FAB_CREATOR_IDENTITY;
-    else t->creator_check = true;
+    t->creator_ser = sh.creator;
+    t->resolve_creator = true;
   }
   if (ch.type == 2) {  // CONFIG_UPDATE: UNSUPPORTED_TX_PAYLOAD after the creator check
-    if (t->status == BH_FAB_OK) t->status = BH_FAB_UNSUPPORTED;
+    t->post_status = BH_FAB_UNSUPPORTED;
     return;
   }
   if (ch.type != 3) return;  // CONFIG: no endorsements
@@ -880,14 +956,14 @@ void decode_tx(Span env_bytes, TxRec* t, std::vector<SdEntry>* ends, IdentCache:
       tx_status = BH_FAB_TX;
   }
   if (tx_status != BH_FAB_OK) {
-    if (t->status == BH_FAB_OK) t->status = tx_status;
+    t->post_status = tx_status;
     return;
   }
   for (const Endorsement& en : ap.action.endorsements) {
     // SignedData{data: prp || endorser, identity: endorser, signature}
     // (validator_keylevel.go:246-260)
     SdEntry x;
-    x.id = ic.get(en.endorser);
+    x.id_ser = en.endorser;
     x.seg[0] = ap.action.prp;
     x.seg[1] = en.endorser;
     x.nseg = 2;
@@ -895,6 +971,138 @@ void decode_tx(Span env_bytes, TxRec* t, std::vector<SdEntry>* ends, IdentCache:
     ends->push_back(x);
   }
   t->end_count = ends->size() - t->end_first;
+}
+
+// The sequential half of decode_tx: identities (the long-lived cache, through
+// a per-block memo: a block repeats a few identities thousands of times).
+struct IdentMemo {
+  IdentCache::Session& ic;
+  std::unordered_multimap<uint64_t, std::pair<Span, IdentP>> m;
+  explicit IdentMemo(IdentCache::Session& s) : ic(s) { m.reserve(256); }
+  IdentP get(Span ser) {
+    const uint64_t h = span_hash(ser.p, ser.n);
+    auto r = m.equal_range(h);
+    for (auto it = r.first; it != r.second; ++it) {
+      const Span& k = it->second.first;
+      if (k.n == ser.n && (k.p == ser.p || !memcmp(k.p, ser.p, ser.n))) return it->second.second;
+    }
+    IdentP id = ic.get(ser);
+    m.emplace(h, std::make_pair(ser, id));
+    return id;
+  }
+};
+
+void resolve_tx(TxRec* t, SdEntry* ends, IdentMemo& memo) {
+  if (t->resolve_creator) {
+    t->creator = memo.get(t->creator_ser);
+    if (!t->creator->ok) {
+      t->status = BH_FAB_CREATOR_IDENTITY;
+    } else {
+      t->creator_check = true;
+      if (t->status == BH_FAB_OK) t->status = t->post_status;
+    }
+  } else if (t->status == BH_FAB_OK) {
+    t->status = t->post_status;
+  }
+  for (size_t k = 0; k < t->end_count; k++) ends[t->end_first + k].id = memo.get(ends[t->end_first + k].id_ser);
+}
+
+// Small persistent worker pool for the block decode (parallel_for over chunk
+// indices; the calling thread takes chunks too). Size: BH_DECODE_THREADS, else
+// min(4, hardware threads) -- the peer's validator shares the host.
+class Pool {
+ public:
+  static Pool& get() {
+    static Pool* p = new Pool();
+    return *p;
+  }
+  size_t size() const { return th_.size() + 1; }
+  void run(size_t tasks, const std::function<void(size_t)>& fn) {
+    if (tasks <= 1 || th_.empty()) {
+      for (size_t k = 0; k < tasks; k++) fn(k);
+      return;
+    }
+    std::unique_lock<std::mutex> call(call_mu_);  // one parallel_for at a time
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      fn_ = &fn;
+      next_ = 0;
+      tasks_ = tasks;
+      left_ = tasks;
+      gen_++;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [&] { return left_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  Pool() {
+    size_t n = std::min<size_t>(4, std::max(1u, std::thread::hardware_concurrency()));
+    if (const char* e = getenv("BH_DECODE_THREADS")) n = std::max(1L, std::min(64L, atol(e)));
+    for (size_t k = 1; k < n; k++) th_.emplace_back([this] { loop(); });
+    for (auto& t : th_) t.detach();
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  void work() {
+    for (;;) {
+      size_t k;
+      const std::function<void(size_t)>* fn;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (!fn_ || next_ >= tasks_) return;
+        k = next_++;
+        fn = fn_;
+      }
+      (*fn)(k);
+      std::lock_guard<std::mutex> g(mu_);
+      if (--left_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_, call_mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(size_t)>* fn_ = nullptr;
+  size_t next_ = 0, tasks_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+};
+
+// Decode every transaction (parallel chunks), then resolve identities in
+// order; ends gets each transaction's endorsements contiguously, in order.
+void decode_block_txs(const std::vector<Span>& data, std::vector<TxRec>* t,
+                      std::vector<SdEntry>* ends) {
+  const size_t n = data.size();
+  Pool& pool = Pool::get();
+  const size_t chunks = std::min<size_t>(n / 16 + 1, 4 * pool.size());
+  std::vector<std::vector<SdEntry>> part(chunks);
+  pool.run(chunks, [&](size_t c) {
+    const size_t lo = n * c / chunks, hi = n * (c + 1) / chunks;
+    part[c].reserve((hi - lo) * 4);
+    for (size_t i = lo; i < hi; i++) decode_tx(data[i], &(*t)[i], &part[c]);
+  });
+  size_t total = 0;
+  for (auto& p : part) total += p.size();
+  ends->reserve(total);
+  for (size_t c = 0; c < chunks; c++) {
+    const size_t lo = n * c / chunks, hi = n * (c + 1) / chunks, base = ends->size();
+    for (size_t i = lo; i < hi; i++) (*t)[i].end_first += base;
+    ends->insert(ends->end(), part[c].begin(), part[c].end());
+  }
+  IdentCache::Session ic(ident_cache());
+  IdentMemo memo(ic);
+  for (size_t i = 0; i < n; i++) resolve_tx(&(*t)[i], ends->data(), memo);
 }
 
 // ---------------------------------------------------------------- x509
@@ -1075,11 +1283,7 @@ extern "C" int bh_fabric_block_preverify(const uint8_t* block, size_t len, uint3
     return bh::host_fail(BH_E_INVALID, "block does not unmarshal (common.Block)");
   std::vector<TxRec> t(data.size());
   std::vector<SdEntry> ends;
-  ends.reserve(data.size() * 4);
-  {
-    IdentCache::Session ic(ident_cache());
-    for (size_t i = 0; i < data.size(); i++) decode_tx(data[i], &t[i], &ends, ic);
-  }
+  decode_block_txs(data, &t, &ends);
   *n_tx = t.size();
   *n_endorse = ends.size();
   if ((t.size() && (!txs || tx_cap < t.size())) ||
@@ -1089,6 +1293,8 @@ extern "C" int bh_fabric_block_preverify(const uint8_t* block, size_t len, uint3
   // one device batch: every creator signature and the first round of every
   // transaction's endorsement set
   Batch creators;
+  creators.base = block;  // every signed span of the block's SignedData lies in the block
+  creators.base_len = len;
   {
     size_t bytes = 0, sig_bytes = 0;
     for (const TxRec& x : t) {

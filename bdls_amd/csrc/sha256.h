@@ -102,4 +102,54 @@ BH_HD void sha256_msg(uint32_t out[8], const uint8_t* m, uint64_t len) {
   for (int i = 0; i < 8; i++) out[i] = h[i];
 }
 
+// ---- two-span messages: m1[0, l1) || m2[0, l2) hashed as one message (a
+// Fabric SignedData prp || endorser, validator_keylevel.go:246-260, without a
+// host-side concatenation). Blocks inside one span load as above; only the
+// block straddling the seam and the padding go byte by byte.
+BH_HD uint32_t msg2_byte(const uint8_t* m1, uint64_t l1, const uint8_t* m2, uint64_t p) {
+  return p < l1 ? m1[p] : m2[p - l1];
+}
+
+BH_HD uint32_t sha256_word2(const uint8_t* m1, uint64_t l1, const uint8_t* m2, uint64_t len,
+                            uint64_t total, uint64_t pos) {
+  uint32_t w = 0;
+  const uint64_t bits = len * 8;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint64_t p = pos + k;
+    uint32_t byte;
+    if (p < len) byte = msg2_byte(m1, l1, m2, p);
+    else if (p == len) byte = 0x80u;
+    else if (p >= total - 8) byte = (uint32_t)(bits >> (8 * (total - 1 - p))) & 0xffu;
+    else byte = 0;
+    w = (w << 8) | byte;
+  }
+  return w;
+}
+
+BH_HD void sha256_msg2(uint32_t out[8], const uint8_t* m1, uint64_t l1, const uint8_t* m2,
+                       uint64_t l2) {
+  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  const uint64_t len = l1 + l2;
+  const uint64_t total = ((len + 9 + 63) / 64) * 64;
+  for (uint64_t blk = 0; blk < total; blk += 64) {
+    uint32_t w[16];
+    const uint8_t* src = blk + 64 <= l1 ? m1 + blk
+                         : (blk >= l1 && blk + 64 <= len) ? m2 + (blk - l1)
+                                                          : nullptr;
+    if (src) {
+      load_le_words<16>(w, src);
+#pragma unroll
+      for (int i = 0; i < 16; i++) w[i] = bswap32(w[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; i++) w[i] = sha256_word2(m1, l1, m2, len, total, blk + 4 * i);
+    }
+    sha256_block(h, w);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = h[i];
+}
+
 }  // namespace bh

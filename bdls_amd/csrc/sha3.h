@@ -152,4 +152,55 @@ BH_HD void sha3_256_msg(uint8_t out[32], const uint8_t* m, uint64_t len) {
   }
 }
 
+// Two-span message (see sha256.h sha256_msg2): m1[0, l1) || m2[0, l2).
+BH_HD uint32_t sha3_word2(const uint8_t* m1, uint64_t l1, const uint8_t* m2, uint64_t len,
+                          uint64_t total, uint64_t pos) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint64_t p = pos + k;
+    uint32_t byte = 0;
+    if (p < len) byte = p < l1 ? m1[p] : m2[p - l1];
+    else if (p == len) byte = 0x06u;
+    if (p == total - 1) byte |= 0x80u;
+    v |= byte << (8 * k);
+  }
+  return v;
+}
+
+BH_HD void sha3_256_msg2(uint8_t out[32], const uint8_t* m1, uint64_t l1, const uint8_t* m2,
+                         uint64_t l2) {
+  K64 a[25];
+#pragma unroll
+  for (int i = 0; i < 25; i++) a[i] = K64{0u, 0u};
+  const uint64_t len = l1 + l2;
+  const uint64_t total = (len / kSha3Rate + 1) * kSha3Rate;
+  for (uint64_t blk = 0; blk < total; blk += kSha3Rate) {
+    uint32_t w[34];
+    const uint8_t* src = blk + kSha3Rate <= l1 ? m1 + blk
+                         : (blk >= l1 && blk + kSha3Rate <= len) ? m2 + (blk - l1)
+                                                                 : nullptr;
+    if (src) {
+      load_le_words<34>(w, src);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 34; i++) w[i] = sha3_word2(m1, l1, m2, len, total, blk + 4 * i);
+    }
+#pragma unroll
+    for (int i = 0; i < 17; i++) {
+      a[i].lo ^= w[2 * i];
+      a[i].hi ^= w[2 * i + 1];
+    }
+    keccak_f1600(a);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      out[8 * i + k] = (uint8_t)(a[i].lo >> (8 * k));
+      out[8 * i + 4 + k] = (uint8_t)(a[i].hi >> (8 * k));
+    }
+  }
+}
+
 }  // namespace bh

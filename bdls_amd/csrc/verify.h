@@ -46,6 +46,10 @@ struct BatchIn {  // device pointers (see include/bdls_hip.h bh_batch)
   const uint64_t* msg_off;
   const uint32_t* msg_len;
   uint32_t flags;
+  // optional second message span (bh_verify_2seg): message i is
+  // msg[msg_off, +msg_len) || msg[msg2_off, +msg2_len); nullptr = one span
+  const uint64_t* msg2_off = nullptr;
+  const uint32_t* msg2_len = nullptr;
 };
 
 // BDLS consensus messages: vendor/github.com/BDLS-bft/bdls/message.go SignedProto
@@ -219,13 +223,16 @@ BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
   // ---- digest -> e (hashToNat: left-most 32 bytes, reduced mod n)
   if (reason == R_OK) {
     const uint8_t* m = in.msg + in.msg_off[i];
+    const uint32_t mlen2 = in.msg2_len ? in.msg2_len[i] : 0u;  // fused modes only
     if constexpr (HK == HK_SHA3_256) {
       uint8_t hb[32];
-      sha3_256_msg(hb, m, mlen);
+      if (mlen2) sha3_256_msg2(hb, m, mlen, in.msg + in.msg2_off[i], mlen2);
+      else sha3_256_msg(hb, m, mlen);
       be32_to_limbs(e, hb);  // hashToNat: the 32-byte digest, big-endian
     } else if (fused) {
       uint32_t h[8];
-      sha256_msg(h, m, mlen);
+      if (mlen2) sha256_msg2(h, m, mlen, in.msg + in.msg2_off[i], mlen2);
+      else sha256_msg(h, m, mlen);
 #pragma unroll
       for (int k = 0; k < 8; k++) e[k] = h[7 - k];
     } else {

@@ -112,6 +112,17 @@ size_t bh_workspace_bytes(size_t n);
 int bh_verify(int curve, const bh_batch *b, size_t n, uint32_t flags, uint8_t *bitmap,
               uint8_t *reason);
 
+/* bh_verify with two-span messages: record i's signed bytes are
+ * msg[msg_off[i], +msg_len[i]) || msg[msg2_off[i], +msg2_len[i]) (msg2_len 0 =
+ * one span), hashed on the device (BH_F_HASH_SHA256 or BH_F_HASH_SHA3_256
+ * required). Replaces the host-side concatenation of a Fabric endorsement's
+ * SignedData, Data = prp || endorser (core/common/validation/statebased/
+ * validator_keylevel.go:246-260; core/committer/txvalidator/v20/plugindispatcher),
+ * so both spans can point into the serialized block itself. */
+int bh_verify_2seg(int curve, const bh_batch *b, const uint64_t *msg2_off,
+                   const uint32_t *msg2_len, size_t n, uint32_t flags, uint8_t *bitmap,
+                   uint8_t *reason);
+
 /* Asynchronous form of bh_verify (the pipelined BatchVerify): enqueues the
  * upload (copy stream), the verify passes and the result download (compute
  * stream) on every device and returns at once with *job. bh_verify_wait(job)

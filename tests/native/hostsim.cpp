@@ -166,6 +166,17 @@ extern "C" int hs_verify2(const uint8_t* pub, const uint8_t* sig, const uint64_t
 // secp256k1 with the Fabric record layout but BHF_NO_LOW_S and a caller-chosen
 // digest: reaches the curve-level edge cases (x wrap, infinity, u1 G == u2 Q)
 // that BLAKE2b-hashed BDLS messages cannot be steered into.
+// bh_verify_2seg's two-span messages: msg[moff, +mlen) || msg[m2off, +m2len)
+extern "C" int hs_verify_2seg(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
+                              const uint32_t* slen, const uint8_t* msg, const uint64_t* moff,
+                              const uint32_t* mlen, const uint64_t* m2off, const uint32_t* m2len,
+                              uint32_t n, uint32_t flags, uint8_t* reason) {
+  BatchIn in{pub, sig, soff, slen, msg, moff, mlen, flags};
+  in.msg2_off = m2off;
+  in.msg2_len = m2len;
+  return run_seq<F30_p256, Fn_p256, Cv_p256>(in, n, 4, kMinUses, reason, nullptr);
+}
+
 extern "C" int hs_verify_k1_digest(const uint8_t* pub, const uint8_t* sig, const uint64_t* soff,
                                    const uint32_t* slen, const uint8_t* dg, const uint64_t* doff,
                                    const uint32_t* dlen, uint32_t n, uint32_t min_uses,

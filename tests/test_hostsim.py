@@ -109,3 +109,43 @@ def test_hostsim_workload_sha3(hs):
     assert (out == w.reason).all()
     out2 = run(hs, w.arrays(), True, 8)
     assert (out2[w.reason == 0] != 0).all()
+
+
+def split_layout(msgs, seed):
+    """Each message m as two spans (m[:k], m[k:]) at seam k (0, 1, block
+    edges, len, random), laid out second span first with random gaps, as
+    bh_verify_2seg sees a block's prp / endorser fields."""
+    rng = np.random.default_rng(seed)
+    buf, off1, len1, off2, len2 = bytearray(), [], [], [], []
+    for i, m in enumerate(msgs):
+        choices = [0, 1, 55, 56, 63, 64, 65, 128, len(m) - 1, len(m), int(rng.integers(0, len(m) + 1))]
+        k = min(len(m), max(0, choices[i % len(choices)]))
+        a, b = m[:k], m[k:]
+        buf += bytes(int(rng.integers(0, 7)))
+        off2.append(len(buf)); len2.append(len(b)); buf += b
+        buf += bytes(int(rng.integers(0, 7)))
+        off1.append(len(buf)); len1.append(len(a)); buf += a
+    buf += b"\0"
+    return (np.frombuffer(bytes(buf), np.uint8), np.array(off1, np.uint64), np.array(len1, np.uint32),
+            np.array(off2, np.uint64), np.array(len2, np.uint32))
+
+
+@pytest.mark.parametrize("family", ["SHA2", "SHA3"])
+def test_hostsim_two_span_messages(hs, family):
+    """bh_verify_2seg's device hashing (sha256_msg2 / sha3_256_msg2): every
+    seam position gives the verdicts of the one-span message."""
+    from bdls_amd import workload
+    from bdls_amd._lib import BH_F_HASH_SHA256, BH_F_HASH_SHA3_256
+    w = workload.generate(330, 30, 300, 4, seed=17, nthreads=4, family=family)
+    pub, sig, so, sl, msg, mo, ml = w.arrays()
+    msgs = [bytes(msg[int(o):int(o) + int(l)]) for o, l in zip(mo, ml)]
+    mbuf, o1, l1, o2, l2 = split_layout(msgs, 5)
+    flags = BH_F_HASH_SHA3_256 if family == "SHA3" else BH_F_HASH_SHA256
+    vp = ctypes.c_void_p
+    hs.hs_verify_2seg.argtypes = [vp] * 9 + [ctypes.c_uint32] * 2 + [vp]
+    out = np.full(w.n, 255, np.uint8)
+    hs.hs_verify_2seg(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
+                      mbuf.ctypes.data, o1.ctypes.data, l1.ctypes.data, o2.ctypes.data,
+                      l2.ctypes.data, w.n, flags, out.ctypes.data)
+    assert (out == w.reason).all()
+    assert (l1 == 0).any() and (l2 == 0).any() and ((l1 > 64) & (l2 > 64)).any()
