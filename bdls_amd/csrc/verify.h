@@ -153,21 +153,47 @@ constexpr int kGEntry = 18;
 constexpr int kQTab = 16;
 constexpr int kQPt = 28;  // words per Jacobian point in the Q table (27 + pad)
 
+struct alignas(16) W4 {
+  uint32_t x, y, z, w;
+};
+
+// Per-record scalars / field elements (e, r, s, prefixes: 8 words; Q, r R,
+// (r + n) R: 9 words). BH_AOS (default): record-major, a record's limbs
+// contiguous -- consecutive lanes still write consecutive bytes (prep, the
+// inverse), and the key-grouped and ladder kernels, whose lanes take records
+// in list order (scattered indices), read each record from one or two cache
+// lines instead of one line per limb. Otherwise limb-major (stride ns).
+#ifndef BH_AOS
+#define BH_AOS 1
+#endif
 BH_HD void ld8(uint32_t v[8], const uint32_t* base, uint32_t i, uint32_t ns) {
+#if BH_AOS
+  const W4* p = reinterpret_cast<const W4*>(base + (size_t)i * 8);
+  const W4 a = p[0], b = p[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+#else
 #pragma unroll
   for (int k = 0; k < 8; k++) v[k] = base[(size_t)k * ns + i];
+#endif
 }
 BH_HD void st8(uint32_t* base, uint32_t i, uint32_t ns, const uint32_t v[8]) {
+#if BH_AOS
+  W4* p = reinterpret_cast<W4*>(base + (size_t)i * 8);
+  p[0] = W4{v[0], v[1], v[2], v[3]};
+  p[1] = W4{v[4], v[5], v[6], v[7]};
+#else
 #pragma unroll
   for (int k = 0; k < 8; k++) base[(size_t)k * ns + i] = v[k];
+#endif
 }
 BH_HD void ld9(uint32_t v[9], const uint32_t* base, uint32_t i, uint32_t ns) {
 #pragma unroll
-  for (int k = 0; k < 9; k++) v[k] = base[(size_t)k * ns + i];
+  for (int k = 0; k < 9; k++) v[k] = BH_AOS ? base[(size_t)i * 9 + k] : base[(size_t)k * ns + i];
 }
 BH_HD void st9(uint32_t* base, uint32_t i, uint32_t ns, const uint32_t v[9]) {
 #pragma unroll
-  for (int k = 0; k < 9; k++) base[(size_t)k * ns + i] = v[k];
+  for (int k = 0; k < 9; k++) (BH_AOS ? base[(size_t)i * 9 + k] : base[(size_t)k * ns + i]) = v[k];
 }
 
 // ------------------------------------------------------------------ prep
@@ -440,9 +466,6 @@ BH_HD void booth5(uint32_t in6, uint32_t* mag, bool* neg) {
 // ((wave * 64 + lane) * 16 + entry) * 28. A lookup is seven 16-byte loads that
 // touch ~2 cache lines per lane; the earlier lane-interleaved layout touched
 // one line per distinct digit per word (measured ~16x L2-miss traffic).
-struct alignas(16) W4 {
-  uint32_t x, y, z, w;
-};
 
 BH_HD uint32_t* qtab_entry(uint32_t* tab, uint32_t wave, uint32_t entry, uint32_t lane) {
   return tab + (((size_t)wave * 64 + lane) * kQTab + entry) * kQPt;
@@ -1050,24 +1073,29 @@ BH_HD bool stage_keycomb_q(const Work& w, uint32_t i, uint32_t j, const uint32_t
 
 // 64-bit key fingerprint of the canonical Montgomery Q (never 0).
 BH_HD uint64_t key_hash(const Work& w, uint32_t i) {
+  uint32_t qx[9], qy[9];
+  ld9(qx, w.qx, i, w.ns);
+  ld9(qy, w.qy, i, w.ns);
   uint64_t h = 0x9e3779b97f4a7c15ull;
 #pragma unroll
   for (int k = 0; k < 9; k++) {
-    h ^= w.qx[(size_t)k * w.ns + i];
+    h ^= qx[k];
     h *= 0xff51afd7ed558ccdull;
-    h ^= (uint64_t)w.qy[(size_t)k * w.ns + i] << 32;
+    h ^= (uint64_t)qy[k] << 32;
     h ^= h >> 29;
   }
   return h ? h : 1;
 }
 
 BH_HD bool same_key(const Work& w, uint32_t a, uint32_t b) {
+  uint32_t xa[9], ya[9], xb[9], yb[9];
+  ld9(xa, w.qx, a, w.ns);
+  ld9(ya, w.qy, a, w.ns);
+  ld9(xb, w.qx, b, w.ns);
+  ld9(yb, w.qy, b, w.ns);
   uint32_t d = 0;
 #pragma unroll
-  for (int k = 0; k < 9; k++) {
-    d |= w.qx[(size_t)k * w.ns + a] ^ w.qx[(size_t)k * w.ns + b];
-    d |= w.qy[(size_t)k * w.ns + a] ^ w.qy[(size_t)k * w.ns + b];
-  }
+  for (int k = 0; k < 9; k++) d |= (xa[k] ^ xb[k]) | (ya[k] ^ yb[k]);
   return d == 0;
 }
 
@@ -1099,21 +1127,24 @@ BH_HD const uint32_t* tab_ptr(const Plan& pl, const KeyReg& g, uint32_t id) {
 
 BH_HD bool reg_key_eq(const KeyReg& g, uint32_t t, const Work& w, uint32_t i) {
   const uint32_t* k = g.keys + (size_t)t * 18;
+  uint32_t qx[9], qy[9];
+  ld9(qx, w.qx, i, w.ns);
+  ld9(qy, w.qy, i, w.ns);
   uint32_t d = 0;
 #pragma unroll
-  for (int q = 0; q < 9; q++) {
-    d |= k[q] ^ w.qx[(size_t)q * w.ns + i];
-    d |= k[9 + q] ^ w.qy[(size_t)q * w.ns + i];
-  }
+  for (int q = 0; q < 9; q++) d |= (k[q] ^ qx[q]) | (k[9 + q] ^ qy[q]);
   return d == 0;
 }
 
 BH_HD void reg_key_store(const KeyReg& g, uint32_t t, const Work& w, uint32_t i) {
   uint32_t* k = g.keys + (size_t)t * 18;
+  uint32_t qx[9], qy[9];
+  ld9(qx, w.qx, i, w.ns);
+  ld9(qy, w.qy, i, w.ns);
 #pragma unroll
   for (int q = 0; q < 9; q++) {
-    k[q] = w.qx[(size_t)q * w.ns + i];
-    k[9 + q] = w.qy[(size_t)q * w.ns + i];
+    k[q] = qx[q];
+    k[9 + q] = qy[q];
   }
 }
 
