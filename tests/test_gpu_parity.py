@@ -278,3 +278,33 @@ def test_key_routing(csp, nkeys, min_frac):
     assert tm.n_keycomb >= min_frac * routed
     if nkeys >= 20_000:
         assert tm.n_keytables == 0
+
+
+@pytest.mark.parametrize("family", ["SHA2", "SHA3"])
+def test_two_span_messages(csp, family):
+    """bh_verify_2seg on the device: each message split at a seam (0, 1,
+    block / rate edges, len, random) with the second span placed first in the
+    buffer -- verdicts equal the one-span batch's; both key paths (repeated
+    keys -> key tables, unique keys -> ladder)."""
+    from bdls_amd import workload
+    from tests.test_hostsim import split_layout
+    flags = _lib.BH_F_HASH_SHA3_256 if family == "SHA3" else _lib.BH_F_HASH_SHA256
+    for nkeys in (60, 9000):
+        w = workload.generate(9000, nkeys, 300, 8, seed=41, family=family)
+        pub, sig, so, sl, msg, mo, ml = w.arrays()
+        msgs = [bytes(msg[int(o):int(o) + int(l)]) for o, l in zip(mo, ml)]
+        mbuf, o1, l1, o2, l2 = split_layout(msgs, 9)
+        b = _lib.BhBatch(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
+                         mbuf.ctypes.data, o1.ctypes.data, l1.ctypes.data)
+        bitmap = np.zeros((w.n + 7) // 8, np.uint8)
+        reason = np.full(w.n, 255, np.uint8)
+        _lib.check(_lib.lib().bh_verify_2seg(_lib.BH_CURVE_P256, ctypes.byref(b), o2.ctypes.data,
+                                             l2.ctypes.data, w.n, flags, bitmap.ctypes.data,
+                                             reason.ctypes.data))
+        assert (reason == w.reason).all(), nkeys
+        assert (np.unpackbits(bitmap, bitorder="little")[:w.n].astype(bool) ==
+                w.expected_valid).all(), nkeys
+    # a two-span batch needs device hashing
+    rc = _lib.lib().bh_verify_2seg(_lib.BH_CURVE_P256, ctypes.byref(b), o2.ctypes.data,
+                                   l2.ctypes.data, w.n, 0, bitmap.ctypes.data, reason.ctypes.data)
+    assert rc != 0
