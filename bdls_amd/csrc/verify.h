@@ -216,9 +216,46 @@ BH_HD bool key_import(const uint8_t* q, uint32_t qx30[9], uint32_t qy30[9]) {
   return j_on_curve<P>(qx30, qy30);
 }
 
+// e = hashToNat(digest) mod n for record i: the given digest, or the fused
+// SHA-256 / SHA3-256 of its (one- or two-span) message.
+template <class C, int HK>
+BH_HD void digest_e(const BatchIn& in, uint32_t i, uint32_t e[8]) {
+  const uint32_t mlen = in.msg_len[i];
+  const bool fused = HK == HK_SHA3_256 || (in.flags & BHF_HASH_SHA256) != 0;
+  const uint8_t* m = in.msg + in.msg_off[i];
+  const uint32_t mlen2 = in.msg2_len ? in.msg2_len[i] : 0u;  // fused modes only
+  if constexpr (HK == HK_SHA3_256) {
+    uint8_t hb[32];
+    if (mlen2) sha3_256_msg2(hb, m, mlen, in.msg + in.msg2_off[i], mlen2);
+    else sha3_256_msg(hb, m, mlen);
+    be32_to_limbs(e, hb);  // hashToNat: the 32-byte digest, big-endian
+  } else if (fused) {
+    uint32_t h[8];
+    if (mlen2) sha256_msg2(h, m, mlen, in.msg + in.msg2_off[i], mlen2);
+    else sha256_msg(h, m, mlen);
+#pragma unroll
+    for (int k = 0; k < 8; k++) e[k] = h[7 - k];
+  } else {
+    const uint32_t L = mlen < 32 ? mlen : 32;
+#pragma unroll
+    for (int k = 0; k < 8; k++) e[k] = 0;
+#pragma unroll
+    for (int j = 0; j < 32; j++) {  // j = byte index from the least significant end
+      uint32_t v = 0;
+      if ((uint32_t)j < L) v = m[L - 1 - j];
+      e[j >> 2] |= v << (8 * (j & 3));
+    }
+  }
+  uint32_t nn[8], t[8];
+  load_const8(nn, C::n);
+  const uint32_t bo = sub8(t, e, nn);
+  if (!bo) copy8(e, t);  // e < 2^256 < 2n: one conditional subtraction
+}
+
 // HK: HK_GIVEN_OR_SHA256 (msg is the digest, or with BHF_HASH_SHA256 the
-// message) or HK_SHA3_256 (msg is the message, SHA3-256 digest).
-template <class P, class N, class C, int HK = HK_GIVEN_OR_SHA256>
+// message) or HK_SHA3_256 (msg is the message, SHA3-256 digest). DEFER: e is
+// left to k_digest (w.e untouched; a rejected record's e is any scalar < n).
+template <class P, class N, class C, int HK = HK_GIVEN_OR_SHA256, bool DEFER = false>
 BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
   uint8_t reason = R_OK;
   uint32_t r[8], s[8], e[8];
@@ -246,36 +283,9 @@ BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
     reason = R_BAD_KEY;
   if (reason == R_OK && (ds.r_big || geq8(r, nn))) reason = R_R_RANGE;
   if (reason == R_OK && (ds.s_big || geq8(s, nn))) reason = R_S_RANGE;
-  // ---- digest -> e (hashToNat: left-most 32 bytes, reduced mod n)
-  if (reason == R_OK) {
-    const uint8_t* m = in.msg + in.msg_off[i];
-    const uint32_t mlen2 = in.msg2_len ? in.msg2_len[i] : 0u;  // fused modes only
-    if constexpr (HK == HK_SHA3_256) {
-      uint8_t hb[32];
-      if (mlen2) sha3_256_msg2(hb, m, mlen, in.msg + in.msg2_off[i], mlen2);
-      else sha3_256_msg(hb, m, mlen);
-      be32_to_limbs(e, hb);  // hashToNat: the 32-byte digest, big-endian
-    } else if (fused) {
-      uint32_t h[8];
-      if (mlen2) sha256_msg2(h, m, mlen, in.msg + in.msg2_off[i], mlen2);
-      else sha256_msg(h, m, mlen);
-#pragma unroll
-      for (int k = 0; k < 8; k++) e[k] = h[7 - k];
-    } else {
-      const uint32_t L = mlen < 32 ? mlen : 32;
-#pragma unroll
-      for (int k = 0; k < 8; k++) e[k] = 0;
-#pragma unroll
-      for (int j = 0; j < 32; j++) {  // j = byte index from the least significant end
-        uint32_t v = 0;
-        if ((uint32_t)j < L) v = m[L - 1 - j];
-        e[j >> 2] |= v << (8 * (j & 3));
-      }
-    }
-    uint32_t t[8];
-    uint32_t bo = sub8(t, e, nn);
-    if (!bo) copy8(e, t);  // e < 2^256 < 2n: one conditional subtraction
-  }
+  // ---- digest -> e (hashToNat: left-most 32 bytes, reduced mod n); DEFER:
+  // k_digest computes it on the second stream (small fused batches)
+  if (reason == R_OK && !DEFER) digest_e<C, HK>(in, i, e);
   uint8_t st = reason;
   if (reason == R_OK) {
     // r*R mod p and, when r + n < p, (r + n)*R mod p for the x-mod-n check
@@ -305,7 +315,7 @@ BH_HD void stage_prep(const BatchIn& in, const Work& w, uint32_t i) {
     f_const(qx30, P::gx_m);
     f_const(qy30, P::gy_m);
   }
-  st8(w.e, i, w.ns, e);
+  if (!DEFER) st8(w.e, i, w.ns, e);
   st8(w.r, i, w.ns, r);
   st8(w.sm, i, w.ns, s);
   st9(w.qx, i, w.ns, qx30);

@@ -29,12 +29,23 @@ using namespace bh;
 
 namespace {
 
-template <class P, class N, class C, class IN, int HK>
+template <class P, class N, class C, class IN, int HK, bool DEFER = false>
 __global__ __launch_bounds__(256) void k_prep(IN in, Work w, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  if constexpr (std::is_same_v<IN, BatchIn>) stage_prep<P, N, C, HK>(in, w, i);
+  if constexpr (std::is_same_v<IN, BatchIn>) stage_prep<P, N, C, HK, DEFER>(in, w, i);
   else stage_prep<P, N, C>(in, w, i);
+}
+
+// e of every record (k_prep<..., DEFER>): the fused digests of a small batch
+// on the second stream, beside prep / inverse / plan / the u2 Q work.
+template <class C, int HK>
+__global__ __launch_bounds__(256) void k_digest(BatchIn in, Work w, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t e[8];
+  digest_e<C, HK>(in, i, e);
+  st8(w.e, i, w.ns, e);
 }
 
 // Fabric records pick the digest source per batch (SHA3 family or not); BDLS
@@ -723,9 +734,10 @@ static hipError_t comb_sort(const Plan& pl, const KeyReg& g, uint32_t n, hipStre
 // (lookup + dedup + split) | key tables + ladder | publish | key comb + bitmap.
 // BDLS batches hash their SignedProtos on the second stream (o.aux): forked
 // after the plan reset, joined before the first kernel that needs u1. Small
-// (wide) BDLS batches run the u2 Q halves of the ladder and key comb before the
-// join and only the u1 G halves after it (the digests of long lock / decide
-// messages are a serial BLAKE2b chain as long as the prep + inverse + plan).
+// (wide) BDLS batches, and small Fabric batches with fused hashing, run the u2 Q
+// halves of the ladder and key comb before the join and only the u1 G halves
+// after it (the digests of long lock / decide messages, or of a block's 4 KB
+// creator payloads, are serial chains as long as prep + inverse + plan).
 template <class P, class N, class C, class IN>
 static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg& g,
                       const uint32_t* gtab, uint32_t n, const LaunchOpts& o, uint64_t* bitmap,
@@ -735,7 +747,9 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   const dim3 grd((n + 255) / 256);
   const uint32_t nlanes = (n + o.inv_chunk - 1) / o.inv_chunk;  // records per lane ~ inv_chunk
   const dim3 grc((nlanes + 255) / 256);
-  const bool split = kBdls && o.wide > 1 && o.aux;
+  bool fused = false;  // Fabric records whose digest the device computes
+  if constexpr (!kBdls) fused = (in.flags & (BHF_HASH_SHA256 | BHF_HASH_SHA3_256)) != 0;
+  const bool split = (kBdls || fused) && o.wide > 1 && o.aux;
   // partial-sum slots (verify.h gpart_slots): ladder pairs, then key-comb groups
   const uint32_t pstride = (uint32_t)gpart_slots(w.ns), pbase = 2u * w.ns;
   hipError_t e;
@@ -758,6 +772,20 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
       hipLaunchKernelGGL((k_bdls_hash<C>), dim3((n * 4 + 255) / 256), blk, 0, s, in, w, n);
     }
     hipLaunchKernelGGL((k_prep<P, N, C, BdlsIn, 0>), grd, blk, 0, s, in, w, n);
+  } else if (split) {
+    hipStream_t aux = (hipStream_t)o.aux;
+    if ((e = hipEventRecord((hipEvent_t)o.ev_fork, s))) return e;
+    if ((e = hipStreamWaitEvent(aux, (hipEvent_t)o.ev_fork, 0))) return e;
+    if (in.flags & BHF_HASH_SHA3_256) {
+      hipLaunchKernelGGL((k_digest<C, HK_SHA3_256>), grd, blk, 0, aux, in, w, n);
+      hipLaunchKernelGGL((k_prep<P, N, C, BatchIn, HK_SHA3_256, true>), grd, blk, 0, s, in, w, n);
+    } else {
+      hipLaunchKernelGGL((k_digest<C, HK_GIVEN_OR_SHA256>), grd, blk, 0, aux, in, w, n);
+      hipLaunchKernelGGL((k_prep<P, N, C, BatchIn, HK_GIVEN_OR_SHA256, true>), grd, blk, 0, s, in,
+                         w, n);
+    }
+    if ((e = hipEventRecord((hipEvent_t)o.ev_join, aux))) return e;
+    joined = false;
   } else {
     launch_prep<P, N, C>(in, w, n, grd, blk, s);
   }
