@@ -17,6 +17,11 @@
 //   k_keycomb     1 lane/record   u2 Q by table additions (no doublings) + u1 G
 //   k_keycomb_wide<L>  L lanes/record, for batches far below chip size
 //   k_bitmap      1 lane/record   validity bitmap from the reason bytes
+// Small batches whose digests the device computes (BDLS BLAKE2b, fused
+// SHA-256 / SHA3) hash on a second stream (k_bdls_hash / k_digest) and split
+// the record work around the join: k_ladder2_q / k_ladder1_q and
+// k_keycomb_wide_q (u2 Q) before it, k_ladder2_g and k_keycomb_wide_g (u1 G,
+// butterfly, x check) after it.
 // plus k_gtab_build once per device at bh_init (fixed-base comb table for G)
 // and k_reg_prep / k_reg_status for bh_keys_register.
 #include <type_traits>
@@ -216,19 +221,6 @@ __global__ __launch_bounds__(256) void k_inv(Work w, uint32_t n, uint32_t lanes)
   if (c >= lanes) return;
   stage_inv<N, U1>(w, c, lanes, n);
 }
-
-// u1 = e w into w.e (the U1 = false inverse, for kernels that read u1 there).
-// Every other u1 reader of a split pass computes it inline (calc_u1).
-template <class N>
-__global__ __launch_bounds__(256) void k_u1(Work w, uint32_t n) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t u1[8];
-  calc_u1<N>(u1, w, i);
-  st8(w.e, i, w.ns, u1);
-}
-
-
 
 // ---- key lookup / dedup / plan ----------------------------------------------
 // Registry hit -> rec_tab; otherwise insert the fingerprint into the batch's
@@ -469,11 +461,26 @@ __global__ __launch_bounds__(256) void k_ladder2_q(Work w, Plan pl, uint32_t pst
   part_store(w, gid, pstride, C, c_inf);
 }
 
-// 8 lanes per record: lanes 0 / 1 start from the two GLV halves, every lane
-// adds the G-comb windows l, l + 8, ... of u1 = e w (computed per lane), then
-// a 3-level butterfly; lane 0 checks. (2 lanes: 13 serial mixed additions.)
+// P-256 (no endomorphism): the whole u2 Q Booth ladder on one lane per
+// record, before the join; partial sum in slot 2 j (k_ladder2_g, PARTS = 1).
+template <class P>
+__global__ __launch_bounds__(256) void k_ladder1_q(Work w, Plan pl, uint32_t pstride) {
+  const uint32_t j0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t cnt = pl.counters[1];
+  if ((j0 & ~63u) >= cnt) return;
+  const uint32_t i = pl.ladder_list[j0 < cnt ? j0 : cnt - 1];
+  J30 C;
+  bool c_inf;
+  q_ladder<P>(C, c_inf, w, i, j0 >> 6, threadIdx.x & 63u);
+  part_store(w, 2 * j0, pstride, C, c_inf);
+}
+
+// 8 lanes per record: lanes l < PARTS start from the u2 Q partial sums (the
+// two GLV halves, or P-256's single ladder), every lane adds the G-comb
+// windows l, l + 8, ... of u1 = e w (computed per lane), then a 3-level
+// butterfly; lane 0 checks. (One lane: 26 serial mixed additions.)
 constexpr int kLadGLanes = 8;
-template <class P, class N>
+template <class P, class N, int PARTS>
 __global__ __launch_bounds__(256) void k_ladder2_g(Work w, Plan pl,
                                                    const uint32_t* __restrict__ gtab,
                                                    uint8_t* __restrict__ reason,
@@ -485,7 +492,7 @@ __global__ __launch_bounds__(256) void k_ladder2_g(Work w, Plan pl,
   const uint32_t i = pl.ladder_list[j0];
   J30 C;
   bool c_inf = true;
-  if (l < 2) {
+  if (l < PARTS) {
     part_load(w, 2 * j0 + l, pstride, C, c_inf);
   } else {
     f_const(C.X, P::r1);
@@ -572,8 +579,7 @@ __global__ __launch_bounds__(256) void k_keycomb_wide_q(Work w, Plan pl, KeyReg 
   part_store(w, pbase + gid, pstride, C, c_inf);
 }
 
-// U1E: u1 is already in w.e (k_u1 ran for the P-256 Booth ladder).
-template <class P, class N, int L, bool U1E>
+template <class P, class N, int L>
 __global__ __launch_bounds__(256) void k_keycomb_wide_g(Work w, Plan pl,
                                                         const uint32_t* __restrict__ gtab,
                                                         uint8_t* __restrict__ reason,
@@ -587,8 +593,7 @@ __global__ __launch_bounds__(256) void k_keycomb_wide_g(Work w, Plan pl,
   bool c_inf;
   part_load(w, pbase + gid, pstride, C, c_inf);
   uint32_t u1[8];
-  if constexpr (U1E) ld8(u1, w.e, i, w.ns);
-  else calc_u1<N>(u1, w, i);
+  calc_u1<N>(u1, w, i);
   g_comb_part<P, L>(C, c_inf, gtab, u1, l);
   group_sum<P, L>(C, c_inf);
   if (l == 0) reason[i] = finish_check<P>(w, i, C, c_inf, C, true) ? R_OK : R_MATH;
@@ -826,6 +831,8 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
     if constexpr (!P::a_is_minus3)
       hipLaunchKernelGGL((k_ladder2_q<P>), dim3((2 * n + 255) / 256), blk, 0, s, w, plc,
                          pstride);
+    else
+      hipLaunchKernelGGL((k_ladder1_q<P>), grd, blk, 0, s, w, plc, pstride);
     if (o.wide == 16)
       hipLaunchKernelGGL((k_keycomb_wide_q<P, 16>), dim3((n * 16 + 255) / 256), blk, 0, s, w, plc,
                          g, pbase, pstride);
@@ -836,20 +843,16 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
     if (o.keep)
       hipLaunchKernelGGL(k_reg_publish, dim3((pl.max_tables + 255) / 256), blk, 0, s, w, plc, g);
     if ((e = join())) return e;
-    if constexpr (!P::a_is_minus3) {
-      hipLaunchKernelGGL((k_ladder2_g<P, N>), dim3((kLadGLanes * n + 255) / 256), blk, 0, s, w,
-                         plc, gtab, reason, pstride);
-    } else {  // P-256 BDLS: the Booth ladder, whole (u1 needed from the start)
-      hipLaunchKernelGGL((k_u1<N>), grd, blk, 0, s, w, n);
-      hipLaunchKernelGGL((k_ktab_ladder<P>), grd, blk, 0, s, w, plc, g, gtab, reason, 0u, grd.x);
-    }
+    hipLaunchKernelGGL((k_ladder2_g<P, N, P::a_is_minus3 ? 1 : 2>),
+                       dim3((kLadGLanes * n + 255) / 256), blk, 0, s, w, plc, gtab, reason,
+                       pstride);
     REC(5);
     if (o.wide == 16)
-      hipLaunchKernelGGL((k_keycomb_wide_g<P, N, 16, P::a_is_minus3>), dim3((n * 16 + 255) / 256),
-                         blk, 0, s, w, plc, gtab, reason, pbase, pstride);
+      hipLaunchKernelGGL((k_keycomb_wide_g<P, N, 16>), dim3((n * 16 + 255) / 256), blk, 0, s, w,
+                         plc, gtab, reason, pbase, pstride);
     else
-      hipLaunchKernelGGL((k_keycomb_wide_g<P, N, 4, P::a_is_minus3>), dim3((n * 4 + 255) / 256),
-                         blk, 0, s, w, plc, gtab, reason, pbase, pstride);
+      hipLaunchKernelGGL((k_keycomb_wide_g<P, N, 4>), dim3((n * 4 + 255) / 256), blk, 0, s, w,
+                         plc, gtab, reason, pbase, pstride);
     hipLaunchKernelGGL(k_bitmap, grd, blk, 0, s, reason, n, bitmap);
     REC(6);
     return hipGetLastError();
