@@ -683,54 +683,95 @@ static hipError_t plan_reset(const Plan& pl, hipStream_t s) {
   return hipMemsetAsync(pl.counters, 0, 16, s);
 }
 
-// Key-grouped comb order: sort keys for the comb list (the record's table id;
-// entries past the list length get kNone and sort last, their values 0).
-// Table ids are compacted to `bits` + 2 bits so the radix sort runs only the
-// passes it needs: a registry id (< 2^bits) as is, a per-batch id kLocal|job
-// (job < 2^16 <= 2^bits) as 2^bits | job, the padding past the list 2^(bits+1).
+// Group the comb list by table id so the (on average 16) records of one key
+// sit in adjacent lanes of one wave: their table reads then hit the same L2
+// lines instead of streaming the 58 KB table once per record. Order within a
+// key does not matter (one record per lane), so this is a counting sort over
+// the compacted ids (k_comb_keys' mapping): histogram, exclusive scan,
+// scatter -- three passes instead of a radix / merge sort's ten. Wide table-id
+// ranges (a registry above 2^16 tables) fall back to the radix sort. Runs on
+// plan buffers that are dead once k_split has routed every record: slot_hash
+// holds the scan temp, slot_cnt / slot_rep the histogram and offsets (or the
+// sort keys), and rec_slot receives the grouped list -- so after this call
+// rec_slot no longer holds slots, and the list is published as
+// Plan::comb_order (every later kernel reads that, never rec_slot).
+constexpr uint32_t kSortMin = 65536;
+constexpr uint32_t kCountSortBits = 16;  // histogram of 2^(bits+1) ids
+
+__device__ __forceinline__ uint32_t comb_key(uint32_t t, uint32_t bits) {
+  return (t & kLocal) ? ((1u << bits) | (t & ~kLocal)) : t;
+}
+
+__global__ __launch_bounds__(256) void k_comb_hist(Plan pl, uint32_t bits,
+                                                   uint32_t* __restrict__ hist) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= pl.counters[0]) return;
+  atomicAdd(&hist[comb_key(pl.rec_tab[pl.comb_list[j]], bits)], 1u);
+}
+
+__global__ __launch_bounds__(256) void k_comb_scatter(Plan pl, uint32_t bits,
+                                                      uint32_t* __restrict__ offs,
+                                                      uint32_t* __restrict__ out) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= pl.counters[0]) return;
+  const uint32_t i = pl.comb_list[j];
+  out[atomicAdd(&offs[comb_key(pl.rec_tab[i], bits)], 1u)] = i;
+}
+
+// Radix-sort fallback keys: table ids compacted to `bits` + 2 bits so the sort
+// runs only the passes it needs (registry id < 2^bits as is, kLocal | job as
+// 2^bits | job); entries past the list length get 2^(bits+1) and sort last.
 __global__ __launch_bounds__(256) void k_comb_keys(Plan pl, uint32_t n, uint32_t bits,
                                                    uint32_t* __restrict__ keys) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const uint32_t cnt = pl.counters[0];
   if (j < cnt) {
-    const uint32_t t = pl.rec_tab[pl.comb_list[j]];
-    keys[j] = (t & kLocal) ? ((1u << bits) | (t & ~kLocal)) : t;
+    keys[j] = comb_key(pl.rec_tab[pl.comb_list[j]], bits);
   } else {
     keys[j] = 2u << bits;
     pl.comb_list[j] = 0;
   }
 }
 
-// Sort the comb list by table id so the (on average 16) records of one key sit
-// in adjacent lanes of one wave: their table reads then hit the same L2 lines
-// instead of streaming the 58 KB table once per record. Runs on plan buffers
-// that are dead once k_split has routed every record: slot_hash holds the
-// sort temp, slot_rep / slot_cnt the keys, and rec_slot receives the sorted
-// list -- so after this call rec_slot no longer holds slots, and the sorted
-// list is published as Plan::comb_order (every later kernel reads that, never
-// rec_slot). Result order never changes results (one record per lane).
-constexpr uint32_t kSortMin = 65536;
 static hipError_t comb_sort(const Plan& pl, const KeyReg& g, uint32_t n, hipStream_t s,
                             Plan* out) {
   *out = pl;
   if (n < kSortMin) return hipSuccess;
   uint32_t bits = 16;
   while ((1ull << bits) < (uint64_t)g.cap) bits++;
-  const int end_bit = (int)bits + 2;
-  size_t temp = 0;
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp, pl.slot_rep, pl.slot_cnt,
-                                                    pl.comb_list, pl.rec_slot, (int)n, 0,
-                                                    end_bit, s);
-  if (e) return e;
-  if (temp > (size_t)pl.hc * 8) return hipSuccess;  // keep the unsorted list
-  hipLaunchKernelGGL(k_comb_keys, dim3((n + 255) / 256), dim3(256), 0, s, pl, n, bits,
-                     pl.slot_rep);
-  e = hipcub::DeviceRadixSort::SortPairs(pl.slot_hash, temp, pl.slot_rep, pl.slot_cnt,
-                                         pl.comb_list, pl.rec_slot, (int)n, 0, end_bit, s);
-  if (e) return e;
+  const uint32_t hsize = 2u << bits;
+  hipError_t e;
+  if (bits <= kCountSortBits && hsize <= pl.hc) {
+    size_t temp = 0;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, temp, pl.slot_cnt, pl.slot_rep,
+                                              (int)hsize, s)))
+      return e;
+    if (temp > (size_t)pl.hc * 8) return hipSuccess;  // keep the unsorted list
+    if ((e = hipMemsetAsync(pl.slot_cnt, 0, (size_t)hsize * 4, s))) return e;
+    const dim3 grd((n + 255) / 256), blk(256);
+    hipLaunchKernelGGL(k_comb_hist, grd, blk, 0, s, pl, bits, pl.slot_cnt);
+    if ((e = hipcub::DeviceScan::ExclusiveSum(pl.slot_hash, temp, pl.slot_cnt, pl.slot_rep,
+                                              (int)hsize, s)))
+      return e;
+    hipLaunchKernelGGL(k_comb_scatter, grd, blk, 0, s, pl, bits, pl.slot_rep, pl.rec_slot);
+  } else {
+    const int end_bit = (int)bits + 2;
+    size_t temp = 0;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp, pl.slot_rep, pl.slot_cnt,
+                                                pl.comb_list, pl.rec_slot, (int)n, 0, end_bit,
+                                                s)))
+      return e;
+    if (temp > (size_t)pl.hc * 8) return hipSuccess;  // keep the unsorted list
+    hipLaunchKernelGGL(k_comb_keys, dim3((n + 255) / 256), dim3(256), 0, s, pl, n, bits,
+                       pl.slot_rep);
+    if ((e = hipcub::DeviceRadixSort::SortPairs(pl.slot_hash, temp, pl.slot_rep, pl.slot_cnt,
+                                                pl.comb_list, pl.rec_slot, (int)n, 0, end_bit,
+                                                s)))
+      return e;
+  }
   out->comb_order = pl.rec_slot;
-  out->rec_slot = nullptr;  // consumed: holds the sorted list now
+  out->rec_slot = nullptr;  // consumed: holds the grouped list now
   return hipSuccess;
 }
 
