@@ -383,9 +383,12 @@ def measure_block(a, L, rank):
                 "parity": check()}
 
     cold = run(0, True)
-    t = time.perf_counter()
-    _lib.check(call(_lib.BH_FAB_F_DECODE_ONLY))
-    decode_ms = (time.perf_counter() - t) * 1e3
+    dec = []
+    for _ in range(max(5, a.steps)):  # host half alone: decode + identities, p50
+        t = time.perf_counter()
+        _lib.check(call(_lib.BH_FAB_F_DECODE_ONLY))
+        dec.append((time.perf_counter() - t) * 1e3)
+    decode_ms = percentile(dec, 50)
     warm = run(_lib.BH_FAB_F_KEEP_KEYS, False)
     return {"warm": warm, "cold": cold, "decode_only_ms": round(decode_ms, 4),
             "transactions": fb.ntx, "signatures": fb.n_signatures,
