@@ -78,7 +78,7 @@ def alg_bytes_per_record(msg_len: int) -> float:
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=1 << 20, help="config 2: records per GPU")
     ap.add_argument("--n-total", type=int, default=CONFIG5_TOTAL,
