@@ -350,15 +350,15 @@ std::vector<Dev*> all_devs() {
 
 bh::LaunchOpts launch_opts(size_t m, uint32_t flags) {
   bh::LaunchOpts o;
-  // records per inversion lane: enough lanes for ~4 waves per SIMD (safegcd
-  // makes the per-lane inversion cheap, so occupancy matters more than
-  // amortisation); BH_INV_CHUNK overrides for tuning
+  // records per inversion lane: ~2 waves per SIMD at 1M records (measured
+  // k_inv at 1M: 4 per lane 0.207 ms, 8 0.155, 16 0.159; 2 0.336);
+  // BH_INV_CHUNK overrides for tuning
   static const long env_chunk = [] {
     const char* e = getenv("BH_INV_CHUNK");
     return e ? atol(e) : 0L;
   }();
   o.inv_chunk = env_chunk > 0 ? (uint32_t)std::min<long>(env_chunk, 64)
-                              : (uint32_t)std::max<size_t>(1, std::min<size_t>(16, m / 262144));
+                              : (uint32_t)std::max<size_t>(1, std::min<size_t>(16, m / 131072));
   o.keep = (flags & BH_F_KEEP_KEYS) != 0;
   // kept tables pay off over later calls, so a second use in the batch is
   // enough; per-batch tables must pay off inside this batch
