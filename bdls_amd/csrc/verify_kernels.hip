@@ -420,34 +420,12 @@ __device__ __forceinline__ void group_sum(J30& C, bool& c_inf) {
   }
 }
 
-// secp256k1 ladder on 2 lanes per record (small, latency-bound batches): lane
-// pair (2j, 2j+1) takes the k1 Q / k2 phi(Q) halves of the GLV split and
-// alternate G-comb windows (verify.h ladder2_part); lane 0 adds the halves.
-// Each lane owns a Q-table slot (the workspace reserves 2 per record for
-// batches this small). Waves past the list length exit whole.
-template <class P>
-__global__ __launch_bounds__(256) void k_ladder2(Work w, Plan pl,
-                                                 const uint32_t* __restrict__ gtab,
-                                                 uint8_t* __restrict__ reason) {
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t j0 = gid >> 1, part = gid & 1u;
-  const uint32_t cnt = pl.counters[1];
-  if ((j0 & ~31u) >= cnt) return;
-  const bool active = j0 < cnt;
-  const uint32_t i = pl.ladder_list[active ? j0 : cnt - 1];
-  J30 C;
-  bool c_inf;
-  ladder2_part<P>(C, c_inf, w, gtab, i, gid >> 6, threadIdx.x & 63u, part);
-  group_sum<P, 2>(C, c_inf);
-  if (part != 0) return;
-  const bool ok = finish_check<P>(w, i, C, c_inf, C, true);
-  if (active) reason[i] = ok ? R_OK : R_MATH;
-}
-
-// The same ladder split around the BDLS digests: k_ladder2_q runs the GLV
-// halves (no u1 needed) while k_bdls_hash runs on the second stream, and
-// k_ladder2_g adds the G-comb windows of u1 = e w afterwards. Partial sums
-// live in the gpart scratch (slot gid, stride pstride).
+// secp256k1 ladder on 2 lanes per record (small, latency-bound batches), split
+// around the digests: lane pair (2j, 2j+1) of k_ladder2_q runs the k1 Q / k2
+// phi(Q) halves of the GLV split (no u1 needed) while the digests are hashed
+// on the second stream; k_ladder2_g adds the G-comb windows of u1 = e w
+// afterwards. Each lane owns a Q-table slot (2 per record for batches this
+// small); partial sums live in the gpart scratch (slot gid, stride pstride).
 template <class P>
 __global__ __launch_bounds__(256) void k_ladder2_q(Work w, Plan pl, uint32_t pstride) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -795,7 +773,7 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   const dim3 grc((nlanes + 255) / 256);
   bool fused = false;  // Fabric records whose digest the device computes
   if constexpr (!kBdls) fused = (in.flags & (BHF_HASH_SHA256 | BHF_HASH_SHA3_256)) != 0;
-  const bool split = (kBdls || fused) && o.wide > 1 && o.aux;
+  const bool split = (kBdls || fused) && o.wide > 1;
   // partial-sum slots (verify.h gpart_slots): ladder pairs, then key-comb groups
   const uint32_t pstride = (uint32_t)gpart_slots(w.ns), pbase = 2u * w.ns;
   hipError_t e;
@@ -805,33 +783,31 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   }
   if ((e = plan_reset(pl, s))) return e;
   REC(0);
+  // digests: on the second stream when there is one (forked here, joined
+  // before the first kernel that needs u1), else first on this stream
   bool joined = true;
+  hipStream_t hs = s;
+  if ((kBdls || split) && o.aux) {
+    hs = (hipStream_t)o.aux;
+    if ((e = hipEventRecord((hipEvent_t)o.ev_fork, s))) return e;
+    if ((e = hipStreamWaitEvent(hs, (hipEvent_t)o.ev_fork, 0))) return e;
+    joined = false;
+  }
   if constexpr (kBdls) {
-    if (o.aux) {
-      hipStream_t aux = (hipStream_t)o.aux;
-      if ((e = hipEventRecord((hipEvent_t)o.ev_fork, s))) return e;
-      if ((e = hipStreamWaitEvent(aux, (hipEvent_t)o.ev_fork, 0))) return e;
-      hipLaunchKernelGGL((k_bdls_hash<C>), dim3((n * 4 + 255) / 256), blk, 0, aux, in, w, n);
-      if ((e = hipEventRecord((hipEvent_t)o.ev_join, aux))) return e;
-      joined = false;
-    } else {
-      hipLaunchKernelGGL((k_bdls_hash<C>), dim3((n * 4 + 255) / 256), blk, 0, s, in, w, n);
-    }
+    hipLaunchKernelGGL((k_bdls_hash<C>), dim3((n * 4 + 255) / 256), blk, 0, hs, in, w, n);
+    if (!joined && (e = hipEventRecord((hipEvent_t)o.ev_join, hs))) return e;
     hipLaunchKernelGGL((k_prep<P, N, C, BdlsIn, 0>), grd, blk, 0, s, in, w, n);
   } else if (split) {
-    hipStream_t aux = (hipStream_t)o.aux;
-    if ((e = hipEventRecord((hipEvent_t)o.ev_fork, s))) return e;
-    if ((e = hipStreamWaitEvent(aux, (hipEvent_t)o.ev_fork, 0))) return e;
     if (in.flags & BHF_HASH_SHA3_256) {
-      hipLaunchKernelGGL((k_digest<C, HK_SHA3_256>), grd, blk, 0, aux, in, w, n);
+      hipLaunchKernelGGL((k_digest<C, HK_SHA3_256>), grd, blk, 0, hs, in, w, n);
+      if (!joined && (e = hipEventRecord((hipEvent_t)o.ev_join, hs))) return e;
       hipLaunchKernelGGL((k_prep<P, N, C, BatchIn, HK_SHA3_256, true>), grd, blk, 0, s, in, w, n);
     } else {
-      hipLaunchKernelGGL((k_digest<C, HK_GIVEN_OR_SHA256>), grd, blk, 0, aux, in, w, n);
+      hipLaunchKernelGGL((k_digest<C, HK_GIVEN_OR_SHA256>), grd, blk, 0, hs, in, w, n);
+      if (!joined && (e = hipEventRecord((hipEvent_t)o.ev_join, hs))) return e;
       hipLaunchKernelGGL((k_prep<P, N, C, BatchIn, HK_GIVEN_OR_SHA256, true>), grd, blk, 0, s, in,
                          w, n);
     }
-    if ((e = hipEventRecord((hipEvent_t)o.ev_join, aux))) return e;
-    joined = false;
   } else {
     launch_prep<P, N, C>(in, w, n, grd, blk, s);
   }
@@ -898,20 +874,9 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
     REC(6);
     return hipGetLastError();
   }
-  if constexpr (!P::a_is_minus3) {
-    if (o.wide > 1) {  // small secp256k1 batch: 2-lane GLV ladder
-      hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, plc, g, gtab,
-                         reason, tab_blocks, 0u);
-      hipLaunchKernelGGL((k_ladder2<P>), dim3((2 * n + 255) / 256), blk, 0, s, w, plc, gtab,
-                         reason);
-    } else {
-      hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x + gp_blocks), blk, 0, s, w,
-                         plc, g, gtab, reason, tab_blocks, grd.x);
-    }
-  } else {
-    hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x + gp_blocks), blk, 0, s, w,
-                       plc, g, gtab, reason, tab_blocks, grd.x);
-  }
+  // (small secp256k1 batches are BDLS, hence split: the 2-lane GLV ladder)
+  hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x + gp_blocks), blk, 0, s, w, plc,
+                     g, gtab, reason, tab_blocks, grd.x);
   REC(4);
   if (o.keep)
     hipLaunchKernelGGL(k_reg_publish, dim3((pl.max_tables + 255) / 256), blk, 0, s, w, plc, g);

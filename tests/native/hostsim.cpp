@@ -138,7 +138,7 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
       ok = keycomb_any<P>(w, gtab, i, tables[tab_of[r]].data());
       combs++;
     } else if (!P::a_is_minus3 && g_wide > 1) {
-      // the 2-lane secp256k1 ladder (verify_kernels.hip k_ladder2): the two
+      // the 2-lane secp256k1 ladder (verify_kernels.hip k_ladder2_q / _g): the two
       // GLV halves in two Q-table slots, added as the kernel's lane 0 does
       J30 C0, C1;
       bool i0, i1;
