@@ -914,13 +914,44 @@ BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_
 //   entry (win, j) = (j+1) 2^(4 win) Q,  win in [0, 65), j in [0, 8)
 // (Jacobian, 28 words). u2 Q is then 65 table additions with 4-bit signed
 // digits in [-7, 8] and no doublings.
-constexpr int kKWin = 65;
-constexpr int kKEnt = 8;
+#ifndef BH_KTAB_W
+#define BH_KTAB_W 4
+#endif
+constexpr int kKW = BH_KTAB_W;                   // signed-window width (bits)
+constexpr int kKWin = (257 + kKW - 1) / kKW;     // 65 windows at 4 bits
+constexpr int kKEnt = 1 << (kKW - 1);            // 8 entries per window at 4 bits
 constexpr uint32_t kKTabWords = (uint32_t)kKWin * kKEnt * kQPt;
 constexpr uint32_t kMinUses = 4;
 // Below this batch size the step is latency-bound (one table build is a
 // serial 1.07M-instruction lane, more than one ladder), so key tables are off.
 constexpr uint32_t kKeyTableMinBatch = 8192;
+
+// Signed kKW-bit digits of a scalar by one addition: with M = sum over the
+// windows of 2^(kKW w + kKW - 1), window w of k + M minus kKEnt is digit w of
+// k in [-kKEnt, kKEnt - 1] (the G comb's recode_goff for the key tables).
+struct KOff {
+  uint32_t v[9];
+};
+constexpr KOff make_koff() {
+  KOff o{};
+  for (int w = 0; w < kKWin; w++) {
+    const int b = w * kKW + kKW - 1;
+    o.v[b / 32] |= 1u << (b % 32);
+  }
+  return o;
+}
+constexpr KOff kKOff = make_koff();
+
+BH_HD void recode_koff(uint32_t v[9], const uint32_t k[8]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    c += (uint64_t)k[q] + kKOff.v[q];
+    v[q] = (uint32_t)c;
+    c >>= 32;
+  }
+  v[8] = (uint32_t)c + kKOff.v[8];
+}
 
 BH_HD void ktab_store(uint32_t* tab, uint32_t win, uint32_t j, const J30& P) {
   uint32_t v[28];
@@ -985,7 +1016,7 @@ BH_HD void ktab_build(uint32_t* tab, const Work& w, uint32_t rec) {
   }
 }
 
-// u2 Q from a key table: 4-bit signed windows (least significant first).
+// u2 Q from a key table: kKW-bit signed windows (least significant first).
 template <class P>
 BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab) {
   uint32_t k2[8];
@@ -994,23 +1025,13 @@ BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint3
   f_const(A.X, P::r1);
   f_const(A.Y, P::r1);
   f_const(A.Z, P::r1);
-  uint32_t carry = 0;
+  uint32_t v[9];
+  recode_koff(v, k2);
   for (int win = 0; win < kKWin; win++) {
-    uint32_t v = (k2[0] & 0xfu) + carry;
-#pragma unroll
-    for (int k = 0; k < 7; k++) k2[k] = (k2[k] >> 4) | (k2[k + 1] << 28);
-    k2[7] >>= 4;
-    uint32_t mag;
-    bool neg;
-    if (v > 8u) {
-      mag = 16u - v;
-      neg = true;
-      carry = 1;
-    } else {
-      mag = v;
-      neg = false;
-      carry = 0;
-    }
+    const int d = (int)(v[0] & (2u * kKEnt - 1u)) - kKEnt;
+    shr_const<kKW>(v);
+    const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+    const bool neg = d < 0;
     J30 T;
     ktab_load(T, tab, win, mag ? mag - 1 : 0);
     if (neg) f_neg<P, 64>(T.Y, T.Y);
@@ -1180,23 +1201,9 @@ BH_HD uint32_t reg_lookup(const KeyReg& g, const Work& w, uint32_t i, uint64_t h
 // L lanes share one record: lane l of the group adds the key-table windows
 // win = l, l + L, ... and the G-comb windows likewise, then the L partial
 // sums are combined by a butterfly over the group. The signed digits come
-// from one addition instead of a carry scan: with M = sum 8 * 16^w the
-// nibbles of k + M minus 8 are the digits of k in [-8, 7] (and the G comb's
-// kGW-bit digits come from recode_goff the same way), so every lane reads its
-// windows directly. Same point as q_keycomb (different digits, same sum).
-
-// v (288-bit, 9 limbs) = k + M, M = pattern in every limb of the low 256 bits
-// plus `top` at bit 256 (the top window's offset).
-BH_HD void recode_offset(uint32_t v[9], const uint32_t k[8], uint32_t pattern, uint32_t top) {
-  uint64_t c = 0;
-#pragma unroll
-  for (int q = 0; q < 8; q++) {
-    c += (uint64_t)k[q] + pattern;
-    v[q] = (uint32_t)c;
-    c >>= 32;
-  }
-  v[8] = (uint32_t)c + top;
-}
+// from one offset addition instead of a carry scan (recode_koff for the key
+// tables, recode_goff for the G comb), so every lane reads its windows
+// directly. Same digits as q_keycomb.
 
 // o = v >> sh (288-bit), 0 <= sh < 192
 BH_HD void shr288(uint32_t o[9], const uint32_t v[9], uint32_t sh) {
@@ -1281,12 +1288,12 @@ BH_HD void keycomb_q_part(J30& C, bool& c_inf, const Work& w, uint32_t i, const 
   f_const(C.Z, P::r1);
   c_inf = true;
   ld8(k, w.r, i, w.ns);
-  recode_offset(v, k, 0x88888888u, 0x8u);
-  shr288(sv, v, 4u * l);
+  recode_koff(v, k);
+  shr288(sv, v, (uint32_t)kKW * l);
   for (int m = 0; m * L < kKWin; m++) {
     const uint32_t win = l + (uint32_t)(m * L);
-    const int d = (int)(sv[0] & 0xfu) - 8;
-    shr_const<4 * L>(sv);
+    const int d = (int)(sv[0] & (2u * kKEnt - 1u)) - kKEnt;
+    shr_const<kKW * L>(sv);
     if (win < (uint32_t)kKWin) {
       const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
       J30 T;
