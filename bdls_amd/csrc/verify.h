@@ -1025,13 +1025,25 @@ BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint3
   f_const(A.X, P::r1);
   f_const(A.Y, P::r1);
   f_const(A.Z, P::r1);
-  uint32_t v[9];
-  recode_koff(v, k2);
+  uint32_t v[9], carry = 0;
+  if constexpr (kKW != 4) recode_koff(v, k2);
   for (int win = 0; win < kKWin; win++) {
-    const int d = (int)(v[0] & (2u * kKEnt - 1u)) - kKEnt;
-    shr_const<kKW>(v);
-    const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-    const bool neg = d < 0;
+    uint32_t mag;
+    bool neg;
+    if constexpr (kKW == 4) {  // carry-scan digits in [-7, 8] (the measured default)
+      const uint32_t t = (k2[0] & 0xfu) + carry;
+#pragma unroll
+      for (int k = 0; k < 7; k++) k2[k] = (k2[k] >> 4) | (k2[k + 1] << 28);
+      k2[7] >>= 4;
+      neg = t > 8u;
+      mag = neg ? 16u - t : t;
+      carry = neg ? 1u : 0u;
+    } else {  // offset digits in [-kKEnt, kKEnt - 1]
+      const int d = (int)(v[0] & (2u * kKEnt - 1u)) - kKEnt;
+      shr_const<kKW>(v);
+      mag = (uint32_t)(d < 0 ? -d : d);
+      neg = d < 0;
+    }
     J30 T;
     ktab_load(T, tab, win, mag ? mag - 1 : 0);
     if (neg) f_neg<P, 64>(T.Y, T.Y);
