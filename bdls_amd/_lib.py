@@ -31,6 +31,7 @@ EXPORTS = (
     "bh_verify_submit", "bh_verify_wait", "bh_host_alloc", "bh_host_free", "bh_csp_stats",
     "bh_fabric_block_preverify", "bh_verify_x509", "bh_signature_sets_verify",
     "bh_envelopes_preverify", "bh_block_signatures_preverify",
+    "bh_block_signatures_preverify_bft",
 )
 KEY_FULL = 255  # bh_keys_register status: registry full
 
@@ -92,6 +93,14 @@ class BhBlocksigResult(ctypes.Structure):
 BH_FAB_F_SHA3 = 1
 BH_FAB_F_KEEP_KEYS = 2
 BH_FAB_F_DECODE_ONLY = 4
+BH_BLK_F_BFT = 8
+
+
+class BhConsenterSet(ctypes.Structure):
+    """include/bdls_hip.h bh_consenter_set."""
+    _fields_ = [(name, ctypes.c_void_p) for name in
+                ("id", "msp_id", "msp_id_off", "msp_id_len", "identity", "identity_off",
+                 "identity_len")] + [("n", ctypes.c_size_t)]
 
 
 class EngineError(RuntimeError):
@@ -148,6 +157,10 @@ def lib() -> ctypes.CDLL:
         L.bh_block_signatures_preverify.argtypes = [vp, vp, vp, sz, u32, vp, vp, sz,
                                                     ctypes.POINTER(sz)]
         L.bh_block_signatures_preverify.restype = i32
+        L.bh_block_signatures_preverify_bft.argtypes = [vp, vp, vp, sz, u32,
+                                                        ctypes.POINTER(BhConsenterSet), vp, vp,
+                                                        sz, ctypes.POINTER(sz)]
+        L.bh_block_signatures_preverify_bft.restype = i32
         L.bh_verify_x509.argtypes = [vp, vp, vp, vp, sz, vp, vp]
         L.bh_verify_x509.restype = i32
         L.bh_csp_stats.argtypes = [vp]

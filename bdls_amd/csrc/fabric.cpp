@@ -811,11 +811,14 @@ struct SetRange {
 
 // common/policies/policy.go:363-395 SignatureSetToValidIdentities over each
 // set, batched: round 1 verifies the first entry of every identity of every
-// set (plus `extra`, e.g. creator signatures, in the same device batch);
-// the in-order replay then marks entries Go skips as duplicates (an identity
-// already validated earlier in the set) and, where an identity's earlier
-// signature failed, queues its next entry for another round (Go checks it).
-// Entries whose identity does not resolve are skipped, as Go skips them.
+// set (plus `extra`, e.g. creator signatures, in the same device batch). Go
+// checks a later entry of an identity only while no earlier one verified, so
+// round 2 verifies -- speculatively, in ONE more device batch -- every later
+// entry of the identities whose first entry failed (rare: a signer repeating
+// itself after a bad signature); the in-order replay then marks the entries
+// Go skips as duplicates (an identity already validated earlier in the set).
+// At most two device passes, however the duplicates are arranged. Entries
+// whose identity does not resolve are skipped, as Go skips them.
 int verify_sets(std::vector<SdEntry>& e, const std::vector<SetRange>& sets, uint32_t vflags,
                 bool decode_only, std::vector<uint32_t>* valid, Batch* extra) {
   Batch b;
@@ -832,7 +835,7 @@ int verify_sets(std::vector<SdEntry>& e, const std::vector<SetRange>& sets, uint
     }
     b.reserve(b.size() + e.size(), b.msg.size() + bytes, b.sig.size() + sig_bytes);
   }
-  std::vector<uint64_t> seen, ok;
+  std::vector<uint64_t> seen, failed;
   for (const SetRange& r : sets) {
     seen.clear();
     for (size_t i = r.first; i < r.first + r.count; i++) {
@@ -846,33 +849,40 @@ int verify_sets(std::vector<SdEntry>& e, const std::vector<SetRange>& sets, uint
       b.add(x);
     }
   }
-  if (!decode_only)
+  if (!decode_only) {
     if (int rc = b.run(vflags)) return rc;
-  valid->assign(sets.size(), 0);
-  for (int round = 0; round < 256; round++) {
     Batch more;
     more.base = b.base;
     more.base_len = b.base_len;
-    for (size_t k = 0; k < sets.size(); k++) {
-      const SetRange& r = sets[k];
-      ok.clear();
+    for (const SetRange& r : sets) {
+      failed.clear();  // identities whose round-1 entry failed
       for (size_t i = r.first; i < r.first + r.count; i++) {
         SdEntry& x = e[i];
         if (!x.id || !x.id->ok) continue;
-        if (std::find(ok.begin(), ok.end(), x.id->key_id) != ok.end()) {
-          x.out = BH_FAB_E_DUPLICATE;
-          continue;
+        if (x.out != BH_SP_NOT_VERIFIED) {
+          if (x.out != BH_R_OK) failed.push_back(x.id->key_id);
+        } else if (std::find(failed.begin(), failed.end(), x.id->key_id) != failed.end()) {
+          more.add(x);
         }
-        if (x.out == BH_SP_NOT_VERIFIED) {  // Go reaches it: verify next round
-          if (!decode_only) more.add(x);
-          break;  // later entries of this set depend on its result
-        }
-        if (x.out == BH_R_OK) ok.push_back(x.id->key_id);
       }
-      (*valid)[k] = (uint32_t)ok.size();
     }
-    if (!more.size() || decode_only) break;
     if (int rc = more.run(vflags)) return rc;
+  }
+  valid->assign(sets.size(), 0);
+  std::vector<uint64_t> ok;
+  for (size_t k = 0; k < sets.size(); k++) {
+    const SetRange& r = sets[k];
+    ok.clear();
+    for (size_t i = r.first; i < r.first + r.count; i++) {
+      SdEntry& x = e[i];
+      if (!x.id || !x.id->ok) continue;
+      if (std::find(ok.begin(), ok.end(), x.id->key_id) != ok.end()) {
+        x.out = BH_FAB_E_DUPLICATE;  // Go skips it (verified speculatively or not at all)
+        continue;
+      }
+      if (x.out == BH_R_OK) ok.push_back(x.id->key_id);
+    }
+    (*valid)[k] = (uint32_t)ok.size();
   }
   return BH_OK;
 }
@@ -1160,33 +1170,38 @@ bool strict_sig(const uint8_t* b, size_t n, std::vector<uint8_t>* r, std::vector
   return cb_uint(in, il, &io, r) && cb_uint(in, il, &io, s) && io == il;
 }
 
+// DER length octets, any size (a certificate's signature BIT STRING is not
+// bounded, so neither are r and s as cryptobyte reads them)
+void der_len(std::vector<uint8_t>* o, size_t n) {
+  if (n < 0x80) {
+    o->push_back((uint8_t)n);
+    return;
+  }
+  uint8_t b[8];
+  int k = 0;
+  for (; n; n >>= 8) b[k++] = (uint8_t)n;
+  o->push_back((uint8_t)(0x80 | k));
+  while (k) o->push_back(b[--k]);
+}
+
 void der_uint(std::vector<uint8_t>* o, const std::vector<uint8_t>& v) {
   const bool pad = v[0] & 0x80;
-  const size_t len = v.size() + (pad ? 1 : 0);
   o->push_back(0x02);
-  if (len < 0x80) {
-    o->push_back((uint8_t)len);
-  } else {
-    o->push_back(0x81);  // <= 255: the signature's own length bounds it
-    o->push_back((uint8_t)len);
-  }
+  der_len(o, v.size() + (pad ? 1 : 0));
   if (pad) o->push_back(0);
   o->insert(o->end(), v.begin(), v.end());
 }
 
-// canonical DER of (r, s): what the device's Go-asn1 parser reads back exactly
+// canonical DER of (r, s): what the device's Go-asn1 parser reads back
+// exactly (an r or s above 32 significant bytes parses as out of range there,
+// as bigmod's SetBytes rejects it in Go)
 void canon_sig(std::vector<uint8_t>* o, const std::vector<uint8_t>& r,
                const std::vector<uint8_t>& s) {
   std::vector<uint8_t> body;
   der_uint(&body, r);
   der_uint(&body, s);
   o->push_back(0x30);
-  if (body.size() < 0x80) {
-    o->push_back((uint8_t)body.size());
-  } else {
-    o->push_back(0x81);
-    o->push_back((uint8_t)body.size());
-  }
+  der_len(o, body.size());
   o->insert(o->end(), body.begin(), body.end());
 }
 
@@ -1337,6 +1352,9 @@ extern "C" int bh_signature_sets_verify(const bh_sd_batch* b, size_t n, const ui
                    !b->data_len || !b->sig_off || !b->sig_len || !result)) ||
       (n_sets && (!set_first || !valid_identities)))
     return bh::host_fail(BH_E_INVALID, "null argument");
+  for (size_t i = 0; i < n; i++)  // a span with bytes needs a buffer (as bh_verify checks)
+    if ((b->data_len[i] && !b->data) || (b->sig_len[i] && !b->sig))
+      return bh::host_fail(BH_E_INVALID, "null data / sig buffer with nonzero lengths");
   if (flags & ~(uint32_t)(BH_FAB_F_SHA3 | BH_FAB_F_KEEP_KEYS | BH_FAB_F_DECODE_ONLY))
     return bh::host_fail(BH_E_INVALID, "unknown flag");
   std::vector<SetRange> sets;
@@ -1458,27 +1476,72 @@ std::vector<uint8_t> block_header_bytes(uint64_t number, Span prev, Span data_ha
 
 }  // namespace
 
-// Block signatures (protoutil/blockutils.go:245-300 BlockSignatureVerifier,
-// non-BFT form; called by orderer/common/cluster/util.go:300
-// VerifyBlockSignature and the peer's gossip MCS) for n serialized blocks in
-// one device batch.
-extern "C" int bh_block_signatures_preverify(const uint8_t* blocks, const uint64_t* block_off,
-                                             const uint32_t* block_len, size_t n, uint32_t flags,
-                                             bh_blocksig_result* res, uint8_t* sig_reason,
-                                             size_t sig_cap, size_t* sig_total) {
+namespace {
+
+// protoutil.MarshalOrPanic(&msp.SerializedIdentity{Mspid, IdBytes})
+// (protoutil/blockutils.go:298-308 searchConsenterIdentityByID): proto3
+// fields in number order, each omitted when empty.
+void pb_put_bytes(std::vector<uint8_t>* o, uint32_t num, const uint8_t* p, size_t n) {
+  if (!n) return;
+  o->push_back((uint8_t)(num << 3 | 2));
+  size_t v = n;
+  while (v >= 0x80) {
+    o->push_back((uint8_t)(v | 0x80));
+    v >>= 7;
+  }
+  o->push_back((uint8_t)v);
+  o->insert(o->end(), p, p + n);
+}
+
+// The BFT consenter set as searchConsenterIdentityByID walks it: the FIRST
+// consenter with the identifier, its marshalled SerializedIdentity (empty: Go
+// treats the signature as outside the set).
+struct Consenters {
+  std::vector<uint32_t> id;
+  std::vector<std::vector<uint8_t>> ser;
+  const std::vector<uint8_t>* find(uint32_t ident) const {
+    for (size_t k = 0; k < id.size(); k++)
+      if (id[k] == ident) return &ser[k];
+    return nullptr;
+  }
+};
+
+int block_signatures(const uint8_t* blocks, const uint64_t* block_off, const uint32_t* block_len,
+                     size_t n, uint32_t flags, const bh_consenter_set* cs, bh_blocksig_result* res,
+                     uint8_t* sig_reason, size_t sig_cap, size_t* sig_total) {
   if (!sig_total || (n && (!blocks || !block_off || !block_len || !res)))
     return bh::host_fail(BH_E_INVALID, "null argument");
-  if (flags & ~(uint32_t)(BH_FAB_F_SHA3 | BH_FAB_F_KEEP_KEYS | BH_FAB_F_DECODE_ONLY))
+  if (flags & ~(uint32_t)(BH_FAB_F_SHA3 | BH_FAB_F_KEEP_KEYS | BH_FAB_F_DECODE_ONLY | BH_BLK_F_BFT))
     return bh::host_fail(BH_E_INVALID, "unknown flag");
+  const bool bft = (flags & BH_BLK_F_BFT) != 0;
+  Consenters cons;
+  if (cs && cs->n) {
+    if (!cs->id || !cs->msp_id_off || !cs->msp_id_len || !cs->identity_off || !cs->identity_len)
+      return bh::host_fail(BH_E_INVALID, "null consenter array");
+    for (size_t k = 0; k < cs->n; k++) {
+      if ((cs->msp_id_len[k] && !cs->msp_id) || (cs->identity_len[k] && !cs->identity))
+        return bh::host_fail(BH_E_INVALID, "null consenter bytes");
+      std::vector<uint8_t> ser;
+      if (cs->msp_id_len[k])
+        pb_put_bytes(&ser, 1, cs->msp_id + cs->msp_id_off[k], cs->msp_id_len[k]);
+      if (cs->identity_len[k])
+        pb_put_bytes(&ser, 2, cs->identity + cs->identity_off[k], cs->identity_len[k]);
+      cons.id.push_back(cs->id[k]);
+      cons.ser.push_back(std::move(ser));
+    }
+  }
   std::vector<SdEntry> e;
+  std::vector<uint8_t> not_in_set;  // per entry: a BFT signature outside the consenter set
   std::vector<SetRange> sets;
   std::vector<std::vector<uint8_t>> hdr_der(n);  // BlockHeaderBytes per block (kept alive)
   std::vector<size_t> set_of(n, SIZE_MAX);
+  // entries outside the consenter set are not part of the policy's set: the
+  // set handed to verify_sets is the in-set entries only (e_set indexes e)
+  std::vector<size_t> e_set;
   std::unique_ptr<IdentCache::Session> ic(new IdentCache::Session(ident_cache()));
   for (size_t i = 0; i < n; i++) {
     res[i] = bh_blocksig_result{BH_BLK_OK, 0, 0, 0};
-    Span header, metadata;
-    bool has_header = false, has_meta = false;
+    bool has_header = false;
     std::vector<Span> mds;
     uint64_t number = 0;
     Span prev, dhash;
@@ -1493,18 +1556,13 @@ extern "C" int bh_block_signatures_preverify(const uint8_t* blocks, const uint64
         });
       }
       if (is_bytes(f, 2)) return pb_walk(f.s.p, f.s.n, [&](const Field&) { return true; });
-      if (is_bytes(f, 3)) {
-        has_meta = true;
+      if (is_bytes(f, 3))
         return pb_walk(f.s.p, f.s.n, [&](const Field& g) {
           if (is_bytes(g, 1)) mds.push_back(g.s);
           return true;
         });
-      }
       return true;
     });
-    (void)header;
-    (void)metadata;
-    (void)has_meta;
     if (!ok || !has_header) {  // Go dereferences the nil header
       res[i].status = BH_BLK_DECODE;
       continue;
@@ -1541,43 +1599,95 @@ extern "C" int bh_block_signatures_preverify(const uint8_t* blocks, const uint64
       continue;
     }
     hdr_der[i] = block_header_bytes(number, prev, dhash);
-    const size_t first = e.size();
-    bool bad = false;
+    const size_t first = e.size(), first_set = e_set.size();
     for (const MSig& m : sigs) {
-      SignatureHeader sh;
-      if (!dec_signature_header(m.sh, &sh)) {  // fails the whole verifier
-        res[i].status = BH_BLK_SIGNATURE_HEADER;
-        bad = true;
-        break;
-      }
       SdEntry x;
-      x.id = ic->get(sh.creator);
       x.seg[0] = value;
-      x.seg[1] = m.sh;
       x.seg[2] = Span{hdr_der[i].data(), hdr_der[i].size(), true};
       x.nseg = 3;
       x.sig = m.sig;
+      if (bft && m.sh.n == 0 && m.idh.n > 0) {
+        // blockutils.go:261-272: the signer is the consenter with the
+        // IdentifierHeader's identifier; signed = value || idh || header
+        uint32_t ident = 0;
+        if (!pb_walk(m.idh.p, m.idh.n, [&](const Field& g) {
+              if (is_varint(g, 1)) ident = (uint32_t)g.v;  // uint32 field: low 32 bits
+              return true;                                 // 2 nonce: bytes, no checks
+            })) {
+          res[i].status = BH_BLK_IDENTIFIER_HEADER;
+          break;
+        }
+        const std::vector<uint8_t>* ser = cons.find(ident);
+        if (!ser || ser->empty()) {  // "not within the consenter set": skipped
+          x.out = BH_FAB_E_NOT_CONSENTER;
+          e.push_back(x);
+          not_in_set.push_back(1);
+          continue;
+        }
+        x.id = ic->get(Span{ser->data(), ser->size(), true});
+        x.seg[1] = m.idh;
+      } else {
+        SignatureHeader sh;
+        if (!dec_signature_header(m.sh, &sh)) {  // fails the whole verifier
+          res[i].status = BH_BLK_SIGNATURE_HEADER;
+          break;
+        }
+        x.id = ic->get(sh.creator);
+        x.seg[1] = m.sh;
+      }
       e.push_back(x);
+      not_in_set.push_back(0);
     }
-    if (bad) {
+    if (res[i].status != BH_BLK_OK) {
       e.resize(first);
+      not_in_set.resize(first);
       continue;
     }
+    for (size_t k = first; k < e.size(); k++)
+      if (!not_in_set[k]) e_set.push_back(k);
     res[i].sig_first = (uint32_t)first;
     res[i].sig_count = (uint32_t)(e.size() - first);
     set_of[i] = sets.size();
-    sets.push_back(SetRange{first, e.size() - first});
+    sets.push_back(SetRange{first_set, e_set.size() - first_set});
   }
   ic.reset();
   *sig_total = e.size();
   if (e.size() && (!sig_reason || sig_cap < e.size()))
     return bh::host_fail(BH_E_INVALID, "sig_reason too small (see *sig_total)");
+  std::vector<SdEntry> in_set;
+  in_set.reserve(e_set.size());
+  for (size_t k : e_set) in_set.push_back(e[k]);
   std::vector<uint32_t> valid;
-  if (int rc = verify_sets(e, sets, verify_flags(flags), (flags & BH_FAB_F_DECODE_ONLY) != 0,
-                           &valid, nullptr))
+  if (int rc = verify_sets(in_set, sets, verify_flags(flags),
+                           (flags & BH_FAB_F_DECODE_ONLY) != 0, &valid, nullptr))
     return rc;
+  for (size_t j = 0; j < e_set.size(); j++) e[e_set[j]].out = in_set[j].out;
   for (size_t i = 0; i < n; i++)
     if (set_of[i] != SIZE_MAX) res[i].valid_identities = valid[set_of[i]];
   for (size_t k = 0; k < e.size(); k++) sig_reason[k] = e[k].out;
   return BH_OK;
+}
+
+}  // namespace
+
+// Block signatures (protoutil/blockutils.go:245-300 BlockSignatureVerifier;
+// called by orderer/common/cluster/util.go:300 VerifyBlockSignature and the
+// peer's gossip MCS) for n serialized blocks in one device batch.
+extern "C" int bh_block_signatures_preverify(const uint8_t* blocks, const uint64_t* block_off,
+                                             const uint32_t* block_len, size_t n, uint32_t flags,
+                                             bh_blocksig_result* res, uint8_t* sig_reason,
+                                             size_t sig_cap, size_t* sig_total) {
+  return block_signatures(blocks, block_off, block_len, n, flags, nullptr, res, sig_reason,
+                          sig_cap, sig_total);
+}
+
+// The same with bftEnabled (flag BH_BLK_F_BFT) and the channel's consenter
+// set (BlockSignatureVerifier(bftEnabled, consenters, policy)).
+extern "C" int bh_block_signatures_preverify_bft(const uint8_t* blocks, const uint64_t* block_off,
+                                                 const uint32_t* block_len, size_t n,
+                                                 uint32_t flags, const bh_consenter_set* consenters,
+                                                 bh_blocksig_result* res, uint8_t* sig_reason,
+                                                 size_t sig_cap, size_t* sig_total) {
+  return block_signatures(blocks, block_off, block_len, n, flags, consenters, res, sig_reason,
+                          sig_cap, sig_total);
 }

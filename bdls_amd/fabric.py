@@ -126,9 +126,11 @@ def envelopes_preverify(envs, sha3: bool = False, keep_keys: bool = False,
 
 
 def block_signatures_preverify(blocks, sha3: bool = False, keep_keys: bool = False,
-                               decode_only: bool = False):
+                               decode_only: bool = False, bft: bool = False, consenters=None):
     """Block signature sets of n serialized blocks: [(status, per-signature,
-    valid identities)]."""
+    valid identities)] (protoutil/blockutils.go:245-308 BlockSignatureVerifier).
+    bft: bftEnabled; consenters: [(id, msp_id bytes, identity bytes)], the
+    channel's cb.Consenter set searched by IdentifierHeader.identifier."""
     L = _lib.lib()
     if not decode_only:
         _lib.ensure_init()
@@ -138,8 +140,21 @@ def block_signatures_preverify(blocks, sha3: bool = False, keep_keys: bool = Fal
     total = ctypes.c_size_t()
     cap = sum(len(b) for b in blocks) // 8 + 64
     sr = np.zeros(cap, np.uint8)
-    _lib.check(L.bh_block_signatures_preverify(buf.ctypes.data, off.ctypes.data, ln.ctypes.data, n,
-                                               _flags(sha3, keep_keys, decode_only), res,
-                                               sr.ctypes.data, cap, ctypes.byref(total)))
+    flags = _flags(sha3, keep_keys, decode_only)
+    if bft or consenters is not None:
+        cons = list(consenters or [])
+        ids = np.array([c[0] for c in cons] or [0], np.uint32)
+        mb, mo, ml = _concat([c[1] for c in cons])
+        ib, io, il = _concat([c[2] for c in cons])
+        cs = _lib.BhConsenterSet(ids.ctypes.data, mb.ctypes.data, mo.ctypes.data, ml.ctypes.data,
+                                 ib.ctypes.data, io.ctypes.data, il.ctypes.data, len(cons))
+        _lib.check(L.bh_block_signatures_preverify_bft(
+            buf.ctypes.data, off.ctypes.data, ln.ctypes.data, n,
+            flags | (_lib.BH_BLK_F_BFT if bft else 0), ctypes.byref(cs), res, sr.ctypes.data,
+            cap, ctypes.byref(total)))
+    else:
+        _lib.check(L.bh_block_signatures_preverify(buf.ctypes.data, off.ctypes.data,
+                                                   ln.ctypes.data, n, flags, res, sr.ctypes.data,
+                                                   cap, ctypes.byref(total)))
     return [(res[i].status, [int(x) for x in sr[res[i].sig_first:res[i].sig_first + res[i].sig_count]],
              res[i].valid_identities) for i in range(n)]

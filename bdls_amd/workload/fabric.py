@@ -164,6 +164,7 @@ class Identity:
     priv: bytes
     pub: bytes
     serialized: bytes
+    cert_pem: bytes = b""
 
 
 def make_identities(L, seed: int, norgs: int, nclients: int):
@@ -190,7 +191,8 @@ def make_identities(L, seed: int, norgs: int, nclients: int):
         meta.append(("client", org, priv, pub))
     sigs = sign_batch(L, signer, [hashlib.sha256(t).digest() for t in tbs_list], seed + 77)
     for tbs, sg, (kind, org, priv, pub) in zip(tbs_list, sigs, meta):
-        ident = Identity(org, priv, pub, serialized_identity(org, pem(x509_cert(tbs, sg))))
+        cp = pem(x509_cert(tbs, sg))
+        ident = Identity(org, priv, pub, serialized_identity(org, cp), cp)
         (peers if kind == "peer" else clients).append(ident)
     return cas, peers, clients
 
@@ -441,3 +443,89 @@ def generate_signed_blocks(nblocks: int = 16, norderers: int = 4, seed: int = 21
             expected.append((0, want, sum(1 for w in want if w == 0)))
         prev = hashlib.sha256(hder).digest()
     return blocks, expected
+
+
+BFT_BLOCKSIG_CORRUPTIONS = ["none", "sig_flip", "unknown_id", "dup_consenter", "bad_idh",
+                            "creator_form", "both_headers", "consenter_bad_identity", "high_s",
+                            "id_wrap"]
+
+
+def generate_bft_signed_blocks(nblocks: int = 20, norderers: int = 4, seed: int = 31,
+                               classes: list[str] | None = None):
+    """Blocks as a BFT orderer cluster (consensus type "BFT", which this fork
+    gives BDLS) signs them: each MetadataSignature has an empty
+    signature_header and an IdentifierHeader{identifier: consenter Id, nonce};
+    the signed bytes are Metadata.value || identifier_header ||
+    BlockHeaderBytes(header) (protoutil/blockutils.go:261-272). Returns
+    (blocks, consenters, expected): consenters = [(id, msp_id, identity PEM)]
+    with Ids 1..norderers, expected[i] = (status, per-signature result, valid
+    identities) with 252 for identifiers outside the set."""
+    L = _gen()
+    st = [seed * 0x2545F4914F6CDD1D + 9]
+    _, orderers, _ = make_identities(L, seed, norderers, 0)
+    garbage = b"-----BEGIN CERTIFICATE-----\n!!\n-----END CERTIFICATE-----\n"
+    consenters = [(k + 1, o.mspid.encode(), o.cert_pem) for k, o in enumerate(orderers)]
+    # first match wins (a later consenter with Id 2 is never consulted); Id 90
+    # has an identity that does not deserialize; Id 91 marshals to nothing
+    consenters += [(2, b"OtherMSP", garbage), (90, b"OrdererMSP", garbage), (91, b"", b"")]
+    blocks, expected = [], []
+    prev = b"\x00" * 32
+    for bi in range(nblocks):
+        cls = classes[bi % len(classes)] if classes else "none"
+        data = b"".join(pb_bytes(1, _rand_bytes(st, 80)) for _ in range(2))
+        dhash = hashlib.sha256(data).digest()
+        number = 500 + bi
+        hdr_pb = pb_varint(1, number) + pb_bytes(2, prev) + pb_bytes(3, dhash)
+        hder = block_header_der(number, prev, dhash)
+        value = pb_bytes(1, pb_varint(1, number - 1))
+        sigs, want = [], []
+        for k, o in enumerate(orderers):
+            ident = k + 1
+            if cls == "unknown_id" and k == 3:
+                ident = 77
+            if cls == "unknown_id" and k == 2:
+                ident = 91  # in the set, but its SerializedIdentity marshals to nothing
+            if cls == "consenter_bad_identity" and k == 0:
+                ident = 90
+            if cls == "id_wrap" and k == 0:
+                ident_field = pb_varint(1, (1 << 32) + 1)  # uint32 field: low 32 bits -> Id 1
+            else:
+                ident_field = pb_varint(1, ident)
+            idh = ident_field + pb_bytes(2, _rand_bytes(st, 24))
+            if cls == "creator_form" and k == 1:  # this signer uses the SignatureHeader form
+                shdr = pb_bytes(1, o.serialized) + pb_bytes(2, _rand_bytes(st, 24))
+                sg = sign(L, o.priv, value + shdr + hder, seed + 100 * bi + k)
+                sigs.append(pb_bytes(1, shdr) + pb_bytes(2, sg))
+                want.append(0)
+                continue
+            sg = sign(L, o.priv, value + idh + hder, seed + 100 * bi + k,
+                      high_s=(cls == "high_s" and k == 2))
+            if cls == "sig_flip" and k == 1:
+                sg = sg[:-1] + bytes([sg[-1] ^ 1])
+            if cls == "both_headers" and k == 0:
+                # a signature header present: the SignatureHeader form is taken,
+                # over value || signature_header || header; signed with the
+                # idh form, so it fails
+                shdr = pb_bytes(1, o.serialized) + pb_bytes(2, b"n" * 24)
+                sigs.append(pb_bytes(1, shdr) + pb_bytes(2, sg) + pb_bytes(3, idh))
+                want.append(9)
+                continue
+            sigs.append(pb_bytes(2, sg) + pb_bytes(3, idh))
+            want.append(252 if (cls == "unknown_id" and k in (2, 3)) else
+                        254 if (cls == "consenter_bad_identity" and k == 0) else
+                        6 if (cls == "high_s" and k == 2) else
+                        9 if (cls == "sig_flip" and k == 1) else 0)
+        if cls == "dup_consenter":
+            sigs.append(sigs[2])
+            want.append(253)
+        if cls == "bad_idh":
+            sigs.insert(1, pb_bytes(2, b"\x30\x00") + pb_bytes(3, b"\x08"))  # truncated varint
+        md = pb_bytes(1, value) + b"".join(pb_bytes(2, x) for x in sigs)
+        meta = pb_bytes(1, md) + pb_bytes(1, b"") + pb_bytes(1, b"")
+        blocks.append(pb_bytes(1, hdr_pb) + pb_bytes(2, data) + pb_bytes(3, meta))
+        if cls == "bad_idh":
+            expected.append((5, [], 0))
+        else:
+            expected.append((0, want, sum(1 for w in want if w == 0)))
+        prev = hashlib.sha256(hder).digest()
+    return blocks, consenters, expected

@@ -389,6 +389,8 @@ int bh_envelopes_preverify(const uint8_t *envs, const uint64_t *env_off, const u
 #define BH_BLK_NO_SIGNATURES 2     /* "no signatures in block metadata" */
 #define BH_BLK_METADATA 3          /* Metadata does not unmarshal */
 #define BH_BLK_SIGNATURE_HEADER 4  /* a signature header does not unmarshal */
+#define BH_BLK_IDENTIFIER_HEADER 5 /* BFT: an IdentifierHeader does not unmarshal */
+#define BH_FAB_E_NOT_CONSENTER 252 /* BFT: identifier outside the consenter set (not in the set) */
 typedef struct bh_blocksig_result {
   int32_t status;            /* BH_BLK_* */
   uint32_t sig_first;
@@ -399,6 +401,35 @@ int bh_block_signatures_preverify(const uint8_t *blocks, const uint64_t *block_o
                                   const uint32_t *block_len, size_t n, uint32_t flags,
                                   bh_blocksig_result *res, uint8_t *sig_reason, size_t sig_cap,
                                   size_t *sig_total);
+
+/* BFT form (protoutil/blockutils.go:245-308 with bftEnabled, the V3_0 channel
+ * capability, common/capabilities/channel.go:111; this fork registers BDLS as
+ * consensus type "BFT", orderer/common/server/main.go:628). With
+ * BH_BLK_F_BFT, a MetadataSignature whose signature_header is empty and whose
+ * identifier_header is not is signed by the consenter with that identifier
+ * (the FIRST cb.Consenter with Id == IdentifierHeader.identifier; identity =
+ * marshalled msp.SerializedIdentity{MspId, Identity}) over Metadata.value ||
+ * identifier_header || BlockHeaderBytes; an identifier outside the set is
+ * skipped by Go (reported BH_FAB_E_NOT_CONSENTER, not part of the set's
+ * de-duplication), and an IdentifierHeader that does not unmarshal fails the
+ * block (BH_BLK_IDENTIFIER_HEADER). Without the flag (or with the signature
+ * header present) this is bh_block_signatures_preverify. consenters may be
+ * NULL (an empty set). */
+#define BH_BLK_F_BFT 8u
+typedef struct bh_consenter_set { /* cb.Consenter{Id, MspId, Identity}, SoA */
+  const uint32_t *id;
+  const uint8_t *msp_id;     /* MspId strings (not NUL-terminated) */
+  const uint64_t *msp_id_off;
+  const uint32_t *msp_id_len;
+  const uint8_t *identity;   /* Identity bytes (PEM certificate) */
+  const uint64_t *identity_off;
+  const uint32_t *identity_len;
+  size_t n;
+} bh_consenter_set;
+int bh_block_signatures_preverify_bft(const uint8_t *blocks, const uint64_t *block_off,
+                                      const uint32_t *block_len, size_t n, uint32_t flags,
+                                      const bh_consenter_set *consenters, bh_blocksig_result *res,
+                                      uint8_t *sig_reason, size_t sig_cap, size_t *sig_total);
 
 /* ---- X.509 certificate signatures ---------------------------------------------
  * Certificate i's signature against issuer key i (X || Y): Go crypto/x509

@@ -540,10 +540,13 @@ def sigfilter(env_bytes: bytes, verify, decode_only: bool = False):
 
 # block signatures
 BLK_OK, BLK_DECODE, BLK_NO_SIGNATURES, BLK_METADATA, BLK_SIGNATURE_HEADER = range(5)
+BLK_IDENTIFIER_HEADER = 5
+E_NOT_CONSENTER = 252
 METADATA_SPEC = {1: ("value", "bytes"),
                  2: ("signatures", ("rep", {1: ("signature_header", "bytes"),
                                             2: ("signature", "bytes"),
                                             3: ("identifier_header", "bytes")}))}
+IDENTIFIER_HEADER_SPEC = {1: ("identifier", "varint"), 2: ("nonce", "bytes")}
 
 
 def _der(tag: int, content: bytes) -> bytes:
@@ -561,9 +564,32 @@ def block_header_bytes(number: int, prev: bytes, data_hash: bytes) -> bytes:
     return _der(0x30, _der(0x02, num) + _der(0x04, prev) + _der(0x04, data_hash))
 
 
-def block_signatures(block: bytes, verify, decode_only: bool = False):
-    """protoutil/blockutils.go:245-300 BlockSignatureVerifier (non-BFT) ->
-    (status, per-signature results, valid identities)."""
+def _pb_len_field(num: int, b: bytes) -> bytes:
+    if not b:
+        return b""  # proto3: empty fields are not marshalled
+    n, v = len(b), bytearray()
+    while n >= 0x80:
+        v.append((n & 0x7F) | 0x80)
+        n >>= 7
+    v.append(n)
+    return bytes([num << 3 | 2]) + bytes(v) + b
+
+
+def search_consenter_identity_by_id(consenters, identifier: int) -> bytes:
+    """protoutil/blockutils.go:298-308: the first consenter with the Id,
+    MarshalOrPanic(&msp.SerializedIdentity{Mspid, IdBytes}), or b"" (nil)."""
+    for cid, mspid, ident in consenters or []:
+        if cid == identifier:
+            return _pb_len_field(1, mspid) + _pb_len_field(2, ident)
+    return b""
+
+
+def block_signatures(block: bytes, verify, decode_only: bool = False, bft: bool = False,
+                     consenters=None):
+    """protoutil/blockutils.go:245-300 BlockSignatureVerifier(bftEnabled,
+    consenters, policy) -> (status, per-signature results, valid identities).
+    Signatures of identifiers outside the consenter set (BFT) are E_NOT_CONSENTER
+    and not part of the policy's signature set."""
     try:
         blk = unmarshal(block, BLOCK_SPEC)
     except DecodeError:
@@ -579,14 +605,26 @@ def block_signatures(block: bytes, verify, decode_only: bool = False):
         return BLK_METADATA, [], 0
     h = blk["header"]
     hdr = block_header_bytes(h["number"], h["previous_hash"] or b"", h["data_hash"] or b"")
-    entries = []
+    entries, where = [], []
     for ms in md["signatures"]:
-        try:
-            sh = unmarshal(ms["signature_header"] or b"", SIGNATURE_HEADER_SPEC)
-        except DecodeError:
-            return BLK_SIGNATURE_HEADER, [], 0
-        entries.append((sh["creator"] or b"",
-                        (md["value"] or b"") + (ms["signature_header"] or b"") + hdr,
-                        ms["signature"] or b""))
+        sh_b, idh_b = ms["signature_header"] or b"", ms["identifier_header"] or b""
+        if bft and not sh_b and idh_b:
+            try:
+                idh = unmarshal(idh_b, IDENTIFIER_HEADER_SPEC)
+            except DecodeError:
+                return BLK_IDENTIFIER_HEADER, [], 0
+            ident = search_consenter_identity_by_id(consenters, idh["identifier"] & 0xFFFFFFFF)
+            if not ident:
+                where.append(None)
+                continue
+            signed = (md["value"] or b"") + idh_b + hdr
+        else:
+            try:
+                sh = unmarshal(sh_b, SIGNATURE_HEADER_SPEC)
+            except DecodeError:
+                return BLK_SIGNATURE_HEADER, [], 0
+            ident, signed = sh["creator"] or b"", (md["value"] or b"") + sh_b + hdr
+        where.append(len(entries))
+        entries.append((ident, signed, ms["signature"] or b""))
     res, nvalid = signature_set_to_valid_identities(entries, verify, decode_only)
-    return BLK_OK, res, nvalid
+    return BLK_OK, [E_NOT_CONSENTER if w is None else res[w] for w in where], nvalid

@@ -267,3 +267,80 @@ def test_gpu_block_signatures(signed_blocks):
     blocks, exp = signed_blocks
     got = fabric.block_signatures_preverify(blocks)
     assert [tuple(g) for g in got] == exp
+
+
+# ---------------------------------------------------------------- BFT block signatures
+@pytest.fixture(scope="module")
+def bft_blocks():
+    return F.generate_bft_signed_blocks(nblocks=len(F.BFT_BLOCKSIG_CORRUPTIONS),
+                                        classes=F.BFT_BLOCKSIG_CORRUPTIONS)
+
+
+def test_bft_oracle_matches_construction(bft_blocks):
+    blocks, cons, exp = bft_blocks
+    assert [R.block_signatures(b, _py_verify, bft=True, consenters=cons) for b in blocks] == exp
+
+
+def test_bft_reference_cases():
+    """protoutil/blockutils_test.go:382-493 restated on the oracle and the C++
+    decode: empty metadata; signatures by identifier 1 and 3 resolve to
+    MarshalOrPanic(SerializedIdentity{msp1, identity1}) / {msp3, identity3};
+    a SignatureHeader signature keeps the creator form with bftEnabled."""
+    cons = [(1, b"msp1", b"identity1"), (2, b"msp2", b"identity2"), (3, b"msp3", b"identity3")]
+    assert R.search_consenter_identity_by_id(cons, 1) == b"\n\x04msp1\x12\tidentity1"
+    assert R.search_consenter_identity_by_id(cons, 3) == b"\n\x04msp3\x12\tidentity3"
+    assert R.search_consenter_identity_by_id(cons, 4) == b""
+    empty = F.pb_bytes(1, b"")  # header {}, metadata {}
+    by_id = F.pb_bytes(1, b"") + F.pb_bytes(3, F.pb_bytes(1, F.pb_bytes(2, F.pb_bytes(
+        3, F.pb_varint(1, 1))) + F.pb_bytes(2, F.pb_bytes(3, F.pb_varint(1, 3)))))
+    by_creator = F.pb_bytes(1, b"") + F.pb_bytes(3, F.pb_bytes(1, F.pb_bytes(2, F.pb_bytes(
+        1, F.pb_bytes(1, b"creator1")))))
+    # the identities are not certificates: DeserializeIdentity fails -> 254
+    want = [(R.BLK_NO_SIGNATURES, [], 0), (R.BLK_OK, [254, 254], 0), (R.BLK_OK, [254], 0)]
+    cases = [empty, by_id, by_creator]
+    assert [R.block_signatures(b, None, decode_only=True, bft=True, consenters=cons)
+            for b in cases] == want
+    got = fabric.block_signatures_preverify(cases, decode_only=True, bft=True, consenters=cons)
+    assert [tuple(g) for g in got] == want
+    # without bftEnabled the identifier form is a SignatureHeader form with an
+    # empty header: empty creator -> 254 for both
+    assert R.block_signatures(by_id, None, decode_only=True, bft=False)[1] == [254, 254]
+
+
+def test_bft_decode_matches_oracle(bft_blocks):
+    blocks, cons, _ = bft_blocks
+    rng = random.Random(15)
+    cases = list(blocks) + [_mutate(rng, rng.choice(blocks)) for _ in range(1000)]
+    for bft in (True, False):
+        py = [R.block_signatures(b, None, decode_only=True, bft=bft, consenters=cons) for b in cases]
+        cc = fabric.block_signatures_preverify(cases, decode_only=True, bft=bft, consenters=cons)
+        assert py == [tuple(c) for c in cc]
+
+
+@pytest.mark.gpu
+def test_gpu_bft_block_signatures(bft_blocks):
+    blocks, cons, exp = bft_blocks
+    want = [R.block_signatures(b, _orc_verify, bft=True, consenters=cons) for b in blocks]
+    assert want == exp
+    got = fabric.block_signatures_preverify(blocks, bft=True, consenters=cons)
+    assert [tuple(g) for g in got] == exp
+    # the same blocks without bftEnabled: identifier-form signatures have no creator
+    got = fabric.block_signatures_preverify(blocks, consenters=cons)
+    assert [tuple(g) for g in got] == [R.block_signatures(b, _orc_verify) for b in blocks]
+
+
+@pytest.mark.gpu
+def test_gpu_sets_many_failed_duplicates():
+    """An identity that repeats itself after bad signatures (Go verifies each
+    until one verifies): 300 failing entries then a valid one then more --
+    two device passes, bit-exact with the sequential loop."""
+    sets = _sets_case()
+    sds = [sd for s in sets for sd in s]
+    good = next(sd for sd in sds if R.signature_set_to_valid_identities([sd], _orc_verify)[1] == 1)
+    bad = (good[0], good[1] + b"x", good[2])
+    other = next(sd for sd in sds if sd[0] != good[0])
+    big = [bad] * 300 + [good, bad, other, good]
+    cases = [big, [bad, bad], [good, bad, good]]
+    want = [R.signature_set_to_valid_identities(s, _orc_verify) for s in cases]
+    assert want[0][0][300] == 0 and want[0][0][301] == 253
+    assert fabric.signature_sets_verify(cases) == want
