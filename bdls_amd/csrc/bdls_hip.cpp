@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -20,6 +21,7 @@
 #include <functional>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <thread>
 #include <vector>
 
@@ -35,6 +37,8 @@ hipError_t launch_verify_bdls(int curve, const BdlsIn& in, const Work& w, const 
                               const KeyReg& g, const uint32_t* gtab, uint32_t n,
                               const LaunchOpts& o, uint64_t* bitmap, uint8_t* reason,
                               hipStream_t s, hipEvent_t* ev);
+hipError_t launch_small(int curve, const BatchIn& in, const Work& w, const KeyReg& g,
+                        const uint32_t* gtab, uint32_t n, uint8_t* reason, hipStream_t s);
 hipError_t launch_register(int curve, const uint8_t* pub, const Work& w, const Plan& pl,
                            const KeyReg& g, uint32_t n, uint8_t* status, hipStream_t s);
 }  // namespace bh
@@ -139,6 +143,7 @@ struct HostBuf {
 // outputs, and the events that order upload -> verify -> download. While the
 // compute stream verifies one slot's batch, the copy stream uploads the next.
 struct Slot {
+  HostBuf host_in;  // latency path: the small batch packed on the host
   DevBuf stage;     // inputs (H2D on the copy stream)
   DevBuf out;       // bitmap words + reasons (device)
   HostBuf host_out; // bitmap words + reasons (pinned, D2H on the compute stream)
@@ -158,6 +163,9 @@ struct Dev {
   DevBuf ws;     // Work + Plan
   DevBuf stage;  // key registration input
   DevBuf out;    // key registration status
+  HostBuf reg_in;                 // coalescer: keys to register (pinned)
+  hipEvent_t reg_done = nullptr;  // their upload + registration pass
+  bool reg_pending = false;
   Slot slot[kSlots];
   uint32_t next_slot = 0;
   Registry reg[2];
@@ -312,7 +320,10 @@ void dev_free(Dev& d) {
   d.ws.release();
   d.stage.release();
   d.out.release();
+  d.reg_in.release();
+  if (d.reg_done) (void)hipEventDestroy(d.reg_done);
   for (Slot& sl : d.slot) {
+    sl.host_in.release();
     sl.stage.release();
     sl.out.release();
     sl.host_out.release();
@@ -596,6 +607,7 @@ struct Part {
   int slot;
   size_t lo, m;
   bool done;
+  bool small = false;  // latency path: reasons only (bitmap formed here)
 };
 
 }  // namespace
@@ -623,6 +635,13 @@ int finish_part(bh_job* j, size_t k) {
   HIPCHK(hipSetDevice(d.id));
   hipError_t e = hipEventSynchronize(sl.done);
   if (e != hipSuccess) return fail(BH_E_DEVICE, std::string("pass failed: ") + hipGetErrorString(e));
+  if (p.small) {
+    const uint8_t* rs = (const uint8_t*)sl.host_out.p;
+    std::memcpy(j->reason + p.lo, rs, p.m);
+    for (size_t i = 0; i < p.m; i++)
+      if (rs[i] == BH_R_OK) j->bitmap[(p.lo + i) >> 3] |= (uint8_t)(1u << ((p.lo + i) & 7));
+    return BH_OK;
+  }
   const uint64_t* words = (const uint64_t*)sl.host_out.p;
   const uint8_t* rs = (const uint8_t*)(words + round64(p.m) / 64);
   std::memcpy(j->bitmap + p.lo / 8, words, (p.m + 7) / 8);  // lo is a multiple of 64
@@ -669,6 +688,93 @@ int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, 
   return BH_OK;
 }
 
+// ---- latency path ------------------------------------------------------------
+// A small host batch (<= kSmallMax records of the bh_batch kind, P-256, no
+// BH_F_KEEP_KEYS) skips the batch machinery: its fields are packed into the
+// slot's pinned buffer on the host (one H2D copy instead of seven), one
+// kernel (k_small: prep, the record's own inverse, registry lookup, key-table
+// or ladder u2 Q, G comb, check) replaces the fourteen stream operations of a
+// batch pass, and only the reason bytes come back (the bitmap is formed on
+// the host). A lone BCCSP Verify is such a batch.
+constexpr size_t kSmallMax = 256;
+
+bool small_ok(int curve, const bh_batch* b, size_t n, uint32_t flags) {
+  (void)b;
+  return curve == BH_CURVE_P256 && n && n <= kSmallMax && !(flags & BH_F_KEEP_KEYS);
+}
+bool small_ok(int, const SegBatch*, size_t, uint32_t) { return false; }
+bool small_ok(int, const bh_bdls_batch*, size_t, uint32_t) { return false; }
+
+int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, size_t m,
+                  uint32_t flags) {
+  HIPCHK(hipSetDevice(d.id));
+  const int k = (int)(d.next_slot++ % kSlots);
+  Slot& sl = d.slot[k];
+  if (sl.owner) {
+    bh_job* o = sl.owner;
+    int rc = finish_part(o, sl.owner_part);
+    if (rc && o->rc == BH_OK) {
+      o->rc = rc;
+      o->err = g_err;
+    }
+  }
+  // layout: pub | sig_off | sig_len | msg_off | msg_len | sig bytes | msg bytes
+  size_t sig_bytes = 0, msg_bytes = 0;
+  for (size_t i = lo; i < lo + m; i++) {
+    sig_bytes += b->sig_len[i];
+    msg_bytes += b->msg_len[i];
+  }
+  const size_t o_pub = 0, o_soff = round256(m * 64), o_slen = o_soff + round256(m * 8),
+               o_moff = o_slen + round256(m * 4), o_mlen = o_moff + round256(m * 8),
+               o_sig = o_mlen + round256(m * 4), o_msg = o_sig + round256(sig_bytes + 1),
+               total = o_msg + round256(msg_bytes + 1);
+  int rc;
+  if ((rc = sl.host_in.ensure(total)) || (rc = sl.stage.ensure(total)) ||
+      (rc = sl.out.ensure(m + 256)) || (rc = sl.host_out.ensure(m + 256)))
+    return rc;
+  char* h = (char*)sl.host_in.p;
+  std::memcpy(h + o_pub, b->pub + lo * 64, m * 64);
+  uint64_t* soff = (uint64_t*)(h + o_soff);
+  uint32_t* slen = (uint32_t*)(h + o_slen);
+  uint64_t* moff = (uint64_t*)(h + o_moff);
+  uint32_t* mlen = (uint32_t*)(h + o_mlen);
+  size_t sp = 0, mp = 0;
+  for (size_t i = 0; i < m; i++) {
+    const size_t sl_ = b->sig_len[lo + i], ml = b->msg_len[lo + i];
+    soff[i] = sp;
+    slen[i] = (uint32_t)sl_;
+    if (sl_) std::memcpy(h + o_sig + sp, b->sig + b->sig_off[lo + i], sl_);
+    sp += sl_;
+    moff[i] = mp;
+    mlen[i] = (uint32_t)ml;
+    if (ml) std::memcpy(h + o_msg + mp, b->msg + b->msg_off[lo + i], ml);
+    mp += ml;
+  }
+  hipStream_t s = d.stream;
+  if (d.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.done, 0));
+  char* dv = (char*)sl.stage.p;
+  HIPCHK(hipMemcpyAsync(dv, h, total, hipMemcpyHostToDevice, s));
+  bh::Work w;
+  bh::Plan pl;
+  if ((rc = carve_work(d, m, &w, &pl))) return rc;
+  const bh::BatchIn in{(const uint8_t*)(dv + o_pub), (const uint8_t*)(dv + o_sig),
+                       (const uint64_t*)(dv + o_soff), (const uint32_t*)(dv + o_slen),
+                       (const uint8_t*)(dv + o_msg), (const uint64_t*)(dv + o_moff),
+                       (const uint32_t*)(dv + o_mlen), flags};
+  HIPCHK(bh::launch_small(curve, in, w, d.reg[curve].g, d.gtab[curve], (uint32_t)m,
+                          (uint8_t*)sl.out.p, s));
+  HIPCHK(hipMemcpyAsync(sl.host_out.p, sl.out.p, m, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(sl.done, s));
+  HIPCHK(hipEventRecord(d.done, s));
+  d.done_recorded = true;
+  sl.owner = j;
+  sl.owner_part = j->parts.size();
+  Part part{&d, k, lo, m, false};
+  part.small = true;
+  j->parts.push_back(part);
+  return BH_OK;
+}
+
 int wait_job(bh_job* j) {
   int rc = j->rc;
   std::string err = j->err;
@@ -699,6 +805,23 @@ int submit_job(int curve, const B* b, size_t n, uint32_t flags, uint8_t* bitmap,
   j->reason = reason;
   j->n = n;
   if (n) std::memset(bitmap, 0, (n + 7) / 8);
+  if (small_ok(curve, b, n, flags) && !getenv("BH_NO_SMALL")) {
+    // one device (round robin): a small batch does not shard
+    static std::atomic<uint32_t> rr{0};
+    Dev& d = *devs[rr++ % devs.size()];
+    int rc;
+    {
+      std::lock_guard<std::mutex> g(d.mu);
+      rc = enqueue_small(j, d, curve, reinterpret_cast<const bh_batch*>(b), 0, n, flags);
+    }
+    if (rc) {
+      const std::string err = g_err;
+      (void)wait_job(j);
+      return fail(rc, err);
+    }
+    *out = j;
+    return BH_OK;
+  }
   const size_t nd = std::min(devs.size(), (n + 63) / 64);
   const size_t per = nd ? round64((n + nd - 1) / nd) : 0;
   for (size_t k = 0; k < nd; k++) {
@@ -763,6 +886,40 @@ int for_devices(int device, const std::function<int(Dev&)>& fn) {
   return BH_OK;
 }
 
+// Queue the registration of n keys on every device without waiting for it:
+// upload + bh_keys_register's kernel sequence on the compute stream, ordered
+// before the next pass (d.done). Errors are ignored (a key that does not
+// register stays on the ladder; results never depend on the registry).
+void register_async(int curve, const uint8_t* pub, size_t n) {
+  n = std::min<size_t>(n, 1 << 16);
+  for (Dev* dp : all_devs()) {
+    Dev& d = *dp;
+    std::lock_guard<std::mutex> g(d.mu);
+    if (hipSetDevice(d.id) != hipSuccess) continue;
+    if (d.reg[curve].g.cap == 0 && reg_alloc(d, curve, kDefaultRegCap)) continue;
+    if (d.reg_pending) {  // the previous registration still reads reg_in
+      if (hipEventSynchronize(d.reg_done) != hipSuccess) continue;
+      d.reg_pending = false;
+    }
+    if (!d.reg_done && hipEventCreateWithFlags(&d.reg_done, hipEventDisableTiming) != hipSuccess)
+      continue;
+    if (d.reg_in.ensure(n * 64) || d.stage.ensure(n * 64 + 256) || d.out.ensure(n + 256)) continue;
+    std::memcpy(d.reg_in.p, pub, n * 64);
+    bh::Work w;
+    bh::Plan pl;
+    if (carve_work(d, n, &w, &pl, true)) continue;
+    hipStream_t s = d.stream;
+    if (d.done_recorded && hipStreamWaitEvent(s, d.done, 0) != hipSuccess) continue;
+    if (hipMemcpyAsync(d.stage.p, d.reg_in.p, n * 64, hipMemcpyHostToDevice, s) != hipSuccess)
+      continue;
+    if (bh::launch_register(curve, (const uint8_t*)d.stage.p, w, pl, d.reg[curve].g,
+                            (uint32_t)n, (uint8_t*)d.out.p, s) != hipSuccess)
+      continue;
+    if (hipEventRecord(d.reg_done, s) == hipSuccess) d.reg_pending = true;
+    if (hipEventRecord(d.done, s) == hipSuccess) d.done_recorded = true;
+  }
+}
+
 // ---- coalescing single-signature verifier -------------------------------------
 // BCCSP.Verify is called one signature at a time by up to validatorPoolSize
 // goroutines (core/peer/config.go:269-272, fan-out v20/validator.go:193-208),
@@ -808,6 +965,28 @@ struct Coalescer {
   size_t cap = 65536;      // records per batch at most
   size_t max_inflight = 2; // = pipeline slots per device
   long linger_us = 0;
+  // Keys are registered in the device key registry on their register_after-th
+  // sighting (0 = never): the device-side twin of the MSP identity cache, so a
+  // long-lived identity's later Verify calls take the key-table route (no
+  // doublings) instead of the ladder. The registration pass is queued before
+  // the batch that sees the key, which then already uses the table; a full
+  // registry leaves new keys on the ladder (results are the same either way).
+  int register_after = 1;
+  std::unordered_map<std::string, uint8_t> sightings;  // 255 = registered (or tried)
+
+  void keys_to_register(const CspBatch& b, std::vector<uint8_t>* keys) {
+    keys->clear();
+    if (register_after <= 0) return;
+    if (sightings.size() > (size_t(1) << 20)) sightings.clear();
+    for (size_t i = 0; i < b.reqs.size(); i++) {
+      uint8_t& c = sightings[std::string((const char*)b.pub.data() + 64 * i, 64)];
+      if (c == 255) continue;
+      if (++c >= register_after) {
+        c = 255;
+        keys->insert(keys->end(), b.pub.data() + 64 * i, b.pub.data() + 64 * i + 64);
+      }
+    }
+  }
 
   void complete(CspBatch& b, int rc, const std::string& err) {
     for (size_t i = 0; i < b.reqs.size(); i++) {
@@ -821,6 +1000,8 @@ struct Coalescer {
       }
     }
   }
+
+  std::vector<uint8_t> new_keys;
 
   void run() {
     std::unique_lock<std::mutex> lk(mu);
@@ -840,6 +1021,7 @@ struct Coalescer {
           spare.pop_back();
         }
         filling->clear();
+        cv_done.notify_all();  // callers waiting for room in a full batch
         const size_t n = b->reqs.size();
         n_req += n;
         n_batch++;
@@ -849,6 +1031,8 @@ struct Coalescer {
         b->reason.assign(n, 0);
         b->b = bh_batch{b->pub.data(), b->sig.data(), b->sig_off.data(), b->sig_len.data(),
                         b->dg.data(), b->dg_off.data(), b->dg_len.data()};
+        keys_to_register(*b, &new_keys);
+        if (!new_keys.empty()) register_async(BH_CURVE_P256, new_keys.data(), new_keys.size() / 64);
         int rc = submit_job(BH_CURVE_P256, &b->b, n, 0u, b->bitmap.data(), b->reason.data(),
                             &b->job);
         const std::string err = rc ? g_err : std::string();
@@ -886,6 +1070,8 @@ struct Coalescer {
         running = true;
         th = std::thread([this] { run(); });
       }
+      // a full batch (cap records) waits until the flusher takes it
+      cv_done.wait(lk, [&] { return filling->reqs.size() < cap; });
       CspBatch& b = *filling;
       b.pub.insert(b.pub.end(), pub, pub + 64);
       b.sig_off.push_back(b.sig.size());
@@ -921,7 +1107,9 @@ struct Coalescer {
 Coalescer& coalescer() {
   static Coalescer* c = [] {
     Coalescer* x = new Coalescer();
+    if (const char* e = getenv("BH_COALESCE_REGISTER")) x->register_after = atoi(e);
     if (const char* e = getenv("BH_COALESCE_US")) x->linger_us = std::max(0L, atol(e));
+    if (const char* e = getenv("BH_COALESCE_CAP")) x->cap = (size_t)std::max(1L, atol(e));
     return x;
   }();
   return *c;
@@ -932,7 +1120,7 @@ Coalescer& coalescer() {
 extern "C" {
 
 const char* bh_last_error(void) { return g_err.c_str(); }
-const char* bh_version(void) { return "bdls-hip 0.2.0 (gfx950)"; }
+const char* bh_version(void) { return "bdls-hip 0.3.0 (gfx950)"; }
 
 int bh_init(uint32_t device_mask, uint32_t flags) {
   (void)flags;

@@ -563,7 +563,8 @@ BH_HD void shr_const(uint32_t v[9]) {
   for (int q = 0; q < 9; q++) {
     const uint32_t lo = (q + ws < 9) ? v[q + ws] : 0u;
     const uint32_t hi = (q + ws + 1 < 9) ? v[q + ws + 1] : 0u;
-    v[q] = bs ? ((lo >> bs) | (hi << (32 - bs))) : lo;
+    if constexpr (bs != 0) v[q] = (lo >> bs) | (hi << (32 - bs));
+    else v[q] = lo;
   }
 }
 

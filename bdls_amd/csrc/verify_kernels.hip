@@ -586,6 +586,58 @@ __global__ __launch_bounds__(256) void k_bitmap(const uint8_t* __restrict__ reas
   if ((threadIdx.x & 63u) == 0) bitmap[i >> 6] = m;
 }
 
+// ---- latency path: one launch for a small batch (bh_csp_verify_p256's
+// coalesced batches, small host batches). 16 lanes per record: lane 0 runs
+// prep and the record's own inverse (no batch inversion, no plan, no dedup)
+// and looks the key up in the registry; then the group either sums the
+// key-table windows and the G-comb windows over its 16 lanes (registered
+// key) or lane 0 runs the Booth ladder while the group adds the G-comb
+// windows (unregistered key); butterfly, lane 0 checks. Same stage functions
+// (verify.h) as the batch path, so the results are bit-identical.
+constexpr int kSmallL = 16;
+template <class P, class N, class CV, int HK>
+__global__ __launch_bounds__(256) void k_small(BatchIn in, Work w, KeyReg g,
+                                               const uint32_t* __restrict__ gtab, uint32_t n,
+                                               uint8_t* __restrict__ reason) {
+  __shared__ uint32_t tab_of[256 / kSmallL];
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j = gid / kSmallL, l = gid % kSmallL, grp = threadIdx.x / kSmallL;
+  const bool act = j < n;
+  if (act && l == 0) {
+    stage_prep<P, N, CV, HK>(in, w, j);
+    uint32_t t = kNone;
+    if ((w.st[j] & 0x7fu) == R_OK) {
+      stage_inv<N, true>(w, j, n, n);  // this record alone: u1 = e w, u2 = r w
+      t = reg_lookup(g, w, j, key_hash(w, j));
+    }
+    tab_of[grp] = t;
+  }
+  __syncthreads();  // w (global) and tab_of (LDS) visible to the group
+  if (!act) return;  // whole groups (and whole waves past n) leave together
+  const uint8_t st = w.st[j] & 0x7fu;
+  if (st != R_OK) {
+    if (l == 0) reason[j] = st;
+    return;
+  }
+  const uint32_t t = tab_of[grp];
+  J30 C;
+  bool c_inf;
+  if (t != kNone) {
+    keycomb_part<P, kSmallL>(C, c_inf, w, gtab, j, g.tables + (size_t)t * kKTabWords, l);
+  } else {
+    f_const(C.X, P::r1);
+    f_const(C.Y, P::r1);
+    f_const(C.Z, P::r1);
+    c_inf = true;
+    if (l == 0) q_ladder<P>(C, c_inf, w, j, j >> 6, j & 63u);  // Q-table slot = record
+    uint32_t u1[8];
+    ld8(u1, w.e, j, w.ns);
+    g_comb_part<P, kSmallL>(C, c_inf, gtab, u1, l);
+  }
+  group_sum<P, kSmallL>(C, c_inf);
+  if (l == 0) reason[j] = finish_check<P>(w, j, C, c_inf, C, true) ? R_OK : R_MATH;
+}
+
 // G comb table (see verify.h gtab_entry): one lane per entry.
 template <class P>
 __global__ __launch_bounds__(64) void k_gtab_build(uint32_t* gtab) {
@@ -915,6 +967,21 @@ hipError_t launch_verify_bdls(int curve, const BdlsIn& in, const Work& w, const 
   if (curve == 0)
     return seq<F30_p256, Fn_p256, Cv_p256>(in, w, pl, g, gtab, n, o, bitmap, reason, s, ev);
   return seq<F30_k1, Fn_k1, Cv_k1>(in, w, pl, g, gtab, n, o, bitmap, reason, s, ev);
+}
+
+// The latency path (k_small): P-256 Fabric / BCCSP records only; reasons only
+// (the host forms the bitmap).
+hipError_t launch_small(int curve, const BatchIn& in, const Work& w, const KeyReg& g,
+                        const uint32_t* gtab, uint32_t n, uint8_t* reason, hipStream_t s) {
+  if (curve != 0 || !n) return n ? hipErrorInvalidValue : hipSuccess;
+  const dim3 grd((n * kSmallL + 255) / 256), blk(256);
+  if (in.flags & BHF_HASH_SHA3_256)
+    hipLaunchKernelGGL((k_small<F30_p256, Fn_p256, Cv_p256, HK_SHA3_256>), grd, blk, 0, s, in, w,
+                       g, gtab, n, reason);
+  else
+    hipLaunchKernelGGL((k_small<F30_p256, Fn_p256, Cv_p256, HK_GIVEN_OR_SHA256>), grd, blk, 0, s,
+                       in, w, g, gtab, n, reason);
+  return hipGetLastError();
 }
 
 // bh_keys_register: import, dedup against the registry and within the call,

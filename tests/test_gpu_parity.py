@@ -8,6 +8,8 @@ Bit-exact bar: bitmap AND per-record reason equal the oracle's on
   * ragged / edge batch sizes (0, 1, 63, 64, 65, ...) and the device-resident API.
 """
 import ctypes
+import json
+import os
 import random
 import threading
 
@@ -18,7 +20,7 @@ from bdls_amd import _lib
 from bdls_amd.bccsp import (BCCSPError, ECDSAPublicKey, HipCSP, R_HIGH_S, R_DER, verify_packed,
                             pack_records)
 from oracle import ecdsa_ref as O
-from tests.conftest import pack
+from tests.conftest import ROOT, pack
 
 pytestmark = pytest.mark.gpu
 C = O.P256
@@ -308,3 +310,39 @@ def test_two_span_messages(csp, family):
     rc = _lib.lib().bh_verify_2seg(_lib.BH_CURVE_P256, ctypes.byref(b), o2.ctypes.data,
                                    l2.ctypes.data, w.n, 0, bitmap.ctypes.data, reason.ctypes.data)
     assert rc != 0
+
+
+@pytest.mark.gpu
+def test_coalescer_cap_enforced():
+    """BH_COALESCE_CAP bounds the records of one coalesced device batch: 32
+    threads against a cap of 4 (a child process, so the coalescer reads the
+    variable at its first use)."""
+    import subprocess
+    import sys
+    code = (
+        "import ctypes, json, threading, sys\n"
+        "sys.path.insert(0, '.')\n"
+        "from bdls_amd import _lib\n"
+        "from tests.conftest import ROOT\n"
+        "recs = [json.loads(l) for l in open(ROOT + '/tests/golden/p256_vectors.jsonl')][:64]\n"
+        "L = _lib.lib(); _lib.ensure_init()\n"
+        "bad = []\n"
+        "def worker(j):\n"
+        "    for k in range(20):\n"
+        "        r = recs[(j * 7 + k) % len(recs)]\n"
+        "        v, rs = ctypes.c_int(), ctypes.c_int()\n"
+        "        pub = int(r['qx'], 16).to_bytes(32, 'big') + int(r['qy'], 16).to_bytes(32, 'big')\n"
+        "        sig, dg = bytes.fromhex(r['sig']), bytes.fromhex(r['digest'])\n"
+        "        _lib.check(L.bh_csp_verify_p256(pub, sig, len(sig), dg, len(dg), ctypes.byref(v), ctypes.byref(rs)))\n"
+        "        if (bool(v.value), rs.value) != (r['valid'], r['reason']): bad.append(r['tag'])\n"
+        "th = [threading.Thread(target=worker, args=(j,)) for j in range(32)]\n"
+        "[t.start() for t in th]; [t.join() for t in th]\n"
+        "st = (ctypes.c_uint64 * 3)(); _lib.check(L.bh_csp_stats(st))\n"
+        "print(json.dumps({'bad': bad, 'req': st[0], 'batches': st[1], 'max': st[2]}))\n")
+    env = dict(os.environ, BH_COALESCE_CAP="4")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert not res["bad"], res["bad"][:5]
+    assert res["req"] == 640 and 1 <= res["max"] <= 4, res
