@@ -38,7 +38,8 @@ hipError_t launch_verify_bdls(int curve, const BdlsIn& in, const Work& w, const 
                               const LaunchOpts& o, uint64_t* bitmap, uint8_t* reason,
                               hipStream_t s, hipEvent_t* ev);
 hipError_t launch_small(int curve, const BatchIn& in, const Work& w, const KeyReg& g,
-                        const uint32_t* gtab, uint32_t n, uint8_t* reason, hipStream_t s);
+                        const uint32_t* gtab, uint32_t n, uint8_t* reason, hipStream_t s,
+                        uint32_t bs);
 hipError_t launch_register(int curve, const uint8_t* pub, const Work& w, const Plan& pl,
                            const KeyReg& g, uint32_t n, uint8_t* status, hipStream_t s);
 }  // namespace bh
@@ -359,6 +360,13 @@ std::vector<Dev*> all_devs() {
   return g_devs;
 }
 
+// threads per workgroup from the environment (64 / 128 / 256), read once
+uint32_t env_block(const char* name, uint32_t dflt) {
+  const char* e = getenv(name);
+  const long v = e ? atol(e) : 0L;
+  return (v == 64 || v == 128 || v == 256) ? (uint32_t)v : dflt;
+}
+
 bh::LaunchOpts launch_opts(size_t m, uint32_t flags) {
   bh::LaunchOpts o;
   // records per inversion lane: ~2 waves per SIMD at 1M records (measured
@@ -377,6 +385,7 @@ bh::LaunchOpts launch_opts(size_t m, uint32_t flags) {
   o.min_batch = o.keep ? 0u : bh::kKeyTableMinBatch;
   // below chip size, spread each key-table record over 16 or 4 lanes
   o.wide = bh::wide_for(m);
+  o.wide_block = env_block("BH_WIDE_BLOCK", 256);
   return o;
 }
 
@@ -761,8 +770,9 @@ int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, si
                        (const uint64_t*)(dv + o_soff), (const uint32_t*)(dv + o_slen),
                        (const uint8_t*)(dv + o_msg), (const uint64_t*)(dv + o_moff),
                        (const uint32_t*)(dv + o_mlen), flags};
+  const uint32_t small_block = env_block("BH_SMALL_BLOCK", 64);
   HIPCHK(bh::launch_small(curve, in, w, d.reg[curve].g, d.gtab[curve], (uint32_t)m,
-                          (uint8_t*)sl.out.p, s));
+                          (uint8_t*)sl.out.p, s, small_block));
   HIPCHK(hipMemcpyAsync(sl.host_out.p, sl.out.p, m, hipMemcpyDeviceToHost, s));
   HIPCHK(hipEventRecord(sl.done, s));
   HIPCHK(hipEventRecord(d.done, s));

@@ -114,6 +114,7 @@ struct LaunchOpts {
   uint32_t min_batch;  // no per-batch tables below this batch size
   bool keep;           // BH_F_KEEP_KEYS: new tables go to the key registry
   int wide;            // lanes per record on the key-table path (1, 4, 16)
+  uint32_t wide_block = 256;  // threads per workgroup of the multi-lane kernels
   // BDLS batches: the BLAKE2b digests run on a second stream (hipStream_t)
   // beside prep / inverse / plan / the u2 Q halves; fork and join are
   // hipEvent_t. Opaque here so the host harness compiles this header.
@@ -915,10 +916,7 @@ BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_
 //   entry (win, j) = (j+1) 2^(4 win) Q,  win in [0, 65), j in [0, 8)
 // (Jacobian, 28 words). u2 Q is then 65 table additions with 4-bit signed
 // digits in [-7, 8] and no doublings.
-#ifndef BH_KTAB_W
-#define BH_KTAB_W 4
-#endif
-constexpr int kKW = BH_KTAB_W;                   // signed-window width (bits)
+constexpr int kKW = 4;                           // signed-window width (bits)
 constexpr int kKWin = (257 + kKW - 1) / kKW;     // 65 windows at 4 bits
 constexpr int kKEnt = 1 << (kKW - 1);            // 8 entries per window at 4 bits
 constexpr uint32_t kKTabWords = (uint32_t)kKWin * kKEnt * kQPt;
@@ -1026,25 +1024,17 @@ BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint3
   f_const(A.X, P::r1);
   f_const(A.Y, P::r1);
   f_const(A.Z, P::r1);
-  uint32_t v[9], carry = 0;
-  if constexpr (kKW != 4) recode_koff(v, k2);
+  uint32_t carry = 0;
   for (int win = 0; win < kKWin; win++) {
-    uint32_t mag;
-    bool neg;
-    if constexpr (kKW == 4) {  // carry-scan digits in [-7, 8] (the measured default)
-      const uint32_t t = (k2[0] & 0xfu) + carry;
+    // carry-scan digits in [-7, 8] (the wide path's recode_koff gives offset
+    // digits in [-8, 7]: the same scalar, another digit string)
+    const uint32_t t = (k2[0] & 0xfu) + carry;
 #pragma unroll
-      for (int k = 0; k < 7; k++) k2[k] = (k2[k] >> 4) | (k2[k + 1] << 28);
-      k2[7] >>= 4;
-      neg = t > 8u;
-      mag = neg ? 16u - t : t;
-      carry = neg ? 1u : 0u;
-    } else {  // offset digits in [-kKEnt, kKEnt - 1]
-      const int d = (int)(v[0] & (2u * kKEnt - 1u)) - kKEnt;
-      shr_const<kKW>(v);
-      mag = (uint32_t)(d < 0 ? -d : d);
-      neg = d < 0;
-    }
+    for (int k = 0; k < 7; k++) k2[k] = (k2[k] >> 4) | (k2[k + 1] << 28);
+    k2[7] >>= 4;
+    const bool neg = t > 8u;
+    const uint32_t mag = neg ? 16u - t : t;
+    carry = neg ? 1u : 0u;
     J30 T;
     ktab_load(T, tab, win, mag ? mag - 1 : 0);
     if (neg) f_neg<P, 64>(T.Y, T.Y);
@@ -1216,7 +1206,11 @@ BH_HD uint32_t reg_lookup(const KeyReg& g, const Work& w, uint32_t i, uint64_t h
 // sums are combined by a butterfly over the group. The signed digits come
 // from one offset addition instead of a carry scan (recode_koff for the key
 // tables, recode_goff for the G comb), so every lane reads its windows
-// directly. Same digits as q_keycomb.
+// directly. These digits (in [-8, 7]) differ from q_keycomb's carry-scan
+// digits (in [-7, 8]) but represent the same scalar, so the sums are the same
+// point; the two paths may meet the rare degenerate addition (A = +-T) on
+// different inputs, and both resolve it exactly (tests/test_hostsim.py and
+// tests/test_bdls.py run crafted scalars through both).
 
 // o = v >> sh (288-bit), 0 <= sh < 192
 BH_HD void shr288(uint32_t o[9], const uint32_t v[9], uint32_t sh) {

@@ -586,15 +586,17 @@ __global__ __launch_bounds__(256) void k_bitmap(const uint8_t* __restrict__ reas
   if ((threadIdx.x & 63u) == 0) bitmap[i >> 6] = m;
 }
 
-// ---- latency path: one launch for a small batch (bh_csp_verify_p256's
-// coalesced batches, small host batches). 16 lanes per record: lane 0 runs
-// prep and the record's own inverse (no batch inversion, no plan, no dedup)
-// and looks the key up in the registry; then the group either sums the
-// key-table windows and the G-comb windows over its 16 lanes (registered
-// key) or lane 0 runs the Booth ladder while the group adds the G-comb
-// windows (unregistered key); butterfly, lane 0 checks. Same stage functions
-// (verify.h) as the batch path, so the results are bit-identical.
+// ---- latency path: two launches for a small batch (bh_csp_verify_p256's
+// coalesced batches, small host batches). 16 lanes per record. k_small: lane
+// 0 runs prep and the record's own inverse (no batch inversion, no plan, no
+// dedup) and looks the key up in the registry; a registered key's record is
+// finished by the group (key-table and G-comb windows over 16 lanes,
+// butterfly, lane 0 checks); an unregistered one is marked for k_small_lad
+// (lane 0 runs the Booth ladder while the group adds the G-comb windows) --
+// a separate kernel so that neither carries the other's registers. Same
+// stage functions (verify.h) as the batch path: bit-identical results.
 constexpr int kSmallL = 16;
+constexpr uint8_t kSmallLadder = 0xfeu;  // reason placeholder: k_small_lad's record
 template <class P, class N, class CV, int HK>
 __global__ __launch_bounds__(256) void k_small(BatchIn in, Work w, KeyReg g,
                                                const uint32_t* __restrict__ gtab, uint32_t n,
@@ -615,25 +617,33 @@ __global__ __launch_bounds__(256) void k_small(BatchIn in, Work w, KeyReg g,
   __syncthreads();  // w (global) and tab_of (LDS) visible to the group
   if (!act) return;  // whole groups (and whole waves past n) leave together
   const uint8_t st = w.st[j] & 0x7fu;
-  if (st != R_OK) {
-    if (l == 0) reason[j] = st;
+  const uint32_t t = tab_of[grp];
+  if (st != R_OK || t == kNone) {
+    if (l == 0) reason[j] = st != R_OK ? st : kSmallLadder;
     return;
   }
-  const uint32_t t = tab_of[grp];
   J30 C;
   bool c_inf;
-  if (t != kNone) {
-    keycomb_part<P, kSmallL>(C, c_inf, w, gtab, j, g.tables + (size_t)t * kKTabWords, l);
-  } else {
-    f_const(C.X, P::r1);
-    f_const(C.Y, P::r1);
-    f_const(C.Z, P::r1);
-    c_inf = true;
-    if (l == 0) q_ladder<P>(C, c_inf, w, j, j >> 6, j & 63u);  // Q-table slot = record
-    uint32_t u1[8];
-    ld8(u1, w.e, j, w.ns);
-    g_comb_part<P, kSmallL>(C, c_inf, gtab, u1, l);
-  }
+  keycomb_part<P, kSmallL>(C, c_inf, w, gtab, j, g.tables + (size_t)t * kKTabWords, l);
+  group_sum<P, kSmallL>(C, c_inf);
+  if (l == 0) reason[j] = finish_check<P>(w, j, C, c_inf, C, true) ? R_OK : R_MATH;
+}
+
+template <class P>
+__global__ __launch_bounds__(256) void k_small_lad(Work w, const uint32_t* __restrict__ gtab,
+                                                   uint32_t n, uint8_t* __restrict__ reason) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j = gid / kSmallL, l = gid % kSmallL;
+  if (j >= n || reason[j] != kSmallLadder) return;  // whole groups leave together
+  J30 C;
+  bool c_inf = true;
+  f_const(C.X, P::r1);
+  f_const(C.Y, P::r1);
+  f_const(C.Z, P::r1);
+  if (l == 0) q_ladder<P>(C, c_inf, w, j, j >> 6, j & 63u);  // Q-table slot = record
+  uint32_t u1[8];
+  ld8(u1, w.e, j, w.ns);
+  g_comb_part<P, kSmallL>(C, c_inf, gtab, u1, l);
   group_sum<P, kSmallL>(C, c_inf);
   if (l == 0) reason[j] = finish_check<P>(w, j, C, c_inf, C, true) ? R_OK : R_MATH;
 }
@@ -821,6 +831,11 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   constexpr bool kBdls = std::is_same_v<IN, BdlsIn>;
   const dim3 blk(256);
   const dim3 grd((n + 255) / 256);
+  // the multi-lane kernels of small batches: o.wide_block threads per
+  // workgroup (64: one wave each, spread over CUs)
+  const uint32_t wb = o.wide_block ? o.wide_block : 256u;
+  const dim3 wblk(wb);
+  auto wgrd = [&](uint32_t lanes) { return dim3((lanes + wb - 1) / wb); };
   const uint32_t nlanes = (n + o.inv_chunk - 1) / o.inv_chunk;  // records per lane ~ inv_chunk
   const dim3 grc((nlanes + 255) / 256);
   bool fused = false;  // Fabric records whose digest the device computes
@@ -898,29 +913,29 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
     hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, plc, g, gtab, reason,
                        tab_blocks, 0u);
     if constexpr (!P::a_is_minus3)
-      hipLaunchKernelGGL((k_ladder2_q<P>), dim3((2 * n + 255) / 256), blk, 0, s, w, plc,
+      hipLaunchKernelGGL((k_ladder2_q<P>), wgrd(2 * n), wblk, 0, s, w, plc,
                          pstride);
     else
-      hipLaunchKernelGGL((k_ladder1_q<P>), grd, blk, 0, s, w, plc, pstride);
+      hipLaunchKernelGGL((k_ladder1_q<P>), wgrd(n), wblk, 0, s, w, plc, pstride);
     if (o.wide == 16)
-      hipLaunchKernelGGL((k_keycomb_wide_q<P, 16>), dim3((n * 16 + 255) / 256), blk, 0, s, w, plc,
+      hipLaunchKernelGGL((k_keycomb_wide_q<P, 16>), wgrd(n * 16), wblk, 0, s, w, plc,
                          g, pbase, pstride);
     else
-      hipLaunchKernelGGL((k_keycomb_wide_q<P, 4>), dim3((n * 4 + 255) / 256), blk, 0, s, w, plc, g,
+      hipLaunchKernelGGL((k_keycomb_wide_q<P, 4>), wgrd(n * 4), wblk, 0, s, w, plc, g,
                          pbase, pstride);
     REC(4);
     if (o.keep)
       hipLaunchKernelGGL(k_reg_publish, dim3((pl.max_tables + 255) / 256), blk, 0, s, w, plc, g);
     if ((e = join())) return e;
     hipLaunchKernelGGL((k_ladder2_g<P, N, P::a_is_minus3 ? 1 : 2>),
-                       dim3((kLadGLanes * n + 255) / 256), blk, 0, s, w, plc, gtab, reason,
+                       wgrd(kLadGLanes * n), wblk, 0, s, w, plc, gtab, reason,
                        pstride);
     REC(5);
     if (o.wide == 16)
-      hipLaunchKernelGGL((k_keycomb_wide_g<P, N, 16>), dim3((n * 16 + 255) / 256), blk, 0, s, w,
+      hipLaunchKernelGGL((k_keycomb_wide_g<P, N, 16>), wgrd(n * 16), wblk, 0, s, w,
                          plc, gtab, reason, pbase, pstride);
     else
-      hipLaunchKernelGGL((k_keycomb_wide_g<P, N, 4>), dim3((n * 4 + 255) / 256), blk, 0, s, w,
+      hipLaunchKernelGGL((k_keycomb_wide_g<P, N, 4>), wgrd(n * 4), wblk, 0, s, w,
                          plc, gtab, reason, pbase, pstride);
     hipLaunchKernelGGL(k_bitmap, grd, blk, 0, s, reason, n, bitmap);
     REC(6);
@@ -935,11 +950,11 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   REC(5);
   switch (o.wide) {
     case 4:
-      hipLaunchKernelGGL((k_keycomb_wide<P, 4>), dim3((n * 4 + 255) / 256), blk, 0, s, w, plc, g,
+      hipLaunchKernelGGL((k_keycomb_wide<P, 4>), wgrd(n * 4), wblk, 0, s, w, plc, g,
                          gtab, reason);
       break;
     case 16:
-      hipLaunchKernelGGL((k_keycomb_wide<P, 16>), dim3((n * 16 + 255) / 256), blk, 0, s, w, plc,
+      hipLaunchKernelGGL((k_keycomb_wide<P, 16>), wgrd(n * 16), wblk, 0, s, w, plc,
                          g, gtab, reason);
       break;
     default:
@@ -971,16 +986,20 @@ hipError_t launch_verify_bdls(int curve, const BdlsIn& in, const Work& w, const 
 
 // The latency path (k_small): P-256 Fabric / BCCSP records only; reasons only
 // (the host forms the bitmap).
+// bs: threads per workgroup (64 = one wave per workgroup, so a latency-bound
+// batch of a few waves spreads over CUs instead of sharing one CU's SIMDs).
 hipError_t launch_small(int curve, const BatchIn& in, const Work& w, const KeyReg& g,
-                        const uint32_t* gtab, uint32_t n, uint8_t* reason, hipStream_t s) {
+                        const uint32_t* gtab, uint32_t n, uint8_t* reason, hipStream_t s,
+                        uint32_t bs) {
   if (curve != 0 || !n) return n ? hipErrorInvalidValue : hipSuccess;
-  const dim3 grd((n * kSmallL + 255) / 256), blk(256);
+  const dim3 grd((n * kSmallL + bs - 1) / bs), blk(bs);
   if (in.flags & BHF_HASH_SHA3_256)
     hipLaunchKernelGGL((k_small<F30_p256, Fn_p256, Cv_p256, HK_SHA3_256>), grd, blk, 0, s, in, w,
                        g, gtab, n, reason);
   else
     hipLaunchKernelGGL((k_small<F30_p256, Fn_p256, Cv_p256, HK_GIVEN_OR_SHA256>), grd, blk, 0, s,
                        in, w, g, gtab, n, reason);
+  hipLaunchKernelGGL((k_small_lad<F30_p256>), grd, blk, 0, s, w, gtab, n, reason);
   return hipGetLastError();
 }
 

@@ -149,3 +149,64 @@ def test_hostsim_two_span_messages(hs, family):
                       l2.ctypes.data, w.n, flags, out.ctypes.data)
     assert (out == w.reason).all()
     assert (l1 == 0).any() and (l2 == 0).any() and ((l1 > 64) & (l2 > 64)).any()
+
+
+def _p256_crafted_u2_records():
+    """P-256 signatures built for chosen u2 at key-table window boundaries
+    (digit carries of the carry-scan recoding, the offset recoding's borrow
+    edges, the top window, n - 1, n/2) -- R = u1 G + u2 Q, r = x(R) mod n,
+    s = r / u2, e = u1 s; plus a flipped-digest twin of each."""
+    import random
+    from oracle import ecdsa_ref as O
+    c = O.P256
+    n = c.n
+    rng = random.Random(77)
+    d = rng.randrange(1, n)
+    qx, qy = O.scalar_mult(c, d, (c.gx, c.gy))
+    u2s = [1, 7, 8, 9, 15, 16, 17, 0x88, 0x8888, 0x7777, 2**252, 2**256 - n, n - 1, n - 2,
+           n // 2, n // 2 + 1, (16**64 - 1) % n, sum(8 * 16**k for k in range(64)) % n,
+           sum(9 * 16**k for k in range(64)) % n, sum(7 * 16**k for k in range(64)) % n]
+    u2s += [rng.randrange(1, n) for _ in range(6)]
+    recs = []
+    for u2 in u2s:
+        u1 = rng.randrange(1, n)
+        R = O.point_add(c, O.scalar_mult(c, u1, (c.gx, c.gy)), O.scalar_mult(c, u2, (qx, qy)))
+        if R is None or R[0] % n == 0:
+            continue
+        r = R[0] % n
+        s = r * pow(u2, -1, n) % n
+        e = u1 * s % n
+        for dg in (e.to_bytes(32, "big"), (e ^ 1).to_bytes(32, "big")):
+            recs.append((qx, qy, O.marshal_ecdsa_signature(r, s), dg))
+    return recs
+
+
+@pytest.mark.parametrize("wide", [1, 16, 4])
+def test_hostsim_p256_crafted_u2_both_recodings(hs, wide):
+    """q_keycomb (carry-scan digits in [-7, 8]) and the wide path's
+    keycomb_q_part (offset digits in [-8, 7]) on scalars at every recoding
+    edge, key tables forced (min_uses = 1), no low-S rule: the signatures are
+    valid by construction and their flipped-digest twins are not."""
+    recs = _p256_crafted_u2_records()
+    pub = np.frombuffer(b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big")
+                                 for x, y, _, _ in recs), np.uint8)
+    sigs, dgs = [t[2] for t in recs], [t[3] for t in recs]
+    sl = np.array([len(x) for x in sigs], np.uint32)
+    dl = np.array([len(x) for x in dgs], np.uint32)
+    so = np.concatenate([[0], np.cumsum(sl[:-1])]).astype(np.uint64)
+    do = np.concatenate([[0], np.cumsum(dl[:-1])]).astype(np.uint64)
+    sig = np.frombuffer(b"".join(sigs), np.uint8)
+    dg = np.frombuffer(b"".join(dgs), np.uint8)
+    out = np.zeros(len(recs), np.uint8)
+    ncomb = ctypes.c_uint32()
+    hs.hs_set_wide(wide)
+    try:
+        hs.hs_verify2(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
+                      dg.ctypes.data, do.ctypes.data, dl.ctypes.data, len(recs), 2, 4, 1,
+                      out.ctypes.data, ctypes.byref(ncomb))
+    finally:
+        hs.hs_set_wide(1)
+    assert ncomb.value > 0
+    # every first record verifies, every flipped twin fails (R_MATH)
+    assert [int(o) for o in out[0::2]] == [0] * (len(recs) // 2)
+    assert all(int(o) == 9 for o in out[1::2])
