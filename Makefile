@@ -9,7 +9,7 @@ LIB  := bdls_amd/lib
 
 HDRS := $(wildcard $(CSRC)/*.h) include/bdls_hip.h
 
-all: $(LIB)/libbdlship.so $(LIB)/libbdlsgen.so oracle tests/native/build/libhostsim.so
+all: $(LIB)/libbdlship.so $(LIB)/libbdlsgen.so oracle tests/native/build/libhostsim.so $(LIB)/csp_load
 
 $(LIB)/verify_kernels.o: $(CSRC)/verify_kernels.hip $(HDRS)
 	@mkdir -p $(LIB)
@@ -61,3 +61,7 @@ $(LIB)/ubench: $(CSRC)/ubench.hip $(HDRS)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
 all: $(LIB)/ubench
+
+# native load generator for the coalesced single Verify (bench.py side configs)
+$(LIB)/csp_load: tools/csp_load.cpp include/bdls_hip.h $(LIB)/libbdlship.so
+	g++ -O2 -std=c++17 -Wall -o $@ $< -L$(LIB) -lbdlship -Wl,-rpath,'$$ORIGIN' -lpthread

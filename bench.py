@@ -819,62 +819,46 @@ def bench_config1(a):
     return 0
 
 
-def single_verify_measure(L, threads_list=(1, 8, 64), calls=None) -> dict:
+def single_verify_measure(L, threads_list=(1, 8, 64, 256)) -> dict:
     """The drop-in single BCCSP.Verify (bh_csp_verify_p256, the coalescer;
     bccsp/sw/impl.go:247-270 as msp/identities.go:190 calls it): per-call
-    latency p50/p99 and throughput at 1, 8 and 64 concurrent callers, with
-    keys the device has never seen (cold) and with the keys registered (the
-    MSP identity cache analog); the CPU proxy of one call beside it."""
+    latency p50 / p99 and throughput at 1 .. 256 concurrent callers, driven by
+    the native load generator (bdls_amd/lib/csp_load: pthreads, as Go's
+    validator goroutines call Verify) in a child process. cold = the device
+    has never seen the keys (the coalescer registers each key on its first
+    sighting, the MSP-identity-cache analog); registered = registered before
+    timing. The CPU proxy of one call beside it."""
     import hashlib
-    import threading
-    from bdls_amd import _lib, workload
+    import subprocess
+    import tempfile
+    from bdls_amd import workload
     from oracle import orc
     w = workload.generate(4096, 64, 256, 0, seed=11)
-    pubs = [bytes(w.pub[64 * i:64 * i + 64]) for i in range(w.n)]
-    sigs = [bytes(w.sig[int(o):int(o) + int(l)]) for o, l in zip(w.sig_off, w.sig_len)]
-    dgs = [hashlib.sha256(bytes(w.msg[int(o):int(o) + int(l)])).digest()
-           for o, l in zip(w.msg_off, w.msg_len)]
+    recs = []
+    for i in range(w.n):
+        sig = bytes(w.sig[int(w.sig_off[i]):int(w.sig_off[i]) + int(w.sig_len[i])])
+        dg = hashlib.sha256(bytes(w.msg[int(w.msg_off[i]):int(w.msg_off[i]) + int(w.msg_len[i])]))
+        recs.append(bytes(w.pub[64 * i:64 * i + 64]) + dg.digest() + bytes([len(sig)]) + sig)
+    tool = os.path.join(ROOT, "bdls_amd", "lib", "csp_load")
     out, ok = {}, True
-    for mode in ("cold", "registered"):
-        _lib.check(L.bh_keys_clear(-1, 0))
-        if mode == "registered":
-            uk = np.unique(w.pub.reshape(-1, 64), axis=0)
-            st = np.zeros(len(uk), np.uint8)
-            _lib.check(L.bh_keys_register(-1, 0, np.ascontiguousarray(uk).ctypes.data, len(uk),
-                                          st.ctypes.data))
-        for nth in threads_list:
-            per = calls or max(8, min(200, 2048 // nth))
-            lat = [[] for _ in range(nth)]
-            bad = [0]
-
-            def worker(t):
-                v, r = ctypes.c_int(), ctypes.c_int()
-                for k in range(per):
-                    i = (t * per + k) % w.n
-                    t0 = time.perf_counter()
-                    rc = L.bh_csp_verify_p256(pubs[i], sigs[i], len(sigs[i]), dgs[i], 32,
-                                              ctypes.byref(v), ctypes.byref(r))
-                    lat[t].append((time.perf_counter() - t0) * 1e6)
-                    if rc or v.value != 1 or r.value != 0:
-                        bad[0] += 1
-            st0 = np.zeros(3, np.uint64)
-            _lib.check(L.bh_csp_stats(st0.ctypes.data))
-            ths = [threading.Thread(target=worker, args=(t,)) for t in range(nth)]
-            t0 = time.perf_counter()
-            for th in ths:
-                th.start()
-            for th in ths:
-                th.join()
-            el = time.perf_counter() - t0
-            st1 = np.zeros(3, np.uint64)
-            _lib.check(L.bh_csp_stats(st1.ctypes.data))
-            allv = [x for l in lat for x in l]
-            out[f"{mode}_{nth}thr"] = {
-                "p50_us": round(percentile(allv, 50), 1), "p99_us": round(percentile(allv, 99), 1),
-                "verifies_per_s": round(nth * per / el, 1),
-                "device_batches": int(st1[1] - st0[1]), "calls": nth * per}
-            ok = ok and bad[0] == 0
-    _lib.check(L.bh_keys_clear(-1, 0))
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(b"".join(recs))
+        path = f.name
+    try:
+        for mode in ("cold", "registered"):
+            for nth in threads_list:
+                per = max(16, min(400, 8192 // nth))
+                r = subprocess.run([tool, path, str(nth), str(per), "1" if mode == "registered" else "0"],
+                                   capture_output=True, text=True, timeout=120)
+                if r.returncode not in (0, 1) or not r.stdout.strip():
+                    out[f"{mode}_{nth}thr"] = {"error": r.stderr[-300:]}
+                    ok = False
+                    continue
+                res = json.loads(r.stdout.strip().splitlines()[-1])
+                ok = ok and res["bad"] == 0
+                out[f"{mode}_{nth}thr"] = res
+    finally:
+        os.unlink(path)
     m = 512
     rates = {}
     for nth in (1, 16):

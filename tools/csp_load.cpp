@@ -1,0 +1,116 @@
+// Native load generator for the drop-in single-signature Verify
+// (bh_csp_verify_p256, the coalescer): T threads each make M blocking calls,
+// as Fabric's validator goroutines call bccsp.Verify (core/peer/config.go:
+// 269-272, v20/validator.go:193-208). Records come from a file written by
+// bench.py (n records: 64 B key, 32 B digest, 1 B sig length, sig bytes);
+// every call's result is checked (all records are valid). Prints one JSON
+// object: per-call latency p50 / p99 (us), calls per second, device batches.
+//
+//   csp_load <records.bin> <threads> <calls_per_thread> [register]
+//
+// register = 1: the records' keys are registered before timing.
+#include <pthread.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../include/bdls_hip.h"
+
+struct Rec {
+  uint8_t pub[64], dg[32], sig[80];
+  uint32_t sig_len;
+};
+
+static std::vector<Rec> g_recs;
+static int g_calls = 0;
+static std::atomic<int> g_bad{0};
+static std::atomic<int> g_ready{0};
+static std::atomic<bool> g_go{false};
+
+struct Arg {
+  int t;
+  std::vector<double> lat;
+};
+
+static void* worker(void* p) {
+  Arg* a = (Arg*)p;
+  a->lat.reserve(g_calls);
+  g_ready++;
+  while (!g_go.load()) {
+  }
+  for (int k = 0; k < g_calls; k++) {
+    const Rec& r = g_recs[(size_t)(a->t * 7919 + k) % g_recs.size()];
+    int valid = 0, reason = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = bh_csp_verify_p256(r.pub, r.sig, r.sig_len, r.dg, 32, &valid, &reason);
+    const auto t1 = std::chrono::steady_clock::now();
+    a->lat.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+    if (rc || !valid || reason) g_bad++;
+  }
+  return nullptr;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 4) {
+    fprintf(stderr, "usage: %s records.bin threads calls [register]\n", argv[0]);
+    return 2;
+  }
+  FILE* f = fopen(argv[1], "rb");
+  if (!f) return 2;
+  for (;;) {
+    Rec r{};
+    uint8_t sl;
+    if (fread(r.pub, 1, 64, f) != 64 || fread(r.dg, 1, 32, f) != 32 || fread(&sl, 1, 1, f) != 1)
+      break;
+    if (sl > sizeof(r.sig) || fread(r.sig, 1, sl, f) != sl) return 2;
+    r.sig_len = sl;
+    g_recs.push_back(r);
+  }
+  fclose(f);
+  const int T = atoi(argv[2]);
+  g_calls = atoi(argv[3]);
+  const bool reg = argc > 4 && atoi(argv[4]) != 0;
+  if (g_recs.empty() || T < 1 || g_calls < 1) return 2;
+  if (bh_init(1, 0) != BH_OK) {
+    fprintf(stderr, "bh_init: %s\n", bh_last_error());
+    return 3;
+  }
+  bh_keys_clear(-1, BH_CURVE_P256);
+  if (reg) {
+    std::vector<uint8_t> pub;
+    for (const Rec& r : g_recs) pub.insert(pub.end(), r.pub, r.pub + 64);
+    if (bh_keys_register(-1, BH_CURVE_P256, pub.data(), g_recs.size(), nullptr) != BH_OK) return 3;
+  }
+  uint64_t st0[3], st1[3];
+  bh_csp_stats(st0);
+  std::vector<Arg> args(T);
+  std::vector<pthread_t> th(T);
+  for (int t = 0; t < T; t++) {
+    args[t].t = t;
+    pthread_create(&th[t], nullptr, worker, &args[t]);
+  }
+  while (g_ready.load() < T) {
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  g_go = true;
+  for (int t = 0; t < T; t++) pthread_join(th[t], nullptr);
+  const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  bh_csp_stats(st1);
+  std::vector<double> all;
+  for (auto& a : args) all.insert(all.end(), a.lat.begin(), a.lat.end());
+  std::sort(all.begin(), all.end());
+  auto pct = [&](double q) { return all[std::min(all.size() - 1, (size_t)(q * all.size()))]; };
+  printf("{\"threads\": %d, \"calls\": %zu, \"p50_us\": %.1f, \"p99_us\": %.1f, "
+         "\"verifies_per_s\": %.1f, \"device_batches\": %llu, \"max_batch\": %llu, "
+         "\"registered_before\": %s, \"bad\": %d}\n",
+         T, all.size(), pct(0.5), pct(0.99), all.size() / el,
+         (unsigned long long)(st1[1] - st0[1]), (unsigned long long)st1[2], reg ? "true" : "false",
+         g_bad.load());
+  bh_shutdown();
+  return g_bad.load() ? 1 : 0;
+}
