@@ -31,7 +31,7 @@ EXPORTS = (
     "bh_verify_submit", "bh_verify_wait", "bh_host_alloc", "bh_host_free", "bh_csp_stats",
     "bh_fabric_block_preverify", "bh_verify_x509", "bh_signature_sets_verify",
     "bh_envelopes_preverify", "bh_block_signatures_preverify",
-    "bh_block_signatures_preverify_bft",
+    "bh_block_signatures_preverify_bft", "bh_fabric_block_preverify_refs",
 )
 KEY_FULL = 255  # bh_keys_register status: registry full
 
@@ -77,6 +77,15 @@ class BhFabTx(ctypes.Structure):
     _fields_ = [("status", ctypes.c_int32), ("type", ctypes.c_int32),
                 ("creator", ctypes.c_uint32), ("endorse_first", ctypes.c_uint32),
                 ("endorse_count", ctypes.c_uint32), ("valid_endorsers", ctypes.c_uint32)]
+
+
+class BhFabSigref(ctypes.Structure):
+    """include/bdls_hip.h bh_fab_sigref."""
+    _fields_ = [("ident_off", ctypes.c_uint64), ("sig_off", ctypes.c_uint64),
+                ("msg_off", ctypes.c_uint64), ("msg2_off", ctypes.c_uint64),
+                ("ident_len", ctypes.c_uint32), ("sig_len", ctypes.c_uint32),
+                ("msg_len", ctypes.c_uint32), ("msg2_len", ctypes.c_uint32),
+                ("reason", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class BhSdBatch(ctypes.Structure):
@@ -150,6 +159,10 @@ def lib() -> ctypes.CDLL:
         L.bh_fabric_block_preverify.argtypes = [vp, sz, u32, vp, sz, ctypes.POINTER(sz), vp, sz,
                                                 ctypes.POINTER(sz)]
         L.bh_fabric_block_preverify.restype = i32
+        L.bh_fabric_block_preverify_refs.argtypes = [vp, sz, u32, vp, sz, ctypes.POINTER(sz), vp,
+                                                     sz, ctypes.POINTER(sz), vp, sz,
+                                                     ctypes.POINTER(sz)]
+        L.bh_fabric_block_preverify_refs.restype = i32
         L.bh_signature_sets_verify.argtypes = [ctypes.POINTER(BhSdBatch), sz, vp, sz, u32, vp, vp]
         L.bh_signature_sets_verify.restype = i32
         L.bh_envelopes_preverify.argtypes = [vp, vp, vp, sz, u32, vp, vp]

@@ -27,6 +27,7 @@
 
 #include "../../include/bdls_hip.h"
 #include "verify.h"
+#include "shard.h"
 
 namespace bh {
 hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s);
@@ -653,7 +654,7 @@ int finish_part(bh_job* j, size_t k) {
   }
   const uint64_t* words = (const uint64_t*)sl.host_out.p;
   const uint8_t* rs = (const uint8_t*)(words + round64(p.m) / 64);
-  std::memcpy(j->bitmap + p.lo / 8, words, (p.m + 7) / 8);  // lo is a multiple of 64
+  bh::shard_bitmap_merge(j->bitmap, bh::Shard{p.lo, p.m}, words);  // lo: a multiple of 64
   std::memcpy(j->reason + p.lo, rs, p.m);
   return BH_OK;
 }
@@ -832,16 +833,15 @@ int submit_job(int curve, const B* b, size_t n, uint32_t flags, uint8_t* bitmap,
     *out = j;
     return BH_OK;
   }
-  const size_t nd = std::min(devs.size(), (n + 63) / 64);
-  const size_t per = nd ? round64((n + nd - 1) / nd) : 0;
+  const size_t nd = bh::shard_devices(n, devs.size());
   for (size_t k = 0; k < nd; k++) {
-    const size_t lo = k * per, hi = std::min(n, lo + per);
-    if (lo >= hi) break;
+    const bh::Shard sh = bh::shard_of(n, nd, k);
+    if (!sh.len) break;
     Dev& d = *devs[k];
     int rc;
     {
       std::lock_guard<std::mutex> g(d.mu);
-      rc = enqueue_part(j, d, curve, b, lo, hi - lo, flags);
+      rc = enqueue_part(j, d, curve, b, sh.lo, sh.len, flags);
     }
     if (rc) {
       const std::string err = g_err;

@@ -567,8 +567,21 @@ bool parse_cert(const uint8_t* d, size_t n, Cert* c) {
 // SerializedIdentity bytes -> resolved P-256 key + the identity key used by
 // SignatureSetToValidIdentities' de-duplication (Mspid + Id, where Id hashes
 // the SANITIZED certificate: newIdentity, msp/identities.go:55-85 ->
-// sanitizeCert -> sanitizeECDSASignedCert, msp/cert.go:76-116, which rewrites
-// an ECDSA certificate signature to low-S). Here: mspid || tbs || r || low-S s.
+// sanitizeCert, msp/mspimpl.go:892-935 -> sanitizeECDSASignedCert,
+// msp/cert.go:76-116, which rewrites the certificate signature's S to low-S
+// with the ISSUER's curve order). Here: mspid || tbs || r. For a given TBS and
+// r, the only signatures Go's chain validation can accept are (r, s) and its
+// twin (r, n_issuer - s), which sanitize to the same certificate, so dropping
+// s gives Go's equivalence without knowing the issuer's curve (a P-384 CA's
+// twins included). A signature that does not parse keeps its raw bytes.
+//
+// What this cannot see: Go's DeserializeIdentity also builds the certificate
+// chain to the MSP's roots (getUniqueValidationChain) and rejects identities
+// that do not chain, are revoked, or fail the OU rules. Those identities are
+// resolved here, so valid_endorsers / valid_identities are UPPER BOUNDS of
+// what Go's policy evaluation receives: informational counts that must not
+// decide a policy on their own (the unchanged Go evaluation consults the
+// per-signature results).
 struct Ident {
   bool ok = false;
   uint8_t pub[64];
@@ -576,38 +589,36 @@ struct Ident {
   uint64_t key_id = 0;  // interned key (IdentCache): equal keys <=> equal ids
 };
 
-constexpr uint32_t kP256HalfN[8] = {0x7e3192a8, 0x79dce561, 0xd38bcf42, 0xde737d56,
-                                    0xffffffff, 0x7fffffff, 0x80000000, 0x7fffffff};
-constexpr uint32_t kP256N[8] = {0xfc632551, 0xf3b9cac2, 0xa7179e84, 0xbce6faad,
-                                0xffffffff, 0xffffffff, 0x00000000, 0xffffffff};
+// r's magnitude (big-endian, no leading zeros, any size) of a signature that
+// Go's asn1 parses with r, s > 0; false otherwise.
+bool sig_r_bytes(const uint8_t* b, size_t n, std::string* out) {
+  bh::DerSig ds;
+  if (n > 0xffffffffu || bh::der_parse_sig(b, (uint32_t)n, &ds) != bh::R_OK) return false;
+  uint32_t off = 0, cls, cmp, tag, len, io = 0, rl;
+  if (bh::der_tag_len(b, (uint32_t)n, &off, &cls, &cmp, &tag, &len)) return false;
+  const uint8_t* in = b + off;
+  if (bh::der_tag_len(in, len, &io, &cls, &cmp, &tag, &rl)) return false;
+  const uint8_t* p = in + io;
+  while (rl > 1 && *p == 0) {
+    p++;
+    rl--;
+  }
+  out->assign((const char*)p, rl);
+  return true;
+}
 
 std::string dedupe_key(const Span& mspid, const Cert& c) {
   std::string k((const char*)mspid.p, mspid.n);
   k.push_back('\0');
   k.append((const char*)c.tbs.raw, c.tbs.raw_n);
-  bh::DerSig ds;
-  memset(&ds, 0, sizeof(ds));
-  if (c.has_sig && bh::der_parse_sig(c.sig.p, (uint32_t)c.sig.n, &ds) == bh::R_OK && !ds.s_big &&
-      !ds.r_big) {
-    uint32_t s[8];
-    memcpy(s, ds.s, 32);
-    bool high = false;  // s > n/2 -> n - s
-    for (int i = 7; i >= 0; i--)
-      if (s[i] != kP256HalfN[i]) {
-        high = s[i] > kP256HalfN[i];
-        break;
-      }
-    if (high) {
-      uint64_t br = 0;
-      for (int i = 0; i < 8; i++) {
-        const uint64_t t = (uint64_t)kP256N[i] - s[i] - br;
-        s[i] = (uint32_t)t;
-        br = (t >> 63) & 1;
-      }
-    }
-    k.append((const char*)ds.r, 32);
-    k.append((const char*)s, 32);
+  std::string r;
+  if (c.has_sig && sig_r_bytes(c.sig.p, c.sig.n, &r)) {
+    k.push_back((char)(r.size() >> 8));
+    k.push_back((char)(r.size() & 0xff));
+    k.append(r);
   } else if (c.has_sig) {
+    k.push_back('\xff');
+    k.push_back('\xff');
     k.append((const char*)c.sig.p, c.sig.n);
   }
   return k;
@@ -1285,11 +1296,11 @@ extern "C" int bh_verify_x509(const uint8_t* certs, const uint64_t* cert_off,
   return BH_OK;
 }
 
-extern "C" int bh_fabric_block_preverify(const uint8_t* block, size_t len, uint32_t flags,
-                                         bh_fab_tx* txs, size_t tx_cap, size_t* n_tx,
-                                         uint8_t* endorse, size_t endorse_cap,
-                                         size_t* n_endorse) {
-  if (!n_tx || !n_endorse || (len && !block))
+static int block_preverify(const uint8_t* block, size_t len, uint32_t flags, bh_fab_tx* txs,
+                           size_t tx_cap, size_t* n_tx, uint8_t* endorse, size_t endorse_cap,
+                           size_t* n_endorse, bh_fab_sigref* refs, size_t ref_cap,
+                           size_t* n_ref) {
+  if (!n_tx || !n_endorse || (len && !block) || (n_ref && !refs && ref_cap))
     return bh::host_fail(BH_E_INVALID, "null argument");
   if (flags & ~(uint32_t)(BH_FAB_F_SHA3 | BH_FAB_F_KEEP_KEYS | BH_FAB_F_DECODE_ONLY))
     return bh::host_fail(BH_E_INVALID, "unknown flag");
@@ -1301,9 +1312,11 @@ extern "C" int bh_fabric_block_preverify(const uint8_t* block, size_t len, uint3
   decode_block_txs(data, &t, &ends);
   *n_tx = t.size();
   *n_endorse = ends.size();
+  if (n_ref) *n_ref = t.size() + ends.size();
   if ((t.size() && (!txs || tx_cap < t.size())) ||
-      (ends.size() && (!endorse || endorse_cap < ends.size())))
-    return bh::host_fail(BH_E_INVALID, "result buffers too small (see *n_tx, *n_endorse)");
+      (ends.size() && (!endorse || endorse_cap < ends.size())) ||
+      (n_ref && (t.size() + ends.size()) && (!refs || ref_cap < t.size() + ends.size())))
+    return bh::host_fail(BH_E_INVALID, "result buffers too small (see *n_tx, *n_endorse, *n_ref)");
   const bool decode_only = (flags & BH_FAB_F_DECODE_ONLY) != 0;
   // one device batch: every creator signature and the first round of every
   // transaction's endorsement set
@@ -1341,7 +1354,58 @@ extern "C" int bh_fabric_block_preverify(const uint8_t* block, size_t len, uint3
     txs[i].valid_endorsers = valid[i];
     for (size_t k = 0; k < x.end_count; k++) endorse[x.end_first + k] = ends[x.end_first + k].out;
   }
+  if (n_ref) {
+    auto off = [&](Span sp) -> uint64_t { return sp.n ? (uint64_t)(sp.p - block) : 0u; };
+    const size_t nt = t.size();
+    for (size_t i = 0; i < nt; i++) {
+      const TxRec& x = t[i];
+      bh_fab_sigref& r = refs[i];
+      memset(&r, 0, sizeof(r));
+      r.reason = x.creator_out;
+      if (!x.creator_ser.n) continue;  // no creator reached (decode failed earlier)
+      r.ident_off = off(x.creator_ser);
+      r.ident_len = (uint32_t)x.creator_ser.n;
+      r.sig_off = off(x.signature);
+      r.sig_len = (uint32_t)x.signature.n;
+      r.msg_off = off(x.payload);
+      r.msg_len = (uint32_t)x.payload.n;
+    }
+    for (size_t j = 0; j < ends.size(); j++) {
+      const SdEntry& e = ends[j];
+      bh_fab_sigref& r = refs[nt + j];
+      memset(&r, 0, sizeof(r));
+      r.reason = e.out;
+      r.ident_off = off(e.id_ser);
+      r.ident_len = (uint32_t)e.id_ser.n;
+      r.sig_off = off(e.sig);
+      r.sig_len = (uint32_t)e.sig.n;
+      r.msg_off = off(e.seg[0]);
+      r.msg_len = (uint32_t)e.seg[0].n;
+      if (e.nseg > 1) {
+        r.msg2_off = off(e.seg[1]);
+        r.msg2_len = (uint32_t)e.seg[1].n;
+      }
+    }
+  }
   return BH_OK;
+}
+
+extern "C" int bh_fabric_block_preverify(const uint8_t* block, size_t len, uint32_t flags,
+                                         bh_fab_tx* txs, size_t tx_cap, size_t* n_tx,
+                                         uint8_t* endorse, size_t endorse_cap,
+                                         size_t* n_endorse) {
+  return block_preverify(block, len, flags, txs, tx_cap, n_tx, endorse, endorse_cap, n_endorse,
+                         nullptr, 0, nullptr);
+}
+
+extern "C" int bh_fabric_block_preverify_refs(const uint8_t* block, size_t len, uint32_t flags,
+                                              bh_fab_tx* txs, size_t tx_cap, size_t* n_tx,
+                                              uint8_t* endorse, size_t endorse_cap,
+                                              size_t* n_endorse, bh_fab_sigref* refs,
+                                              size_t ref_cap, size_t* n_ref) {
+  if (!n_ref) return bh::host_fail(BH_E_INVALID, "null argument");
+  return block_preverify(block, len, flags, txs, tx_cap, n_tx, endorse, endorse_cap, n_endorse,
+                         refs, ref_cap, n_ref);
 }
 
 // SignatureSetToValidIdentities over many signature sets in one device batch.

@@ -11,7 +11,7 @@
 //
 // Value contract ("beta"): every element is a non-negative integer < beta * p
 // whose limbs 0..7 are < 2^30 ("normalised"; limb 8 holds the rest).
-//   f_mul(a, b)  requires beta_a * beta_b <= 16384 and normalised limbs;
+//   f_mul(a, b)  requires beta_a * beta_b <= 16000 and normalised limbs;
 //                returns beta 2 (t < ab/R + p < 2p).
 //   f_add        beta_a + beta_b
 //   f_sub<K>     a - b + K p, K in {32, 64}: requires beta_b <= K - 1;
@@ -51,8 +51,7 @@ BH_HD void f_const(uint32_t r[9], const C& c) {
 // Two phases for instruction-level parallelism: (1) the 17 product columns are
 // accumulated independently (17 parallel v_mad_u64_u32 chains of <= 9), then
 // (2) one short sequential pass folds the carries and the reduction terms
-// (critical path ~2 instructions per column). Column bound: <= 9 products
-// < 2^60 plus reduction terms < 2^60 + 2^46 + 2^42 + 2^36 and the carry, < 2^64.
+// (critical path ~2 instructions per column; column bounds in f_redc).
 // c += m * k as ONE v_mad_u64_u32. For power-of-two k hipcc otherwise emits a
 // 64-bit shift of the whole column plus two masks and an add (4 instructions),
 // so k is hidden behind an empty asm that claims to rewrite it in an SGPR:
@@ -75,21 +74,38 @@ template <class F>
 BH_HD void f_redc(uint32_t r[9], uint64_t C[17]) {
   uint64_t acc = 0;
   if constexpr (F::sparse_p256) {
-    // p = 2^256 - 2^224 + 2^192 + 2^96 - 1 and -p^-1 = 1 mod 2^30, so m_k is the
-    // low limb of the running column and m_k p, limb-aligned at column k, is
-    //   -m_k               (col k: cancels the low limb exactly -> just shift)
+    // p = 2^256 - 2^224 + 2^192 + 2^96 - 1 and -p^-1 = 1 mod 2^30, so any m_k
+    // congruent to the running column mod 2^30 works, and m_k p, limb-aligned
+    // at column k, is
+    //   -m_k               (col k)
     //   + m_k 2^96  = m_k << 6   at col k+3
     //   + m_k 2^192 = m_k << 12  at col k+6
     //   + m_k (2^256 - 2^224) = m_k p[7] at col k+7 + m_k p[8] at col k+8
+    // Columns 0..7 take m_k = the column's whole LOW WORD (< 2^32): -m_k then
+    // clears 32 bits, and the carry into column k+1 is 4 x the high word, one
+    // v_mad_u64_u32 instead of a 64-bit shift, a mask and a 64-bit add. Column
+    // bound: m_k p[7] < 2^62, so <= 9 products + 2^62 + 2^48 + 2^44 + 2^38 + the
+    // carry 2^34 < 13.01 x 2^60. Column 8 takes the masked 30-bit m_8, so
+    // M = sum m_k 2^(30k) < 2^270 + 2^242 and t < ab/R + (1 + 2^-28) p, which is
+    // < 2p for beta_a beta_b <= 16000 (the formulas stay <= 9604).
 #pragma unroll
-    for (int k = 0; k < 17; k++) {
+    for (int k = 0; k < 8; k++) {
+      const uint32_t m = (uint32_t)C[k];
+      mac_k<64u>(C[k + 3], m);
+      mac_k<4096u>(C[k + 6], m);
+      mac_k<F::p[7]>(C[k + 7], m);
+      mac_k<F::p[8]>(C[k + 8], m);
+      mac_k<4u>(C[k + 1], (uint32_t)(C[k] >> 32));
+    }
+#pragma unroll
+    for (int k = 8; k < 17; k++) {
       acc += C[k];
       const uint32_t m = (uint32_t)acc & kM30;
-      if (k < 9) {
-        mac_k<64u>(C[k + 3], m);
-        mac_k<4096u>(C[k + 6], m);
-        mac_k<F::p[7]>(C[k + 7], m);
-        mac_k<F::p[8]>(C[k + 8], m);
+      if (k == 8) {
+        mac_k<64u>(C[11], m);
+        mac_k<4096u>(C[14], m);
+        mac_k<F::p[7]>(C[15], m);
+        mac_k<F::p[8]>(C[16], m);
       } else {
         r[k - 9] = m;
       }

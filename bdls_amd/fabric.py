@@ -63,6 +63,60 @@ def block_preverify(block: bytes, sha3: bool = False, keep_keys: bool = False,
     return out
 
 
+@dataclass
+class SigRef:
+    """One signature of a block and its verified outcome: the key of the
+    caller's verified-signature cache."""
+    identity: bytes
+    data: bytes       # the signed bytes (msg || msg2)
+    signature: bytes
+    reason: int       # BH_R_*, E_DUPLICATE, E_BAD_IDENTITY, NOT_VERIFIED
+
+
+def block_preverify_refs(block: bytes, sha3: bool = False, keep_keys: bool = False,
+                         decode_only: bool = False):
+    """block_preverify plus, per signature, its (identity, signed bytes,
+    signature) inside the block (bh_fabric_block_preverify_refs): the creator
+    signatures (one per transaction, None when the transaction has no creator
+    to check) and the endorsements, in endorse[] order."""
+    L = _lib.lib()
+    if not decode_only:
+        _lib.ensure_init()
+    flags = _flags(sha3, keep_keys, decode_only)
+    buf = np.frombuffer(bytes(block) + b"\0", np.uint8)
+    ntx, nend, nref = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    rc = L.bh_fabric_block_preverify_refs(buf.ctypes.data, len(block),
+                                          flags | _lib.BH_FAB_F_DECODE_ONLY, None, 0,
+                                          ctypes.byref(ntx), None, 0, ctypes.byref(nend), None, 0,
+                                          ctypes.byref(nref))
+    if rc != 0 and nref.value == 0:
+        _lib.check(rc)
+    txs = (_lib.BhFabTx * max(1, ntx.value))()
+    end = np.zeros(max(1, nend.value), np.uint8)
+    refs = (_lib.BhFabSigref * max(1, nref.value))()
+    _lib.check(L.bh_fabric_block_preverify_refs(
+        buf.ctypes.data, len(block), flags, txs, ntx.value, ctypes.byref(ntx), end.ctypes.data,
+        nend.value, ctypes.byref(nend), refs, nref.value, ctypes.byref(nref)))
+    assert nref.value == ntx.value + nend.value
+    out = []
+    for i in range(ntx.value):
+        t = txs[i]
+        out.append(TxResult(t.status, t.type, t.creator,
+                            [int(x) for x in end[t.endorse_first:t.endorse_first + t.endorse_count]],
+                            t.valid_endorsers))
+
+    def ref(r):
+        if r.ident_len == 0:
+            return None
+        sp = lambda off, n: bytes(block[off:off + n])  # noqa: E731
+        return SigRef(sp(r.ident_off, r.ident_len),
+                      sp(r.msg_off, r.msg_len) + sp(r.msg2_off, r.msg2_len),
+                      sp(r.sig_off, r.sig_len), int(r.reason))
+    creators = [ref(refs[i]) for i in range(ntx.value)]
+    endorsements = [ref(refs[ntx.value + j]) for j in range(nend.value)]
+    return out, creators, endorsements
+
+
 def _concat(items):
     ln = np.array([len(x) for x in items], np.uint32)
     off = np.zeros(len(items), np.uint64)

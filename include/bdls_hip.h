@@ -341,6 +341,29 @@ int bh_fabric_block_preverify(const uint8_t *block, size_t len, uint32_t flags, 
                               size_t tx_cap, size_t *n_tx, uint8_t *endorse, size_t endorse_cap,
                               size_t *n_endorse);
 
+/* bh_fabric_block_preverify plus, per signature, where its inputs lie in the
+ * block: the keys of the caller's verified-signature cache (INTEGRATION.md
+ * sections 4-5), consulted by the unchanged checkSignatureFromCreator
+ * (msgvalidation.go:26-64) and SignatureSetToValidIdentities (policy.go:
+ * 363-395) with exactly (identity, signed bytes, signature). refs[i] (i <
+ * *n_tx) is transaction i's creator signature (identity = SignatureHeader.
+ * creator, signed bytes = Envelope.payload, signature = Envelope.signature;
+ * ident_len 0 when the transaction has no creator to check); refs[*n_tx + j]
+ * is endorsement j (identity = endorser, signed bytes = proposal_response_
+ * payload || endorser, the SignedData of validator_keylevel.go:246-260).
+ * Offsets are byte offsets into `block`; reason repeats txs[i].creator /
+ * endorse[j]. *n_ref = *n_tx + *n_endorse; ref_cap must cover it. */
+typedef struct bh_fab_sigref {
+  uint64_t ident_off, sig_off, msg_off, msg2_off;
+  uint32_t ident_len, sig_len, msg_len, msg2_len; /* signed bytes: msg || msg2 */
+  uint32_t reason;                                /* BH_R_*, BH_FAB_E_*, BH_SP_NOT_VERIFIED */
+  uint32_t reserved;
+} bh_fab_sigref;
+int bh_fabric_block_preverify_refs(const uint8_t *block, size_t len, uint32_t flags,
+                                   bh_fab_tx *txs, size_t tx_cap, size_t *n_tx, uint8_t *endorse,
+                                   size_t endorse_cap, size_t *n_endorse, bh_fab_sigref *refs,
+                                   size_t ref_cap, size_t *n_ref);
+
 /* ---- signature sets: SignatureSetToValidIdentities as a batch ------------------
  * common/policies/policy.go:363-395, the batch point of every policy
  * evaluation (cauthdsl, implicit-meta sub-policies, the endorsement policy,

@@ -342,7 +342,7 @@ class Ident:
     key: bytes  # Mspid + Id (sanitized certificate) for the de-duplication
 
 
-def deserialize(ser: bytes, half_n: int, n: int):
+def deserialize(ser: bytes):
     """msp DeserializeIdentity, as far as the key and the identifier."""
     from . import ecdsa_ref as O
     try:
@@ -358,14 +358,19 @@ def deserialize(ser: bytes, half_n: int, n: int):
     if ck is None:
         return None
     x, y, tbs_raw, sig = ck
+    # Id = hash of the certificate sanitized to low-S with the ISSUER's order
+    # (msp/mspimpl.go:892-935, msp/cert.go:76-116): for one TBS and r the
+    # chain-valid signatures are s and n_issuer - s, both sanitized alike, so
+    # the key drops s (fabric.cpp dedupe_key). Go's chain building to the MSP
+    # roots is not restated: identities that would not chain still resolve here
+    # (the counts are upper bounds, as in the engine).
     key = (si["mspid"] or b"") + b"\0" + tbs_raw
     rc, r, s = O.unmarshal_ecdsa_signature(sig)
-    if rc == O.R_OK and r < 2**256 and s < 2**256:
-        if s > half_n:  # sanitizeECDSASignedCert: low-S
-            s = n - s
-        key += r.to_bytes(32, "little") + s.to_bytes(32, "little")
+    if rc == O.R_OK:
+        rb = r.to_bytes(max(1, (r.bit_length() + 7) // 8), "big")
+        key += len(rb).to_bytes(2, "big") + rb
     else:
-        key += sig
+        key += b"\xff\xff" + sig
     return Ident(x, y, key)
 
 
@@ -382,8 +387,6 @@ class TxOut:
 def validate_block(block: bytes, verify, decode_only: bool = False) -> list[TxOut]:
     """verify(x, y, msg, sig) -> BH_R_* reason of identity.Verify(msg, sig)
     (hash then bccsp Verify; 0 = valid)."""
-    from . import ecdsa_ref as O
-    n, half = O.P256.n, O.P256.n >> 1
     blk = unmarshal(block, BLOCK_SPEC)
     data = (blk["data"] or {"data": []})["data"]
     out = []
@@ -421,7 +424,7 @@ def validate_block(block: bytes, verify, decode_only: bool = False) -> list[TxOu
         if env["signature"] is None or env["payload"] is None:
             t.status = CREATOR_SIGNATURE
         else:
-            cid = deserialize(sh["creator"], half, n)
+            cid = deserialize(sh["creator"])
             if cid is None:
                 t.status = CREATOR_IDENTITY
             elif not decode_only:
@@ -461,7 +464,7 @@ def validate_block(block: bytes, verify, decode_only: bool = False) -> list[TxOu
         id_map = set()
         for e in cap["action"]["endorsements"]:
             endorser = e["endorser"] or b""
-            ident = deserialize(endorser, half, n)
+            ident = deserialize(endorser)
             if ident is None:
                 t.endorse.append(E_BAD_IDENTITY)
                 continue
@@ -484,11 +487,9 @@ def signature_set_to_valid_identities(entries, verify, decode_only: bool = False
     """common/policies/policy.go:363-395 over one set of (identity, data, sig):
     per entry BH_R_* / E_DUP / E_BAD_IDENTITY / NOT_VERIFIED, and the number
     of valid (de-duplicated) identities."""
-    from . import ecdsa_ref as O
-    n, half = O.P256.n, O.P256.n >> 1
     id_map, out = set(), []
     for ident_bytes, data, sig in entries:
-        ident = deserialize(ident_bytes, half, n)
+        ident = deserialize(ident_bytes)
         if ident is None:
             out.append(E_BAD_IDENTITY)
             continue

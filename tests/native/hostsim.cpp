@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../bdls_amd/csrc/verify.h"
+#include "../../bdls_amd/csrc/shard.h"
 
 using namespace bh;
 
@@ -235,4 +236,36 @@ extern "C" void hs_sha256(const uint8_t* msg, uint32_t len, uint32_t* out) {
 }
 extern "C" void hs_sha3_256(const uint8_t* msg, uint32_t len, uint8_t* out) {
   sha3_256_msg(out, msg, len);
+}
+
+// bh_verify's multi-device split (bdls_amd/csrc/shard.h, used by bdls_hip.cpp
+// submit_job / finish_part) for n records over ndev devices: returns 0 when
+// the shards are contiguous, 64-aligned, non-empty, cover [0, n) and their
+// bitmaps merge into exactly the single-device bitmap of `valid` (n bytes,
+// 0/1); otherwise a code naming the first broken property.
+extern "C" int hs_shard_check(size_t n, size_t ndev, const uint8_t* valid, size_t* nshards) {
+  const size_t nd = bh::shard_devices(n, ndev);
+  std::vector<uint8_t> want((n + 7) / 8 + 1, 0), got((n + 7) / 8 + 1, 0);
+  for (size_t i = 0; i < n; i++)
+    if (valid[i]) want[i >> 3] |= (uint8_t)(1u << (i & 7));
+  size_t next = 0, used = 0;
+  for (size_t k = 0; k < nd; k++) {
+    const bh::Shard s = bh::shard_of(n, nd, k);
+    if (!s.len) break;
+    if (s.lo != next) return 1;           // not contiguous
+    if (s.lo % 64) return 2;              // bitmap offset not byte / word aligned
+    if (k + 1 < nd && bh::shard_of(n, nd, k + 1).len && s.len % 64) return 3;  // ragged before the end
+    // the device's result words for this shard: bit i = record lo + i
+    std::vector<uint64_t> words((s.len + 63) / 64, 0);
+    for (size_t i = 0; i < s.len; i++)
+      if (valid[s.lo + i]) words[i >> 6] |= 1ull << (i & 63);
+    bh::shard_bitmap_merge(got.data(), s, words.data());
+    next = s.lo + s.len;
+    used++;
+  }
+  if (next != n) return 4;                // records left out
+  if (n && used != nd) return 5;          // a device got no work
+  if (memcmp(want.data(), got.data(), want.size())) return 6;  // merged bitmap differs
+  *nshards = used;
+  return 0;
 }

@@ -344,3 +344,114 @@ def test_gpu_sets_many_failed_duplicates():
     want = [R.signature_set_to_valid_identities(s, _orc_verify) for s in cases]
     assert want[0][0][300] == 0 and want[0][0][301] == 253
     assert fabric.signature_sets_verify(cases) == want
+
+
+P384_N = int("ffffffffffffffffffffffffffffffffffffffffffffffffc7634d81f4372ddf"
+             "581a0db248b0a77aecec196accc52973", 16)
+
+
+def _twin_identity(ser: bytes, order: int) -> bytes:
+    """The same certificate with its signature's S replaced by order - S (the
+    high-S / low-S twin that sanitizeECDSASignedCert maps back, msp/cert.go:
+    76-116, when `order` is the issuer's curve order)."""
+    si = R.unmarshal(ser, R.SERIALIZED_IDENTITY_SPEC)
+    der = R.pem_decode(si["id_bytes"])
+    _x, _y, tbs, sig = R.cert_p256_key(der)
+    rc, r, s = O.unmarshal_ecdsa_signature(sig)
+    assert rc == O.R_OK
+    twin_sig = F.der(0x30, F.der_int(r) + F.der_int(order - s))
+    return F.serialized_identity(si["mspid"].decode(), F.pem(F.x509_cert(tbs, twin_sig)))
+
+
+def test_twin_certificates_share_the_identity_key():
+    """Go's identity Id hashes the certificate sanitized to low-S with
+    the ISSUER's order, so a certificate and its S-twin are one identity even
+    for a P-384 CA; the de-duplication key must not depend on P-256's order."""
+    sets = _sets_case()
+    ser = sets[1][0][0]
+    base = R.deserialize(ser)
+    for order in (O.P256.n, P384_N):
+        twin = R.deserialize(_twin_identity(ser, order))
+        assert twin is not None and twin.key == base.key
+        assert (twin.x, twin.y) == (base.x, base.y)
+
+
+@pytest.mark.gpu
+def test_gpu_twin_certificates_deduplicated():
+    sets = _sets_case()
+    sds = [sd for s in sets for sd in s]
+    good = next(sd for sd in sds if R.signature_set_to_valid_identities([sd], _orc_verify)[1] == 1)
+    cases = []
+    for order in (O.P256.n, P384_N):
+        twin = (_twin_identity(good[0], order), good[1], good[2])
+        cases += [[good, twin], [twin, good], [(good[0], good[1] + b"x", good[2]), twin]]
+    want = [R.signature_set_to_valid_identities(s, _orc_verify) for s in cases]
+    assert [w[1] for w in want] == [1, 1, 1] * 2
+    assert want[0][0] == [0, 253]
+    assert fabric.signature_sets_verify(cases) == want
+
+
+def _recorded_calls(block):
+    """Every (x, y, msg, sig) the sequential validator flow verifies."""
+    calls = []
+
+    def rec(x, y, msg, sig):
+        calls.append((x, y, bytes(msg), bytes(sig)))
+        return _orc_verify(x, y, msg, sig)
+    out = R.validate_block(block, rec)
+    return out, calls
+
+
+def _ref_key(ref):
+    ident = R.deserialize(ref.identity)
+    return None if ident is None else (ident.x, ident.y, ref.data, ref.signature)
+
+
+def test_block_refs_cover_every_go_verify(classes_block):
+    """bh_fabric_block_preverify_refs (decode only): every signature check the
+    sequential flow makes (checkSignatureFromCreator, SignatureSetToValid-
+    Identities) has a reference with the same identity key, signed bytes and
+    signature -- the keys of the verified-signature cache."""
+    block = classes_block.block
+    txs, creators, ends = fabric.block_preverify_refs(block, decode_only=True)
+    assert [_got(t) for t in txs] == [_got(t) for t in fabric.block_preverify(block, decode_only=True)]
+    assert len(ends) == sum(len(t.endorse) for t in txs)
+    keys = {_ref_key(r) for r in creators + ends if r is not None}
+    _, calls = _recorded_calls(block)
+    assert calls and set(calls) <= keys
+    assert all(r is None or r.reason in (fabric.NOT_VERIFIED, fabric.E_BAD_IDENTITY, fabric.E_DUPLICATE)
+               for r in creators + ends)
+
+
+@pytest.mark.gpu
+def test_gpu_block_refs_two_phase(classes_block):
+    """Phase 1: the device batch with references; phase 2: the sequential flow
+    consulting a cache of the cacheable outcomes (BH_R_OK -> valid, BH_R_BAD_KEY
+    / R_RANGE / MATH -> invalid), falling back to a CPU verify on a miss. The
+    results equal the plain flow, and only non-cacheable records miss."""
+    block = classes_block.block
+    txs, creators, ends = fabric.block_preverify_refs(block)
+    plain = fabric.block_preverify(block)
+    assert [_got(t) for t in txs] == [_got(t) for t in plain]
+    assert [r.reason if r else None for r in ends] == [e for t in plain for e in t.endorse]
+    for t, c in zip(plain, creators):
+        if c is not None:
+            assert c.reason == t.creator
+    cache = {}
+    for r in creators + ends:
+        if r is not None and r.reason in (0, 7, 8, 9):
+            cache[_ref_key(r)] = r.reason
+    misses = []
+
+    def phase2(x, y, msg, sig):
+        k = (x, y, bytes(msg), bytes(sig))
+        if k in cache:
+            return cache[k]
+        misses.append(k)
+        return _orc_verify(x, y, msg, sig)
+    want, calls = _recorded_calls(block)
+    got = R.validate_block(block, phase2)
+    assert [_got(o) for o in got] == [_got(o) for o in want]
+    assert len(cache) > 0 and len(misses) < len(calls)
+    for k in misses:  # a miss is a record whose Go error text depends on the parse
+        assert _orc_verify(*k) in (1, 2, 3, 4, 5, 6)

@@ -179,3 +179,28 @@ def test_submit_wait_pipeline(L):
     b = _lib.BhBatch(*([0] * 7))
     _lib.check(L.bh_verify_submit(0, ctypes.byref(b), 0, 0, None, None, ctypes.byref(job)))
     _lib.check(L.bh_verify_wait(job))
+
+
+def test_unique_keys_forced_passes(L, small_chunks):
+    """Config 5's shape (every key used once: the variable-base ladder, no key
+    tables) through the pass loop: 300,000 unique keys in 131,072-record passes
+    (two full passes and a ragged one), host and device APIs."""
+    n = 300_000
+    w = workload.generate(n, n, 64, 16, seed=44)
+    valid, reason = host_verify(L, w)
+    assert (reason == w.reason).all() and (valid == w.expected_valid).all()
+    bits, dreason, tm = dev_verify(L, w)
+    assert (dreason == w.reason).all() and (bits == w.expected_valid).all()
+    assert tm.n_keytables == 0 and tm.n_keycomb == 0
+    orc_sample(w, 200, seed=2)
+
+
+def test_unique_keys_one_pass_of_1m(L):
+    """One 1,048,576-record pass of unique keys: the ladder's per-lane Q-table
+    scratch at pass size (1,792 B per record), as each config-5 rank runs it."""
+    n = 1 << 20
+    w = workload.generate(n, n, 64, 16, seed=45)
+    bits, reason, tm = dev_verify(L, w)
+    assert (reason == w.reason).all() and (bits == w.expected_valid).all()
+    assert tm.n_ladder == int((w.reason == 0).sum()) + int((w.reason == 9).sum())
+    orc_sample(w, 200, seed=3)
