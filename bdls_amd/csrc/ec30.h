@@ -34,11 +34,8 @@ BH_HD void j_sel(J30& r, bool c, const J30& a, const J30& b) {
 }
 
 // Requires beta(X) <= 100, beta(Y) + beta(Z) <= 128. Output beta (34/66, 34, 34/4).
-// zf != nullptr: Z3 is formed as Z * zf with zf = 2Y returned (the Z ratio
-// Z3 / Z that the isomorphic key tables record, verify.h ktab_build; same
-// cost: one multiplication instead of one squaring; Z3 beta 2).
 template <class F>
-BH_HD void j_dbl(J30& r, const J30& p, uint32_t* zf = nullptr) {
+BH_HD void j_dbl(J30& r, const J30& p) {
   if constexpr (F::a_is_minus3) {
     uint32_t delta[9], gamma[9], bt[9], t0[9], t1[9], u[9], alpha[9];
     f_sqr<F>(delta, p.Z);                 // [b2]
@@ -48,15 +45,11 @@ BH_HD void j_dbl(J30& r, const J30& p, uint32_t* zf = nullptr) {
     f_add(t1, p.X, delta);                // [bX+2]
     f_mul<F>(u, t0, t1);                  // [b2]  (bX+32)(bX+2) <= 13464
     f_mulc<3>(alpha, u);                  // [b6]
-    if (zf) {  // Z3 = Z (2Y)
-      f_add(zf, p.Y, p.Y);                // [2bY]
-      f_mul<F>(r.Z, p.Z, zf);             // [b2]
-    } else {   // Z3 = (Y + Z)^2 - gamma - delta
-      f_add(t0, p.Y, p.Z);                // [bY+bZ]
-      f_sqr<F>(t0, t0);                   // [b2]
-      f_add(t1, gamma, delta);            // [b4]
-      f_sub<F, 32>(r.Z, t0, t1);          // [b34]
-    }
+    // Z3 = (Y + Z)^2 - gamma - delta
+    f_add(t0, p.Y, p.Z);                  // [bY+bZ]
+    f_sqr<F>(t0, t0);                     // [b2]
+    f_add(t1, gamma, delta);              // [b4]
+    f_sub<F, 32>(r.Z, t0, t1);            // [b34]
     // X3 = alpha^2 - 8 beta
     f_sqr<F>(u, alpha);                   // [b2]  36
     f_mulc<8>(t0, bt);                    // [b16]
@@ -74,17 +67,11 @@ BH_HD void j_dbl(J30& r, const J30& p, uint32_t* zf = nullptr) {
     uint32_t A[9], B[9], Cc[9], D[9], E[9], t[9], t2[9];
     f_sqr<F>(A, p.X);                     // [b2]
     f_sqr<F>(B, p.Y);                     // [b2]
-    if (zf) {
-      f_add(zf, p.Y, p.Y);                // [2bY]
-      f_mul<F>(t, p.Z, zf);               // [b2]  2 bY bZ <= 16000
-    } else {
-      f_mul<F>(t, p.Y, p.Z);              // [b2]  bY*bZ <= 16000
-    }
+    f_mul<F>(t, p.Y, p.Z);                // [b2]  bY*bZ <= 16000
     f_sqr<F>(Cc, B);                      // [b2]
     f_add(t2, p.X, B);                    // [bX+2]
     f_sqr<F>(t2, t2);                     // [b2]
-    if (zf) f_copy(r.Z, t);               // [b2]
-    else f_mulc<2>(r.Z, t);               // [b4]
+    f_mulc<2>(r.Z, t);                    // [b4]
     f_add(t, A, Cc);                      // [b4]
     f_sub<F, 32>(t2, t2, t);              // [b34]
     f_mulc<2>(D, t2);                     // [b68]
@@ -106,9 +93,8 @@ BH_HD void j_dbl(J30& r, const J30& p, uint32_t* zf = nullptr) {
 // (X (2Y)^2, Y (2Y)^3, 2YZ) = (4 X Y^2, 8 Y^4, Z3), both intermediates of the
 // doubling. Requires beta(X) <= 63, beta(Y) + beta(Z) <= 128. Output r as
 // j_dbl (a = -3: (34, 34, 34); a = 0: (34, 34, 4)); pp beta (8, 16) / (2, 16).
-// zf: as j_dbl (Z3 = Z * zf, zf = 2Y returned).
 template <class F>
-BH_HD void j_dblu(J30& r, J30& pp, const J30& p, uint32_t* zf = nullptr) {
+BH_HD void j_dblu(J30& r, J30& pp, const J30& p) {
   if constexpr (F::a_is_minus3) {
     uint32_t delta[9], gamma[9], bt[9], t0[9], t1[9], u[9], alpha[9];
     f_sqr<F>(delta, p.Z);                 // [b2]
@@ -118,15 +104,10 @@ BH_HD void j_dblu(J30& r, J30& pp, const J30& p, uint32_t* zf = nullptr) {
     f_add(t1, p.X, delta);                // [bX+2]
     f_mul<F>(u, t0, t1);                  // [b2]
     f_mulc<3>(alpha, u);                  // [b6]
-    if (zf) {
-      f_add(zf, p.Y, p.Y);                // [2bY]
-      f_mul<F>(r.Z, p.Z, zf);             // [b2]   2YZ
-    } else {
-      f_add(t0, p.Y, p.Z);                // [bY+bZ]
-      f_sqr<F>(t0, t0);                   // [b2]
-      f_add(t1, gamma, delta);            // [b4]
-      f_sub<F, 32>(r.Z, t0, t1);          // [b34]  2YZ
-    }
+    f_add(t0, p.Y, p.Z);                  // [bY+bZ]
+    f_sqr<F>(t0, t0);                     // [b2]
+    f_add(t1, gamma, delta);              // [b4]
+    f_sub<F, 32>(r.Z, t0, t1);            // [b34]  2YZ
     f_sqr<F>(u, alpha);                   // [b2]
     f_mulc<8>(t0, bt);                    // [b16]
     f_sub<F, 32>(r.X, u, t0);             // [b34]
@@ -142,17 +123,11 @@ BH_HD void j_dblu(J30& r, J30& pp, const J30& p, uint32_t* zf = nullptr) {
     uint32_t A[9], B[9], Cc[9], D[9], E[9], t[9], t2[9];
     f_sqr<F>(A, p.X);                     // [b2]
     f_sqr<F>(B, p.Y);                     // [b2]
-    if (zf) {
-      f_add(zf, p.Y, p.Y);                // [2bY]
-      f_mul<F>(t, p.Z, zf);               // [b2]
-    } else {
-      f_mul<F>(t, p.Y, p.Z);              // [b2]
-    }
+    f_mul<F>(t, p.Y, p.Z);                // [b2]
     f_sqr<F>(Cc, B);                      // [b2]
     f_add(t2, p.X, B);                    // [bX+2]
     f_sqr<F>(t2, t2);                     // [b2]
-    if (zf) f_copy(r.Z, t);               // [b2]   2YZ
-    else f_mulc<2>(r.Z, t);               // [b4]   2YZ
+    f_mulc<2>(r.Z, t);                    // [b4]   2YZ
     f_add(t, A, Cc);                      // [b4]
     f_sub<F, 32>(t2, t2, t);              // [b34]
     f_mulc<2>(D, t2);                     // [b68]  D = 4 X Y^2
@@ -175,10 +150,9 @@ BH_HD void j_dblu(J30& r, J30& pp, const J30& p, uint32_t* zf = nullptr) {
 // rescaled in place to r's Z (5M + 2S instead of 12M + 4S). Requires
 // beta(X1), beta(Y1) <= 64, beta(X2), beta(Y2) <= 63, beta(Z) <= 34.
 // Output r beta (34, 34, 2), p beta (2, 2, 2). Incomplete: p = +-q is not
-// detected (callers guarantee it cannot happen). zf != nullptr receives the
-// Z ratio Z3 / Z = X1 - X2 (+64p, beta <= 128).
+// detected (callers guarantee it cannot happen).
 template <class F>
-BH_HD void j_zaddu(J30& r, J30& p, const J30& q, uint32_t* zf = nullptr) {
+BH_HD void j_zaddu(J30& r, J30& p, const J30& q) {
   uint32_t t1[9], c[9], w1[9], w2[9], t2[9], d[9], t3[9];
   f_sub<F, 64>(t1, p.X, q.X);             // [b128]
   f_sqr<F>(c, t1);                        // [b2]   C = (X1 - X2)^2
@@ -194,7 +168,6 @@ BH_HD void j_zaddu(J30& r, J30& p, const J30& q, uint32_t* zf = nullptr) {
   f_mul<F>(t3, t2, t3);                   // [b2]   128*66
   f_sub<F, 32>(r.Y, t3, p.Y);             // [b34]  Y3 = (Y1 - Y2)(W1 - X3) - A1
   f_mul<F>(r.Z, p.Z, t1);                 // [b2]   Z3 = Z (X1 - X2): 34*128
-  if (zf) f_copy(zf, t1);
   f_copy(p.X, w1);                        // [b2]
   f_copy(p.Z, r.Z);
 }

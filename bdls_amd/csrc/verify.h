@@ -914,12 +914,8 @@ BH_HD bool stage_ladder(const Work& w, const uint32_t* gtab, uint32_t i, uint32_
 // Records whose public key occurs >= kMinUses times in the batch share one
 // fixed-base table for their key, built inside the same step:
 //   entry (win, j) = (j+1) 2^(4 win) Q,  win in [0, 65), j in [0, 8)
-// u2 Q is then 65 table additions with 4-bit signed digits in [-7, 8] and no
-// doublings. The entries are stored AFFINE ON AN ISOMORPHIC CURVE (round 3):
-// all 520 share one Jacobian Z = Zc, so (X, Y) = (x Zc^2, y Zc^3) is an affine
-// point of E': y^2 = x^3 + a Zc^4 x + b Zc^6, and the table additions are mixed
-// additions (8M + 3S, which use neither a nor b) instead of full Jacobian ones
-// (12M + 4S). The sum (X', Y', Z') on E' is the E point (X', Y', Z' Zc).
+// (Jacobian, 28 words). u2 Q is then 65 table additions with 4-bit signed
+// digits in [-7, 8] and no doublings.
 constexpr int kKW = 4;                           // signed-window width (bits)
 constexpr int kKWin = (257 + kKW - 1) / kKW;     // 65 windows at 4 bits
 constexpr int kKEnt = 1 << (kKW - 1);            // 8 entries per window at 4 bits
@@ -956,35 +952,22 @@ BH_HD void recode_koff(uint32_t v[9], const uint32_t k[8]) {
   v[8] = (uint32_t)c + kKOff.v[8];
 }
 
-// Table layout (kKTabWords words per key). During the build, entry e =
-// win kKEnt + j is the raw Jacobian (X, Y) of the co-Z chain and the ratio
-// f_e = Z_e / Z_(e-1) at words [kQPt e, +27); the final entries (x', y') are
-// written by a backward pass at words [kKAffBase + kKAff e, +18), which never
-// overlaps a raw entry still to be read (kKAffBase >= (kQPt - kKAff) e for
-// every e); Zc goes to words [0, 9) last.
-constexpr uint32_t kKEntries = (uint32_t)kKWin * kKEnt;
-constexpr uint32_t kKAff = 20;  // words per final entry: x' (9), y' (9), pad
-constexpr uint32_t kKAffBase = 4160;
-static_assert(kKAffBase % 4 == 0 && kKAffBase >= (kQPt - kKAff) * (kKEntries - 1) &&
-                  kKAffBase + kKAff * kKEntries <= kKTabWords && kKAffBase >= 12,
-              "key-table layout");
-
-BH_HD void kraw_store(uint32_t* tab, uint32_t e, const J30& P, const uint32_t f[9]) {
+BH_HD void ktab_store(uint32_t* tab, uint32_t win, uint32_t j, const J30& P) {
   uint32_t v[28];
 #pragma unroll
   for (int k = 0; k < 9; k++) {
     v[k] = P.X[k];
     v[9 + k] = P.Y[k];
-    v[18 + k] = f[k];
+    v[18 + k] = P.Z[k];
   }
   v[27] = 0;
-  W4* d = reinterpret_cast<W4*>(tab + (size_t)e * kQPt);
+  W4* d = reinterpret_cast<W4*>(tab + ((size_t)win * kKEnt + j) * kQPt);
 #pragma unroll
   for (int q = 0; q < 7; q++) d[q] = W4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
 }
 
-BH_HD void kraw_load(uint32_t x[9], uint32_t y[9], uint32_t f[9], const uint32_t* tab, uint32_t e) {
-  const W4* s = reinterpret_cast<const W4*>(tab + (size_t)e * kQPt);
+BH_HD void ktab_load(J30& P, const uint32_t* tab, uint32_t win, uint32_t j) {
+  const W4* s = reinterpret_cast<const W4*>(tab + ((size_t)win * kKEnt + j) * kQPt);
   uint32_t v[28];
 #pragma unroll
   for (int q = 0; q < 7; q++) {
@@ -996,119 +979,51 @@ BH_HD void kraw_load(uint32_t x[9], uint32_t y[9], uint32_t f[9], const uint32_t
   }
 #pragma unroll
   for (int k = 0; k < 9; k++) {
-    x[k] = v[k];
-    y[k] = v[9 + k];
-    f[k] = v[18 + k];
+    P.X[k] = v[k];
+    P.Y[k] = v[9 + k];
+    P.Z[k] = v[18 + k];
   }
 }
 
-BH_HD void kaff_store(uint32_t* tab, uint32_t e, const uint32_t x[9], const uint32_t y[9]) {
-  W4* d = reinterpret_cast<W4*>(tab + kKAffBase + (size_t)e * kKAff);
-  d[0] = W4{x[0], x[1], x[2], x[3]};
-  d[1] = W4{x[4], x[5], x[6], x[7]};
-  d[2] = W4{x[8], y[0], y[1], y[2]};
-  d[3] = W4{y[3], y[4], y[5], y[6]};
-  d[4] = W4{y[7], y[8], 0u, 0u};
-}
-
-BH_HD void kaff_load(uint32_t x[9], uint32_t y[9], const uint32_t* tab, uint32_t win, uint32_t j) {
-  const W4* s = reinterpret_cast<const W4*>(tab + kKAffBase + ((size_t)win * kKEnt + j) * kKAff);
-  const W4 a = s[0], b = s[1], c = s[2], d = s[3], e = s[4];
-  x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
-  x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
-  x[8] = c.x; y[0] = c.y; y[1] = c.z; y[2] = c.w;
-  y[3] = d.x; y[4] = d.y; y[5] = d.z; y[6] = d.w;
-  y[7] = e.x; y[8] = e.y;
-}
-
-BH_HD void kzc_load(uint32_t zc[9], const uint32_t* tab) {
-#pragma unroll
-  for (int k = 0; k < 9; k++) zc[k] = tab[k];
-}
-
-// One lane per table. Forward: per window a co-Z chain (ec30.h j_dblu /
-// j_zaddu): DBLU gives 2B and B on 2B's Z, then six ZADDUs give 3B..8B, each
-// re-basing B onto the new sum's Z, and one doubling of 8B gives the next
-// window's base 16B: 8 + 6 x 7 + 8 = 58 F_p mul/sqr per window (the last
-// window's doubling is skipped). Every step multiplies Z by a ratio the chain
-// already forms (2Y for a doubling, X1 - X2 for a ZADDU), stored with the raw
-// (X, Y). Backward: with S_e = Zc / Z_e (S_519 = 1, S_(e-1) = S_e f_e), entry e
-// becomes (X S^2, Y S^3) on the common Z = Zc: 1S + 3M + 1M per entry, no
-// inversion (the isomorphic-curve trick of libsecp256k1's odd-multiples
-// tables). ZADDU cannot degenerate here: k B = +-B would need n to divide
-// (k -+ 1) 16^w with k - 1 <= 7, and n is a prime of 256 bits.
+// One lane per table: entry j of window w = (j+1) 16^w Q. Per window a co-Z
+// chain (ec30.h j_dblu / j_zaddu): DBLU gives 2B and B on 2B's Z, then six
+// ZADDUs give 3B..8B, each re-basing B onto the new sum's Z, and one doubling
+// of 8B gives the next window's base 16B:
+//   8 + 6 x 7 + 8 = 58 F_p mul/sqr per window (the plain Jacobian sequence,
+//   5 doublings + 3 full additions, is 88).
+// The entries are ordinary Jacobian points (each with its own Z), so the key
+// comb is unchanged. ZADDU cannot degenerate here: k B = +-B would need n to
+// divide (k -+ 1) 16^w with k - 1 <= 7, and n is a prime of 256 bits.
 template <class P>
 BH_HD void ktab_build(uint32_t* tab, const Work& w, uint32_t rec) {
   J30 B, Bz, S;
-  uint32_t f[9];
   ld9(B.X, w.qx, rec, w.ns);
   ld9(B.Y, w.qy, rec, w.ns);
   f_const(B.Z, P::r1);
-  f_const(f, P::r1);  // entry 0's ratio (never used)
-  uint32_t e = 0;
   for (uint32_t win = 0; win < (uint32_t)kKWin; win++) {
-    kraw_store(tab, e++, B, f);               // 1 B
-    j_dblu<P>(S, Bz, B, f);                   // S = 2B, Bz = B on S's Z
-    kraw_store(tab, e++, S, f);               // 2 B
+    ktab_store(tab, win, 0, B);               // 1 B
+    j_dblu<P>(S, Bz, B);                      // S = 2B, Bz = B on S's Z
+    ktab_store(tab, win, 1, S);               // 2 B
 #pragma unroll 1  // one ZADDU body (~10 KB of code; unrolled: same speed, 5x the code)
     for (uint32_t j = 2; j < (uint32_t)kKEnt; j++) {
       J30 T;
-      j_zaddu<P>(T, Bz, S, f);                // T = (j+1) B; Bz onto T's Z
-      kraw_store(tab, e++, T, f);
+      j_zaddu<P>(T, Bz, S);                   // T = (j+1) B; Bz onto T's Z
+      ktab_store(tab, win, j, T);
       j_copy(S, T);
     }
-    if (win + 1 < (uint32_t)kKWin) j_dbl<P>(B, S, f);  // 16 B: the next window's base
+    j_dbl<P>(B, S);                           // 16 B: the next window's base
   }
-  // backward: S.Z is the last entry's Z = Zc; entry 519 keeps its raw (X, Y).
-  // The raw entry of the next iteration is loaded one iteration ahead (a
-  // build lane is one wave per SIMD: a load it waits on is not hidden).
-  uint32_t x[9], y[9], fn[9], nx[9], ny[9], nf[9], s[9], s2[9], s3[9];
-  kraw_load(x, y, fn, tab, kKEntries - 1);
-  kraw_load(nx, ny, nf, tab, kKEntries - 2);
-  kaff_store(tab, kKEntries - 1, x, y);       // [b34]
-  f_copy(s, fn);                              // S_518
-#pragma unroll 1
-  for (uint32_t k = kKEntries - 1; k-- > 0;) {
-    f_copy(x, nx);
-    f_copy(y, ny);
-    f_copy(fn, nf);
-    if (k) kraw_load(nx, ny, nf, tab, k - 1);  // never overlaps final(k) (layout above)
-    f_sqr<P>(s2, s);                          // [b2]
-    f_mul<P>(s3, s2, s);                      // [b2]
-    f_mul<P>(x, x, s2);                       // [b2]
-    f_mul<P>(y, y, s3);                       // [b2]
-    kaff_store(tab, k, x, y);
-    if (k) f_mul<P>(s, s, fn);                // S_(k-1), [b2] (fn beta <= 128)
-  }
-  W4* zd = reinterpret_cast<W4*>(tab);
-  zd[0] = W4{S.Z[0], S.Z[1], S.Z[2], S.Z[3]};
-  zd[1] = W4{S.Z[4], S.Z[5], S.Z[6], S.Z[7]};
-  zd[2] = W4{S.Z[8], 0u, 0u, 0u};
-}
-
-template <class P>
-BH_HD void j_acc_iso(J30& A, bool& a_inf, bool& on_e, const uint32_t tx[9], const uint32_t ty[9],
-                     const uint32_t one[9], const uint32_t zc[9], bool t_inf);  // below
-
-// The sum on E' -> the E point (X', Y', Z' Zc) (unless an earlier rare window
-// already moved it to E).
-template <class P>
-BH_HD void iso_to_e(J30& A, bool on_e, const uint32_t zc[9]) {
-  if (!on_e) f_mul<P>(A.Z, A.Z, zc);
 }
 
 // u2 Q from a key table: kKW-bit signed windows (least significant first).
 template <class P>
 BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab) {
-  uint32_t k2[8], one[9], zc[9];
+  uint32_t k2[8];
   ld8(k2, w.r, i, w.ns);
-  kzc_load(zc, tab);
-  f_const(one, P::r1);
   a_inf = true;
-  bool on_e = false;
-  f_copy(A.X, one);
-  f_copy(A.Y, one);
-  f_copy(A.Z, one);
+  f_const(A.X, P::r1);
+  f_const(A.Y, P::r1);
+  f_const(A.Z, P::r1);
   uint32_t carry = 0;
   for (int win = 0; win < kKWin; win++) {
     // carry-scan digits in [-7, 8] (the wide path's recode_koff gives offset
@@ -1120,12 +1035,24 @@ BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint3
     const bool neg = t > 8u;
     const uint32_t mag = neg ? 16u - t : t;
     carry = neg ? 1u : 0u;
-    uint32_t tx[9], ty[9];
-    kaff_load(tx, ty, tab, win, mag ? mag - 1 : 0);
-    if (neg) f_neg<P, 64>(ty, ty);
-    j_acc_iso<P>(A, a_inf, on_e, tx, ty, one, zc, mag == 0);
+    J30 T;
+    ktab_load(T, tab, win, mag ? mag - 1 : 0);
+    if (neg) f_neg<P, 64>(T.Y, T.Y);
+    J30 R;
+    bool same;
+    const bool deg = j_add<P>(R, A, T, &same);
+    const bool take = mag != 0;
+    const bool use_t = take && a_inf;
+    const bool use_r = take && !a_inf && !deg;
+    const bool rare = take && !a_inf && deg;  // only via the mod-n wrap of the top window
+    j_sel(A, use_r, R, A);
+    j_sel(A, use_t, T, A);
+    if (rare) {
+      if (same) j_dbl<P>(A, T);
+      else a_inf = true;
+    }
+    if (use_t) a_inf = false;
   }
-  iso_to_e<P>(A, on_e, zc);
 }
 
 template <class P>
@@ -1354,51 +1281,6 @@ BH_HD void j_acc_aff(J30& A, bool& a_inf, const uint32_t tx[9], const uint32_t t
   if (use_t) a_inf = false;
 }
 
-// Acc += (tx, ty), an affine point of the key table's isomorphic curve E'
-// (mixed addition; the formula uses neither a nor b). The rare degenerate
-// case Acc = T needs a doubling, whose formula does use a: the sum then moves
-// to E -- Acc = 2 (tx, ty, Zc) -- and stays there (on_e): later windows add
-// (tx, ty, Zc) with the full Jacobian addition. Only crafted scalars reach it
-// (a partial sum equal to the next window's point).
-template <class P>
-BH_HD void j_acc_iso(J30& A, bool& a_inf, bool& on_e, const uint32_t tx[9], const uint32_t ty[9],
-                     const uint32_t one[9], const uint32_t zc[9], bool t_inf) {
-  if (on_e) {
-    J30 T;
-    f_copy(T.X, tx);
-    f_copy(T.Y, ty);
-    f_copy(T.Z, zc);
-    j_acc<P>(A, a_inf, T, t_inf);
-    return;
-  }
-  J30 R;
-  bool same;
-  const bool deg = j_madd<P>(R, A, tx, ty, &same);
-  const bool take = !t_inf;
-  const bool use_t = take && a_inf;
-  const bool use_r = take && !a_inf && !deg;
-  const bool rare = take && !a_inf && deg;
-  j_sel(A, use_r, R, A);
-  if (use_t) {
-    f_copy(A.X, tx);
-    f_copy(A.Y, ty);
-    f_copy(A.Z, one);
-  }
-  if (rare) {
-    if (same) {
-      J30 T;
-      f_copy(T.X, tx);
-      f_copy(T.Y, ty);
-      f_copy(T.Z, zc);
-      j_dbl<P>(A, T);
-      on_e = true;
-    } else {
-      a_inf = true;
-    }
-  }
-  if (use_t) a_inf = false;
-}
-
 template <class P, int L>
 BH_HD void g_comb_part(J30& C, bool& c_inf, const uint32_t* gtab, const uint32_t u1[8],
                        uint32_t l);  // below
@@ -1407,14 +1289,11 @@ BH_HD void g_comb_part(J30& C, bool& c_inf, const uint32_t* gtab, const uint32_t
 template <class P, int L>
 BH_HD void keycomb_q_part(J30& C, bool& c_inf, const Work& w, uint32_t i, const uint32_t* tab,
                           uint32_t l) {
-  uint32_t k[8], v[9], sv[9], one[9], zc[9];
-  f_const(one, P::r1);
-  kzc_load(zc, tab);
-  f_copy(C.X, one);
-  f_copy(C.Y, one);
-  f_copy(C.Z, one);
+  uint32_t k[8], v[9], sv[9];
+  f_const(C.X, P::r1);
+  f_const(C.Y, P::r1);
+  f_const(C.Z, P::r1);
   c_inf = true;
-  bool on_e = false;
   ld8(k, w.r, i, w.ns);
   recode_koff(v, k);
   shr288(sv, v, (uint32_t)kKW * l);
@@ -1424,13 +1303,12 @@ BH_HD void keycomb_q_part(J30& C, bool& c_inf, const Work& w, uint32_t i, const 
     shr_const<kKW * L>(sv);
     if (win < (uint32_t)kKWin) {
       const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-      uint32_t tx[9], ty[9];
-      kaff_load(tx, ty, tab, win, mag ? mag - 1 : 0);
-      if (d < 0) f_neg<P, 64>(ty, ty);
-      j_acc_iso<P>(C, c_inf, on_e, tx, ty, one, zc, mag == 0);
+      J30 T;
+      ktab_load(T, tab, win, mag ? mag - 1 : 0);
+      if (d < 0) f_neg<P, 64>(T.Y, T.Y);
+      j_acc<P>(C, c_inf, T, mag == 0);
     }
   }
-  iso_to_e<P>(C, on_e, zc);  // the group's butterfly and the G windows add on E
 }
 
 // Lane l's partial sum C = sum over its windows of (key-table digit points
