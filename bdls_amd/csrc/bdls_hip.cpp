@@ -85,6 +85,13 @@ size_t max_chunk() {
   return x > 0 ? std::min(kMaxChunk, round64((size_t)x)) : kMaxChunk;
 }
 
+// Compute lanes for host-API batches: 2 (default) or BH_LANES=1 (one lane,
+// every pass serialised as before round 3). Read per call.
+uint32_t lanes() {
+  const char* e = getenv("BH_LANES");
+  return (e && atoi(e) == 1) ? 1u : 2u;
+}
+
 size_t pow2_at_least(size_t v) {
   size_t p = 1;
   while (p < v) p <<= 1;
@@ -155,6 +162,21 @@ struct Slot {
 };
 constexpr int kSlots = 3;  // up to 3 host batches in flight per device
 
+// The second compute lane of a device (round 3). Host-API batches alternate
+// between lane 0 (Dev::stream / aux / ws) and lane 1, each with its own
+// workspace, so batch k+1's kernels run beside batch k's: the table builds (one
+// lane per key, chain-bound at one build wave per SIMD) and the plan stage's
+// short kernels leave issue slots that the other batch's waves fill. Everything
+// else -- the device-resident API, BDLS batches, registry writes, the latency
+// path -- stays serialised behind both lanes (wait_lanes).
+struct Lane1 {
+  hipStream_t stream = nullptr, aux = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, done = nullptr;
+  hipEvent_t build = nullptr;  // end of this lane's last table-build kernel
+  bool done_recorded = false;
+  DevBuf ws;
+};
+
 struct Dev {
   int id = -1;
   hipStream_t stream = nullptr;  // compute (+ result download)
@@ -172,8 +194,14 @@ struct Dev {
   uint32_t next_slot = 0;
   Registry reg[2];
   hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  hipEvent_t done = nullptr;  // end of the last pass (orders passes across streams)
+  hipEvent_t done = nullptr;  // end of the last pass on lane 0 (orders passes across streams)
   bool done_recorded = false;
+  Lane1 l1;                   // the second compute lane (host-API batches)
+  hipEvent_t build = nullptr; // end of lane 0's last table-build kernel
+  bool build_staggered = false;  // lane builds alternate (BH_LANE_STAGGER, default on)
+  uint32_t next_lane = 0;
+  hipEvent_t reg_written = nullptr;  // the last registry write (lane 1 passes wait for it)
+  bool reg_written_recorded = false;
   // deferred timing (bh_timing_begin/_end): one event set per pass, read at end
   bool defer = false;
   std::vector<std::vector<hipEvent_t>> ev_pool;
@@ -210,11 +238,13 @@ size_t work_bytes(size_t ns) {
          256 * 27;
 }
 
-int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl, bool reg = false) {
+int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl, bool reg = false,
+               DevBuf* ws = nullptr) {
   const size_t ns = round64(n);
-  int rc = d.ws.ensure(work_bytes(ns));
+  DevBuf& buf = ws ? *ws : d.ws;
+  int rc = buf.ensure(work_bytes(ns));
   if (rc) return rc;
-  char* p = (char*)d.ws.p;
+  char* p = (char*)buf.p;
   auto take = [&](size_t bytes) {
     char* q = p;
     p += round256(bytes);
@@ -252,6 +282,28 @@ int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl, bool reg = false) {
   return BH_OK;
 }
 
+// Order stream s after every pass on both lanes (serialised operations).
+hipError_t wait_lanes(Dev& d, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  if (d.done_recorded && (e = hipStreamWaitEvent(s, d.done, 0)) != hipSuccess) return e;
+  if (d.l1.done_recorded && s != d.l1.stream) e = hipStreamWaitEvent(s, d.l1.done, 0);
+  return e;
+}
+
+// Host wait for every pass on both lanes.
+int sync_lanes(Dev& d) {
+  if (d.done_recorded) HIPCHK(hipEventSynchronize(d.done));
+  if (d.l1.done_recorded) HIPCHK(hipEventSynchronize(d.l1.done));
+  return BH_OK;
+}
+
+// A registry write was enqueued on s: lane-1 passes enqueued later wait for it.
+hipError_t note_reg_write(Dev& d, hipStream_t s) {
+  hipError_t e = hipEventRecord(d.reg_written, s);
+  if (e == hipSuccess) d.reg_written_recorded = true;
+  return e;
+}
+
 // (Re)allocate and clear a key registry (caller holds d.mu, device set).
 int reg_alloc(Dev& d, int curve, size_t cap) {
   Registry& r = d.reg[curve];
@@ -259,7 +311,7 @@ int reg_alloc(Dev& d, int curve, size_t cap) {
   const size_t hc = pow2_at_least(2 * cap);
   const size_t bytes = round256(hc * 8) + round256(hc * 4) + round256(cap * 72) +
                        round256(cap * (size_t)bh::kKTabWords * 4) + 256;
-  if (d.done_recorded) HIPCHK(hipEventSynchronize(d.done));
+  if (int rc = sync_lanes(d)) return rc;
   r.mem.release();
   r.g = bh::KeyReg{};
   int rc = r.mem.ensure(bytes);
@@ -308,14 +360,36 @@ int dev_init(Dev& d, int id) {
   }
   for (auto& e : d.ev) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&d.reg_written, hipEventDisableTiming));
+  HIPCHK(hipStreamCreateWithFlags(&d.l1.stream, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&d.l1.aux, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&d.l1.fork, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&d.l1.join, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&d.l1.done, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&d.l1.build, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&d.build, hipEventDisableTiming));
+  {
+    const char* e = getenv("BH_LANE_STAGGER");
+    d.build_staggered = !(e && atoi(e) == 0);
+  }
   HIPCHK(hipStreamSynchronize(d.stream));
   return BH_OK;
 }
 
 void dev_free(Dev& d) {
   (void)hipSetDevice(d.id);
-  if (d.done_recorded) (void)hipEventSynchronize(d.done);
+  (void)sync_lanes(d);
   if (d.stream) (void)hipStreamSynchronize(d.stream);
+  if (d.l1.stream) {
+    (void)hipStreamSynchronize(d.l1.stream);
+    (void)hipStreamSynchronize(d.l1.aux);
+  }
+  d.l1.ws.release();
+  for (hipEvent_t e : {d.l1.fork, d.l1.join, d.l1.done, d.l1.build, d.build, d.reg_written})
+    if (e) (void)hipEventDestroy(e);
+  if (d.l1.aux) (void)hipStreamDestroy(d.l1.aux);
+  if (d.l1.stream) (void)hipStreamDestroy(d.l1.stream);
+  d.l1 = Lane1{};
   if (d.copy) (void)hipStreamSynchronize(d.copy);
   for (auto& g : d.gtab)
     if (g) (void)hipFree(g);
@@ -426,28 +500,44 @@ hipError_t launch(int curve, const bh::BdlsIn& in, const bh::Work& w, const bh::
 
 // Core device-resident pass (caller holds d.mu and has set the device).
 // With t != nullptr, events bracket every stage and the call synchronises.
+// lane -1: serialised (after every pass on both lanes; lane 0's workspace);
+// lane 0 / 1: a host-API batch on that lane (after the lane's previous pass;
+// lane 1 also after the last registry write). BH_F_KEEP_KEYS passes write the
+// registry and are always serialised.
 template <class B>
 int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* bitmap,
-            uint8_t* reason, hipStream_t s, bh_timing* t) {
+            uint8_t* reason, hipStream_t s, bh_timing* t, int lane = -1) {
   if (t) *t = bh_timing{};
+  if (flags & BH_F_KEEP_KEYS) lane = -1;
   if ((flags & BH_F_KEEP_KEYS) && d.reg[curve].g.cap == 0) {
     int rc = reg_alloc(d, curve, kDefaultRegCap);
     if (rc) return rc;
   }
-  // the workspace is shared by every pass on this device: a pass on another
-  // stream starts after the previous one ended
-  if (d.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.done, 0));
+  const bool l1 = lane == 1;
+  if (lane < 0) {
+    HIPCHK(wait_lanes(d, s));
+  } else if (!l1) {
+    if (d.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.done, 0));
+  } else {
+    if (d.l1.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.l1.done, 0));
+    if (d.reg_written_recorded) HIPCHK(hipStreamWaitEvent(s, d.reg_written, 0));
+  }
   const size_t chunk = max_chunk();
   for (size_t base = 0; base < n; base += chunk) {
     const size_t m = std::min(chunk, n - base);
     bh::Work w;
     bh::Plan pl;
-    int rc = carve_work(d, m, &w, &pl);
+    int rc = carve_work(d, m, &w, &pl, false, l1 ? &d.l1.ws : nullptr);
     if (rc) return rc;
     bh::LaunchOpts o = launch_opts(m, flags);
-    o.aux = d.aux;
-    o.ev_fork = d.fork;
-    o.ev_join = d.join;
+    o.aux = l1 ? d.l1.aux : d.aux;
+    o.ev_fork = l1 ? d.l1.fork : d.fork;
+    o.ev_join = l1 ? d.l1.join : d.join;
+    if (lane >= 0 && d.build_staggered && lanes() > 1) {
+      // (an event never recorded is complete: the first builds do not wait)
+      o.ev_build_wait = l1 ? d.build : d.l1.build;
+      o.ev_build_done = l1 ? d.l1.build : d.build;
+    }
     hipEvent_t* ev = t ? d.ev : nullptr;
     if (!t && d.defer) {
       if (d.ev_used == d.ev_pool.size()) {
@@ -479,8 +569,14 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
       t->wide = (uint32_t)o.wide;
     }
   }
-  HIPCHK(hipEventRecord(d.done, s));
-  d.done_recorded = true;
+  if (l1) {
+    HIPCHK(hipEventRecord(d.l1.done, s));
+    d.l1.done_recorded = true;
+  } else {
+    HIPCHK(hipEventRecord(d.done, s));
+    d.done_recorded = true;
+  }
+  if (flags & BH_F_KEEP_KEYS) HIPCHK(note_reg_write(d, s));
   return BH_OK;
 }
 
@@ -683,11 +779,14 @@ int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, 
   const B db = upload(u, b, lo, m, f);
   HIPCHK(u.err);
   HIPCHK(hipEventRecord(sl.uploaded, d.copy));
-  hipStream_t s = d.stream;
+  // alternate the compute lanes (BH_LANES=1: lane 0 only); registry writers
+  // (BH_F_KEEP_KEYS) serialise on lane 0
+  const int lane = (flags & BH_F_KEEP_KEYS) ? -1 : (int)(d.next_lane++ % lanes());
+  hipStream_t s = lane == 1 ? d.l1.stream : d.stream;
   HIPCHK(hipStreamWaitEvent(s, sl.uploaded, 0));
   uint64_t* dbm = (uint64_t*)sl.out.p;
   uint8_t* drs = (uint8_t*)(dbm + round64(m) / 64);
-  if ((rc = run_dev(d, curve, &db, m, flags, dbm, drs, s, nullptr))) return rc;
+  if ((rc = run_dev(d, curve, &db, m, flags, dbm, drs, s, nullptr, lane))) return rc;
   HIPCHK(hipMemcpyAsync(sl.host_out.p, dbm, round64(m) / 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync((uint8_t*)sl.host_out.p + round64(m) / 8, drs, m,
                         hipMemcpyDeviceToHost, s));
@@ -760,8 +859,9 @@ int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, si
     if (ml) std::memcpy(h + o_msg + mp, b->msg + b->msg_off[lo + i], ml);
     mp += ml;
   }
-  hipStream_t s = d.stream;
+  hipStream_t s = d.stream;  // lane 0: its workspace, and registry writes are ordered on it
   if (d.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.done, 0));
+  if (d.reg_written_recorded) HIPCHK(hipStreamWaitEvent(s, d.reg_written, 0));
   char* dv = (char*)sl.stage.p;
   HIPCHK(hipMemcpyAsync(dv, h, total, hipMemcpyHostToDevice, s));
   bh::Work w;
@@ -919,7 +1019,7 @@ void register_async(int curve, const uint8_t* pub, size_t n) {
     bh::Plan pl;
     if (carve_work(d, n, &w, &pl, true)) continue;
     hipStream_t s = d.stream;
-    if (d.done_recorded && hipStreamWaitEvent(s, d.done, 0) != hipSuccess) continue;
+    if (wait_lanes(d, s) != hipSuccess) continue;  // no pass reads the registry meanwhile
     if (hipMemcpyAsync(d.stage.p, d.reg_in.p, n * 64, hipMemcpyHostToDevice, s) != hipSuccess)
       continue;
     if (bh::launch_register(curve, (const uint8_t*)d.stage.p, w, pl, d.reg[curve].g,
@@ -927,6 +1027,7 @@ void register_async(int curve, const uint8_t* pub, size_t n) {
       continue;
     if (hipEventRecord(d.reg_done, s) == hipSuccess) d.reg_pending = true;
     if (hipEventRecord(d.done, s) == hipSuccess) d.done_recorded = true;
+    (void)note_reg_write(d, s);
   }
 }
 
@@ -945,6 +1046,7 @@ struct CspReq {
   int valid = 0, reason = 0, rc = BH_OK;
   std::string err;
   bool done = false;
+  std::condition_variable cv;  // this caller alone is woken (no thundering herd)
 };
 
 struct CspBatch {
@@ -998,6 +1100,7 @@ struct Coalescer {
     }
   }
 
+  // (caller holds mu) results out, each waiting caller woken on its own cv
   void complete(CspBatch& b, int rc, const std::string& err) {
     for (size_t i = 0; i < b.reqs.size(); i++) {
       CspReq* r = b.reqs[i];
@@ -1008,6 +1111,7 @@ struct Coalescer {
         r->valid = (b.bitmap[i >> 3] >> (i & 7)) & 1;
         r->reason = b.reason[i];
       }
+      r->cv.notify_one();
     }
   }
 
@@ -1092,7 +1196,7 @@ struct Coalescer {
       if (dl) b.dg.insert(b.dg.end(), dg, dg + dl);
       b.reqs.push_back(&req);
       cv_work.notify_one();
-      cv_done.wait(lk, [&] { return req.done; });
+      req.cv.wait(lk, [&] { return req.done; });
     }
     if (req.rc) return fail(req.rc, req.err);
     *valid = req.valid;
@@ -1339,8 +1443,9 @@ int bh_sync(int device) {
   if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
   std::lock_guard<std::mutex> g(d->mu);
   HIPCHK(hipSetDevice(d->id));
-  if (d->done_recorded) HIPCHK(hipEventSynchronize(d->done));
+  if (int rc = sync_lanes(*d)) return rc;
   HIPCHK(hipStreamSynchronize(d->stream));
+  HIPCHK(hipStreamSynchronize(d->l1.stream));
   return BH_OK;
 }
 
@@ -1442,7 +1547,7 @@ int bh_keys_register(int device, int curve, const uint8_t* pub, size_t n, uint8_
       bh::Plan pl;
       if ((rc = carve_work(d, m, &w, &pl, true))) return rc;
       hipStream_t s = d.stream;
-      if (d.done_recorded) HIPCHK(hipEventSynchronize(d.done));
+      if (int rc2 = sync_lanes(d)) return rc2;
       HIPCHK(hipMemcpyAsync(d.stage.p, pub + lo * 64, m * 64, hipMemcpyHostToDevice, s));
       HIPCHK(bh::launch_register(curve, (const uint8_t*)d.stage.p, w, pl, d.reg[curve].g,
                                  (uint32_t)m, (uint8_t*)d.out.p, s));
@@ -1460,7 +1565,7 @@ int bh_keys_clear(int device, int curve) {
   return for_devices(device, [&](Dev& d) -> int {
     const bh::KeyReg& g = d.reg[curve].g;
     if (g.cap == 0) return BH_OK;
-    if (d.done_recorded) HIPCHK(hipEventSynchronize(d.done));
+    if (int rc = sync_lanes(d)) return rc;
     HIPCHK(hipMemsetAsync(g.slot_hash, 0, (size_t)g.hc * 8, d.stream));
     HIPCHK(hipMemsetAsync(g.count, 0, 4, d.stream));
     HIPCHK(hipStreamSynchronize(d.stream));
@@ -1477,7 +1582,7 @@ int bh_keys_count(int device, int curve, size_t* count) {
     const bh::KeyReg& g = d.reg[curve].g;
     size_t c = 0;
     if (g.cap) {
-      if (d.done_recorded) HIPCHK(hipEventSynchronize(d.done));
+      if (int rc = sync_lanes(d)) return rc;
       uint32_t v = 0;
       HIPCHK(hipMemcpy(&v, g.count, 4, hipMemcpyDeviceToHost));
       c = std::min<size_t>(v, g.cap);

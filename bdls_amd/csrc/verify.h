@@ -121,6 +121,12 @@ struct LaunchOpts {
   void* aux = nullptr;
   void* ev_fork = nullptr;
   void* ev_join = nullptr;
+  // Two compute lanes (bdls_hip.cpp Lane1): the table-build kernel waits for
+  // the other lane's last build (build_wait) and marks its own end
+  // (build_done), so the two lanes' chain-bound builds alternate and each runs
+  // beside the other lane's key comb instead of beside its build.
+  void* ev_build_wait = nullptr;
+  void* ev_build_done = nullptr;
 };
 
 // Lanes per record on the key-table path by batch size (records far below

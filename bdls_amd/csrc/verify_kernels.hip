@@ -387,6 +387,11 @@ __global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
     return;
   }
   if (blockIdx.x < tab_blocks) {
+#ifdef BH_BUILD_PRIO
+    // the builds are chain-bound (one lane per table): let their waves issue
+    // first, the u1 G / ladder waves (and the other lane's kernels) fill in
+    __builtin_amdgcn_s_setprio(BH_BUILD_PRIO);
+#endif
     const uint32_t nt = min(pl.counters[2], pl.max_tables);
     const uint32_t base = blockIdx.x * kBuildPerBlock;
     const uint32_t t = base + threadIdx.x;
@@ -942,8 +947,10 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
     return hipGetLastError();
   }
   // (small secp256k1 batches are BDLS, hence split: the 2-lane GLV ladder)
+  if (o.ev_build_wait && (e = hipStreamWaitEvent(s, (hipEvent_t)o.ev_build_wait, 0))) return e;
   hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x + gp_blocks), blk, 0, s, w, plc,
                      g, gtab, reason, tab_blocks, grd.x);
+  if (o.ev_build_done && (e = hipEventRecord((hipEvent_t)o.ev_build_done, s))) return e;
   REC(4);
   if (o.keep)
     hipLaunchKernelGGL(k_reg_publish, dim3((pl.max_tables + 255) / 256), blk, 0, s, w, plc, g);
