@@ -387,11 +387,6 @@ __global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
     return;
   }
   if (blockIdx.x < tab_blocks) {
-#ifdef BH_BUILD_PRIO
-    // the builds are chain-bound (one lane per table): let their waves issue
-    // first, the u1 G / ladder waves (and the other lane's kernels) fill in
-    __builtin_amdgcn_s_setprio(BH_BUILD_PRIO);
-#endif
     const uint32_t nt = min(pl.counters[2], pl.max_tables);
     const uint32_t base = blockIdx.x * kBuildPerBlock;
     const uint32_t t = base + threadIdx.x;
