@@ -215,6 +215,51 @@ BH_HD int32_t divsteps30(int32_t zeta, uint32_t f, uint32_t g, Div2x2& t) {
   return zeta;
 }
 
+// Variable-time form of divsteps30 for a lane that inverts ONE public scalar
+// alone (the latency kernel k_small: no other lane waits on its schedule).
+// Same 30 divsteps and the same transition matrix, computed in runs: a run of
+// zero low bits of g is one shift, and up to min(eta + 1, i, 6) low bits of g
+// are cancelled at once by adding w f, w = -g f^-1 mod 2^limit (f^-1 mod 64 by
+// one Newton step from f, valid mod 8 for odd f). eta = -delta (starts at -1).
+// The published variable-time optimisation of Bernstein-Yang's divsteps.
+BH_HD int32_t divsteps30_var(int32_t eta, uint32_t f, uint32_t g, Div2x2& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  int i = 30;
+  for (;;) {
+    const int zeros = __builtin_ctz(g | (0xffffffffu << i));
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+    if (i == 0) break;
+    // g is odd here
+    if (eta < 0) {
+      const uint32_t x = f, y = u, z = v;
+      eta = -eta;
+      f = g;
+      u = q;
+      v = r;
+      g = 0u - x;
+      q = 0u - y;
+      r = 0u - z;
+    }
+    int limit = eta + 1 < i ? eta + 1 : i;
+    if (limit > 6) limit = 6;
+    const uint32_t m = (0xffffffffu >> (32 - limit)) & 63u;
+    const uint32_t finv = f * (2u - f * f);   // f^-1 mod 64
+    const uint32_t w = (0u - g * finv) & m;   // g + w f = 0 mod 2^limit
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+  t.u = (int32_t)u;
+  t.v = (int32_t)v;
+  t.q = (int32_t)q;
+  t.r = (int32_t)r;
+  return eta;
+}
+
 constexpr int32_t kS30Mask = 0x3fffffff;
 
 // [d, e] <- (t [d, e] + m [md, me]) / 2^30 with md, me chosen so the division
@@ -285,7 +330,9 @@ BH_HD void s30_addm_neg(int32_t d[9], bool c, bool neg) {
 }
 
 // r = a^-1 mod m for plain canonical a in [1, m) (32-bit limbs in and out).
-template <class M>
+// VAR: divsteps30_var batches, stopping once g = 0 (the remaining batches
+// would leave d mod m and f unchanged).
+template <class M, bool VAR = false>
 BH_HD void mod_inv_sg(uint32_t r[8], const uint32_t a[8]) {
   int32_t d[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   int32_t e[9] = {1, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -298,10 +345,21 @@ BH_HD void mod_inv_sg(uint32_t r[8], const uint32_t a[8]) {
     if (w + 1 < 8) x |= (uint64_t)a[w + 1] << 32;
     g[i] = (int32_t)((x >> s) & (i < 8 ? (uint64_t)kS30Mask : 0xffffffffull));
   }
+  // divsteps30: zeta = -(delta + 1/2), delta = 1/2 (600 >= 590 steps suffice);
+  // divsteps30_var: eta = -delta, Bernstein-Yang's original delta = 1, whose
+  // bound for 256-bit inputs is (49 * 256 + 57) / 17 = 741 <= 25 * 30 steps
   int32_t zeta = -1;
-  for (int it = 0; it < 20; it++) {
+  for (int it = 0; it < (VAR ? 25 : 20); it++) {
     Div2x2 t;
-    zeta = divsteps30(zeta, (uint32_t)f[0], (uint32_t)g[0], t);
+    if constexpr (VAR) {
+      int32_t any = 0;
+#pragma unroll
+      for (int k = 0; k < 9; k++) any |= g[k];
+      if (!any) break;
+      zeta = divsteps30_var(zeta, (uint32_t)f[0], (uint32_t)g[0], t);
+    } else {
+      zeta = divsteps30(zeta, (uint32_t)f[0], (uint32_t)g[0], t);
+    }
     divsteps_update_de<M>(d, e, t);
     divsteps_update_fg(f, g, t);
   }
@@ -318,11 +376,12 @@ BH_HD void mod_inv_sg(uint32_t r[8], const uint32_t a[8]) {
 }
 
 // Montgomery-domain inverse by safegcd: input aR, output a^-1 R
-// ((aR)^-1 * R^3 * R^-1).
-template <class M>
+// ((aR)^-1 * R^3 * R^-1). VAR: variable-time divsteps with an early exit
+// once g = 0 (a lane inverting alone; the result is the same).
+template <class M, bool VAR = false>
 BH_HD void mont_inv_sg(uint32_t r[8], const uint32_t a[8]) {
   uint32_t t[8], r3[8];
-  mod_inv_sg<M>(t, a);
+  mod_inv_sg<M, VAR>(t, a);
   load_const8(r3, M::r3);
   mont_mul<M>(r, t, r3);
 }

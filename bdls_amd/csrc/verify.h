@@ -424,7 +424,7 @@ BH_HD void stage_prep(const BdlsIn& in, const Work& w, uint32_t i) {
 // One lane's records (strided). Montgomery's trick: one safegcd inversion per
 // lane, 3 multiplications per record. U1 = false (BDLS batches whose digests
 // are still being hashed): w = s^-1 R goes to w.sm for stage_u1, u1 later.
-template <class N, bool U1 = true>
+template <class N, bool U1 = true, bool VAR = false>
 BH_HD void stage_inv(const Work& w, uint32_t c, uint32_t stride, uint32_t n) {
   // lane c owns records c, c + stride, c + 2 stride, ... (< n): consecutive
   // lanes touch consecutive records, so every limb access is coalesced
@@ -439,7 +439,7 @@ BH_HD void stage_inv(const Work& w, uint32_t c, uint32_t stride, uint32_t n) {
   }
   if (c >= n) return;
   uint32_t inv[8];
-  mont_inv_sg<N>(inv, acc);  // (prod s_i)^-1 * R
+  mont_inv_sg<N, VAR>(inv, acc);  // (prod s_i)^-1 * R
   for (uint32_t i = last;; i -= stride) {
     uint32_t pre[8], wi[8], t[8];
     ld8(pre, w.pre, i, w.ns);
@@ -1226,7 +1226,7 @@ BH_HD void shr288(uint32_t o[9], const uint32_t v[9], uint32_t sh) {
   for (int q = 0; q < 9; q++) {
     uint32_t x = 0;
 #pragma unroll
-    for (uint32_t d = 0; d < 6; d++)
+    for (uint32_t d = 0; d < 9; d++)  // every word shift of a 288-bit value
       if (ws == d) x = (q + (int)d < 9) ? v[q + d] : 0u;
     t[q] = x;
   }

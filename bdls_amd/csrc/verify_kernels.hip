@@ -587,15 +587,17 @@ __global__ __launch_bounds__(256) void k_bitmap(const uint8_t* __restrict__ reas
 }
 
 // ---- latency path: two launches for a small batch (bh_csp_verify_p256's
-// coalesced batches, small host batches). 16 lanes per record. k_small: lane
-// 0 runs prep and the record's own inverse (no batch inversion, no plan, no
-// dedup) and looks the key up in the registry; a registered key's record is
-// finished by the group (key-table and G-comb windows over 16 lanes,
+// coalesced batches, small host batches). 32 lanes per record (round 3: 3 key
+// windows + 1 G window + a 5-level butterfly per lane, ~140 F_p ops of chain
+// against ~166 at 16 lanes). k_small: lane 0 runs prep and the record's own
+// inverse (variable-time safegcd: no batch inversion, no plan, no dedup) and
+// looks the key up in the registry; a registered key's record is finished by
+// the group (key-table and G-comb windows over 32 lanes,
 // butterfly, lane 0 checks); an unregistered one is marked for k_small_lad
 // (lane 0 runs the Booth ladder while the group adds the G-comb windows) --
 // a separate kernel so that neither carries the other's registers. Same
 // stage functions (verify.h) as the batch path: bit-identical results.
-constexpr int kSmallL = 16;
+constexpr int kSmallL = 32;
 constexpr uint8_t kSmallLadder = 0xfeu;  // reason placeholder: k_small_lad's record
 template <class P, class N, class CV, int HK>
 __global__ __launch_bounds__(256) void k_small(BatchIn in, Work w, KeyReg g,
@@ -609,7 +611,7 @@ __global__ __launch_bounds__(256) void k_small(BatchIn in, Work w, KeyReg g,
     stage_prep<P, N, CV, HK>(in, w, j);
     uint32_t t = kNone;
     if ((w.st[j] & 0x7fu) == R_OK) {
-      stage_inv<N, true>(w, j, n, n);  // this record alone: u1 = e w, u2 = r w
+      stage_inv<N, true, true>(w, j, n, n);  // this record alone (variable-time): u1, u2
       t = reg_lookup(g, w, j, key_hash(w, j));
     }
     tab_of[grp] = t;

@@ -59,6 +59,7 @@ static bool keycomb_any(const Work& w, const uint32_t* gtab, uint32_t i, const u
     case 4: return wide_keycomb<P, 4>(w, gtab, i, tab);
     case 8: return wide_keycomb<P, 8>(w, gtab, i, tab);
     case 16: return wide_keycomb<P, 16>(w, gtab, i, tab);
+    case 32: return wide_keycomb<P, 32>(w, gtab, i, tab);  // k_small's group
     case 0: return stage_keycomb<P>(w, gtab, i, tab);
     default:  // the device's split: u1 G stored by list position, then the table half
       stage_gpart<P>(w, gtab, i, i);
@@ -226,6 +227,10 @@ extern "C" void hs_bdls_hash(uint32_t version, const uint8_t* x32, const uint8_t
 extern "C" void hs_n_inv(int curve, const uint32_t* a, uint32_t* r) {
   if (curve == 0) mod_inv_sg<Fn_p256>(r, a);
   else mod_inv_sg<Fn_k1>(r, a);
+}
+extern "C" void hs_n_inv_var(int curve, const uint32_t* a, uint32_t* r) {
+  if (curve == 0) mod_inv_sg<Fn_p256, true>(r, a);
+  else mod_inv_sg<Fn_k1, true>(r, a);
 }
 extern "C" void hs_n_mont_inv(int curve, const uint32_t* a, uint32_t* r) {
   if (curve == 0) mont_inv_sg<Fn_p256>(r, a);

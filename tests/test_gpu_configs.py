@@ -204,3 +204,41 @@ def test_unique_keys_one_pass_of_1m(L):
     assert (reason == w.reason).all() and (bits == w.expected_valid).all()
     assert tm.n_ladder == int((w.reason == 0).sum()) + int((w.reason == 9).sum())
     orc_sample(w, 200, seed=3)
+
+
+def test_two_lanes_with_registry_writes(L):
+    """Host batches alternate between the device's two compute lanes; a
+    BH_F_KEEP_KEYS batch writes the key registry and is serialised behind both
+    lanes, and the lane-1 batches after it wait for that write. Six batches in
+    flight in submission order [plain, keep, plain, plain, keep, plain] over
+    overlapping key sets (large enough for key tables), collected out of order:
+    every bitmap and reason equal the expected ones, and the registry holds
+    the kept keys afterwards."""
+    _lib.check(L.bh_keys_clear(0, 0))
+    ws = [workload.generate(40_000 + 1111 * k, 800 + 50 * k, 96, 8, seed=60 + k % 3)
+          for k in range(6)]
+    flags = [0, _lib.BH_F_KEEP_KEYS, 0, 0, _lib.BH_F_KEEP_KEYS, 0]
+    keep, jobs = [], []
+    for w, f in zip(ws, flags):
+        arrs = []
+        for x in w.arrays():
+            h, v = _lib.HostArray.from_numpy(x)
+            keep.append(h)
+            arrs.append(v)
+        b = _lib.BhBatch(*[x.ctypes.data for x in arrs])
+        keep.append(b)
+        bm = np.zeros((w.n + 7) // 8, np.uint8)
+        rs = np.zeros(w.n, np.uint8)
+        job = ctypes.c_void_p()
+        _lib.check(L.bh_verify_submit(0, ctypes.byref(b), w.n, _lib.BH_F_HASH_SHA256 | f,
+                                      bm.ctypes.data, rs.ctypes.data, ctypes.byref(job)))
+        jobs.append((job, bm, rs, w))
+    for k in [3, 0, 5, 1, 4, 2]:
+        job, bm, rs, w = jobs[k]
+        _lib.check(L.bh_verify_wait(job))
+        assert (rs == w.reason).all(), k
+        assert (np.unpackbits(bm, bitorder="little")[:w.n].astype(bool) == w.expected_valid).all(), k
+    cnt = ctypes.c_size_t()
+    _lib.check(L.bh_keys_count(0, 0, ctypes.byref(cnt)))
+    assert cnt.value > 0
+    _lib.check(L.bh_keys_clear(0, 0))

@@ -70,7 +70,7 @@ def test_hostsim_golden_keycomb_path(hs, golden, fused):
     assert not bad
 
 
-@pytest.mark.parametrize("wide", [4, 16])
+@pytest.mark.parametrize("wide", [4, 16, 32])
 @pytest.mark.parametrize("fused", [False, True])
 def test_hostsim_golden_wide_keycomb(hs, golden, fused, wide):
     """The L-lanes-per-record key-table path (k_keycomb_wide): interleaved
@@ -181,7 +181,7 @@ def _p256_crafted_u2_records():
     return recs
 
 
-@pytest.mark.parametrize("wide", [1, 16, 4])
+@pytest.mark.parametrize("wide", [1, 16, 4, 32])
 def test_hostsim_p256_crafted_u2_both_recodings(hs, wide):
     """q_keycomb (carry-scan digits in [-7, 8]) and the wide path's
     keycomb_q_part (offset digits in [-8, 7]) on scalars at every recoding

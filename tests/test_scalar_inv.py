@@ -55,3 +55,17 @@ def test_mont_inv_sg(L, curve):
     for a in cases(n)[:100]:
         L.hs_n_mont_inv(curve, to8(a * R % n), out)
         assert from8(out) == pow(a, -1, n) * R % n, hex(a)
+
+
+@pytest.mark.parametrize("curve", [0, 1])
+def test_mod_inv_sg_variable_time(L, curve):
+    """The latency kernel's variable-time divsteps (divsteps30_var: runs of
+    zeros shifted at once, up to 6 low bits cancelled per step, early exit at
+    g = 0) give the same inverse as the constant-time schedule."""
+    n = N[curve]
+    rng = random.Random(curve + 99)
+    out = (ctypes.c_uint32 * 8)()
+    for a in cases(n) + [rng.randrange(1, n) for _ in range(3000)] + \
+            [rng.randrange(1, 2**k) for k in range(1, 257, 5)]:
+        L.hs_n_inv_var(curve, to8(a), out)
+        assert from8(out) == pow(a, -1, n), hex(a)
