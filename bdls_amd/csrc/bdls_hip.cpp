@@ -530,6 +530,10 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
     int rc = carve_work(d, m, &w, &pl, false, l1 ? &d.l1.ws : nullptr);
     if (rc) return rc;
     bh::LaunchOpts o = launch_opts(m, flags);
+    {
+      const char* e = getenv("BH_LL");
+      o.ll_tables = !(e && atoi(e) == 0);
+    }
     o.aux = l1 ? d.l1.aux : d.aux;
     o.ev_fork = l1 ? d.l1.fork : d.fork;
     o.ev_join = l1 ? d.l1.join : d.join;

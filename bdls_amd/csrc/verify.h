@@ -127,6 +127,9 @@ struct LaunchOpts {
   // beside the other lane's key comb instead of beside its build.
   void* ev_build_wait = nullptr;
   void* ev_build_done = nullptr;
+  // per-batch key tables of one-lane-per-record batches as Lim-Lee combs
+  // (verify.h lltab_build; BH_LL=0 keeps the 4-bit windows everywhere)
+  bool ll_tables = true;
 };
 
 // Lanes per record on the key-table path by batch size (records far below
@@ -1061,6 +1064,100 @@ BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint3
   }
 }
 
+// ---------------------------------------------------------------- per-key Lim-Lee comb
+// Per-batch key tables of LARGE batches (one lane per record, o.wide == 1;
+// round 3). A Lim-Lee comb with 7 teeth spaced 37 bits apart:
+//   T[b] = sum over the set bits i of b of 2^(37 i) Q,   b in [1, 128)
+// (127 Jacobian entries, 28 words each, entry b at index b - 1), and
+//   u2 Q = sum_{j < 37} 2^j T[b_j],  b_j = bits j, j + 37, ..., j + 222 of u2,
+// by Horner: 36 doublings + 37 table additions per record instead of the 65
+// additions of the 4-bit windows (a doubling, 3M + 5S, issues ~1,440 VALU
+// instructions against ~2,950 for an addition). Build, one lane per table:
+// B_k = 2^(37 k) Q by 222 doublings, then every T[b] along a Gray-code walk
+// (each step adds or subtracts one B_k: 120 additions) -- about the windowed
+// build's chain length (3,696 vs 3,770 F_p ops), a quarter of its table
+// bytes. No step of the walk can degenerate: every T[b] is a sum of distinct
+// 2^(37 i) Q with 37 i <= 222, never +-B_k for k outside it (the integers
+// differ and stay below n). Registry tables and small batches keep the
+// windowed tables (their lanes split the windows; a comb's doublings cannot).
+constexpr int kLLTeeth = 7, kLLSpace = 37;
+constexpr uint32_t kLLEnt = (1u << kLLTeeth) - 1u;
+static_assert(kLLTeeth * kLLSpace >= 256 && kLLEnt * kQPt <= kKTabWords, "comb table");
+
+BH_HD void lltab_store(uint32_t* tab, uint32_t b, const J30& P) {
+  ktab_store(tab, 0, b - 1, P);  // entry b - 1 (window 0 addressing, 28 words each)
+}
+
+BH_HD void lltab_load(J30& P, const uint32_t* tab, uint32_t b) { ktab_load(P, tab, 0, b - 1); }
+
+template <class P>
+BH_HD void lltab_build(uint32_t* tab, const Work& w, uint32_t rec) {
+  J30 B;
+  ld9(B.X, w.qx, rec, w.ns);
+  ld9(B.Y, w.qy, rec, w.ns);
+  f_const(B.Z, P::r1);
+  lltab_store(tab, 1, B);                       // B_0 = Q
+  for (uint32_t k = 1; k < (uint32_t)kLLTeeth; k++) {
+#pragma unroll 1
+    for (int d = 0; d < kLLSpace; d++) j_dbl<P>(B, B);
+    lltab_store(tab, 1u << k, B);               // B_k = 2^(37 k) Q
+  }
+  // Gray-code walk: g_i = i ^ (i >> 1) flips bit ctz(i) at step i
+  J30 A, Bk, Bn;
+  lltab_load(A, tab, 1);
+  lltab_load(Bn, tab, 2);                       // the base point of step 2
+#pragma unroll 1
+  for (uint32_t i = 2; i <= kLLEnt; i++) {
+    const uint32_t k = (uint32_t)__builtin_ctz(i);
+    const uint32_t g = i ^ (i >> 1), gp = (i - 1) ^ ((i - 1) >> 1);
+    j_copy(Bk, Bn);
+    if (i < kLLEnt) {
+      const uint32_t kn = (uint32_t)__builtin_ctz(i + 1);
+      lltab_load(Bn, tab, 1u << kn);            // prefetch the next step's base point
+    }
+    if ((g & (g - 1u)) == 0u) {                 // a base point: stored by phase A
+      lltab_load(A, tab, g);
+      continue;
+    }
+    if (g < gp) f_neg<P, 64>(Bk.Y, Bk.Y);       // bit k cleared: subtract B_k
+    J30 R;
+    bool same;
+    (void)j_add<P>(R, A, Bk, &same);            // never degenerate (see above)
+    j_copy(A, R);
+    lltab_store(tab, g, A);
+  }
+}
+
+// u2 Q from a Lim-Lee comb table (Horner over the 37 columns, top first).
+template <class P>
+BH_HD void q_llcomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab) {
+  uint32_t k2[8];
+  ld8(k2, w.r, i, w.ns);
+  uint64_t sl[kLLTeeth];  // bits [37 s, 37 s + 37) of u2
+#pragma unroll
+  for (int t = 0; t < kLLTeeth; t++) {
+    const int lo = kLLSpace * t, wd = lo >> 5, sh = lo & 31;
+    uint64_t x = (uint64_t)k2[wd] >> sh;
+    if (wd + 1 < 8) x |= (uint64_t)k2[wd + 1] << (32 - sh);
+    if (wd + 2 < 8 && sh > 27) x |= (uint64_t)k2[wd + 2] << (64 - sh);
+    sl[t] = x & ((1ull << kLLSpace) - 1ull);
+  }
+  a_inf = true;
+  f_const(A.X, P::r1);
+  f_const(A.Y, P::r1);
+  f_const(A.Z, P::r1);
+#pragma unroll 1
+  for (int j = kLLSpace - 1; j >= 0; j--) {
+    uint32_t b = 0;
+#pragma unroll
+    for (int t = 0; t < kLLTeeth; t++) b |= (uint32_t)((sl[t] >> j) & 1ull) << t;
+    j_dbl<P>(A, A);  // (while a_inf, A is a placeholder the next point replaces)
+    J30 T;
+    lltab_load(T, tab, b ? b : 1u);
+    j_acc<P>(A, a_inf, T, b == 0);
+  }
+}
+
 template <class P>
 BH_HD bool stage_keycomb(const Work& w, const uint32_t* gtab, uint32_t i, const uint32_t* tab) {
   J30 A, B;
@@ -1096,10 +1193,12 @@ BH_HD void stage_gpart(const Work& w, const uint32_t* gtab, uint32_t i, uint32_t
 }
 
 template <class P>
-BH_HD bool stage_keycomb_q(const Work& w, uint32_t i, uint32_t j, const uint32_t* tab) {
+BH_HD bool stage_keycomb_q(const Work& w, uint32_t i, uint32_t j, const uint32_t* tab,
+                           bool ll = false) {
   J30 A, B;
   bool a_inf;
-  q_keycomb<P>(A, a_inf, w, i, tab);
+  if (ll) q_llcomb<P>(A, a_inf, w, i, tab);  // a per-batch Lim-Lee comb table
+  else q_keycomb<P>(A, a_inf, w, i, tab);
   const uint32_t* o = w.gpart + j;
 #pragma unroll
   for (int k = 0; k < 9; k++) {

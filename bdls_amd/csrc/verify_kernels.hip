@@ -380,7 +380,7 @@ __global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
                                                      const uint32_t* __restrict__ gtab,
                                                      uint8_t* __restrict__ reason,
                                                      uint32_t tab_blocks,
-                                                     uint32_t lad_blocks) {
+                                                     uint32_t lad_blocks, uint32_t ll) {
   if (blockIdx.x >= tab_blocks + lad_blocks) {
     const uint32_t j = (blockIdx.x - tab_blocks - lad_blocks) * blockDim.x + threadIdx.x;
     if (j < pl.counters[0]) stage_gpart<P>(w, gtab, pl.comb_order[j], j);
@@ -390,7 +390,14 @@ __global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
     const uint32_t nt = min(pl.counters[2], pl.max_tables);
     const uint32_t base = blockIdx.x * kBuildPerBlock;
     const uint32_t t = base + threadIdx.x;
-    if (t < nt) ktab_build<P>(const_cast<uint32_t*>(tab_ptr(pl, g, pl.tab_dst[t])), w, pl.tab_rec[t]);
+    if (t < nt) {
+      // per-batch tables of one-lane-per-record batches are Lim-Lee combs;
+      // registry tables (and small batches') keep the 4-bit windows
+      const uint32_t id = pl.tab_dst[t];
+      uint32_t* tab = const_cast<uint32_t*>(tab_ptr(pl, g, id));
+      if (ll && (id & kLocal)) lltab_build<P>(tab, w, pl.tab_rec[t]);
+      else ktab_build<P>(tab, w, pl.tab_rec[t]);
+    }
     return;
   }
   const uint32_t j0 = (blockIdx.x - tab_blocks) * blockDim.x + threadIdx.x;
@@ -513,12 +520,13 @@ __global__ __launch_bounds__(256) void k_reg_publish(Work w, Plan pl, KeyReg g) 
 template <class P>
 __global__ __launch_bounds__(256) BH_KEYCOMB_ATTR void k_keycomb(Work w, Plan pl, KeyReg g,
                                                  const uint32_t* __restrict__ gtab,
-                                                 uint8_t* __restrict__ reason) {
+                                                 uint8_t* __restrict__ reason, uint32_t ll) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t cnt = pl.counters[0];
   if (j >= cnt) return;
   const uint32_t i = pl.comb_order[j];
-  const bool ok = stage_keycomb_q<P>(w, i, j, tab_ptr(pl, g, pl.rec_tab[i]));
+  const uint32_t id = pl.rec_tab[i];
+  const bool ok = stage_keycomb_q<P>(w, i, j, tab_ptr(pl, g, id), ll && (id & kLocal));
   reason[i] = ok ? R_OK : R_MATH;
 }
 
@@ -913,7 +921,7 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   if (split) {
     // key tables (no u1), then the u2 Q halves; u1 G after the join
     hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, plc, g, gtab, reason,
-                       tab_blocks, 0u);
+                       tab_blocks, 0u, 0u);
     if constexpr (!P::a_is_minus3)
       hipLaunchKernelGGL((k_ladder2_q<P>), wgrd(2 * n), wblk, 0, s, w, plc,
                          pstride);
@@ -945,8 +953,10 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   }
   // (small secp256k1 batches are BDLS, hence split: the 2-lane GLV ladder)
   if (o.ev_build_wait && (e = hipStreamWaitEvent(s, (hipEvent_t)o.ev_build_wait, 0))) return e;
+  // Lim-Lee comb tables for the one-lane key comb (o.wide == 1)
+  const uint32_t ll = (o.ll_tables && o.wide <= 1) ? 1u : 0u;
   hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x + gp_blocks), blk, 0, s, w, plc,
-                     g, gtab, reason, tab_blocks, grd.x);
+                     g, gtab, reason, tab_blocks, grd.x, ll);
   if (o.ev_build_done && (e = hipEventRecord((hipEvent_t)o.ev_build_done, s))) return e;
   REC(4);
   if (o.keep)
@@ -962,7 +972,7 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
                          g, gtab, reason);
       break;
     default:
-      hipLaunchKernelGGL((k_keycomb<P>), grd, blk, 0, s, w, plc, g, gtab, reason);
+      hipLaunchKernelGGL((k_keycomb<P>), grd, blk, 0, s, w, plc, g, gtab, reason, ll);
   }
   hipLaunchKernelGGL(k_bitmap, grd, blk, 0, s, reason, n, bitmap);
   REC(6);
@@ -1022,7 +1032,7 @@ static hipError_t reg_seq(const uint8_t* pub, const Work& w, const Plan& pl, con
   hipLaunchKernelGGL(k_key_plan, grd, blk, 0, s, w, pl, g, n, 1u, 0u, 1u, 1u);
   const uint32_t tab_blocks = (pl.max_tables + kBuildPerBlock - 1) / kBuildPerBlock;
   hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, pl, g,
-                     (const uint32_t*)nullptr, (uint8_t*)nullptr, tab_blocks, 0u);
+                     (const uint32_t*)nullptr, (uint8_t*)nullptr, tab_blocks, 0u, 0u);
   hipLaunchKernelGGL(k_reg_publish, dim3((pl.max_tables + 255) / 256), blk, 0, s, w, pl, g);
   hipLaunchKernelGGL(k_reg_status, grd, blk, 0, s, w, pl, n, status);
   return hipGetLastError();

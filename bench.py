@@ -45,17 +45,22 @@ sys.path.insert(0, ROOT)
 # Algorithmic work per verify in SURVEY.md 8(d) units: F_p mul/sqr x 128 u32
 # MACs (64 product + 64 reduction). The variable-base ladder is schedule S0
 # (3.2e3 F_p ops = 4.1e5 MACs). The per-key comb path is split over two
-# kernels: k_ktab_ladder builds the key tables (co-Z chain, 65 windows x 58 F_p
-# ops = 3,770 per table) and, beside them, the u1 G half of every key-comb
-# record (G_WINDOWS mixed adds of 11 ops over the 10-bit G comb: BH_GCOMB_BITS
-# in verify.h); k_keycomb adds the 65 key-table points (KTAB_ADD ops each) and
-# the stored u1 G and checks x (~23 ops).
+# kernels: k_ktab_ladder builds the key tables and, beside them, the u1 G half
+# of every key-comb record (G_WINDOWS mixed adds of 11 ops over the 10-bit G
+# comb: BH_GCOMB_BITS in verify.h); k_keycomb adds the key-table part and the
+# stored u1 G and checks x (~23 ops). Per-batch tables of large batches are
+# Lim-Lee combs (round 3, verify.h lltab_build; BH_LL=0: 4-bit windows):
+#   build: 222 doublings (8 ops) + 120 additions (16) = 3,696 per table
+#   comb:  36 doublings + 37 additions = 880 per record
+# windows: build 65 x 58 = 3,770 per table (co-Z chain), comb 65 additions
+# (16 ops: the tables are Jacobian) = 1,040 per record.
 MAC_PER_FP = 128
 G_COMB_BITS = 10
 G_WINDOWS = (257 + G_COMB_BITS - 1) // G_COMB_BITS
-KTAB_ADD = 16  # Jacobian addition (12M + 4S): the key tables are Jacobian
-FP_LADDER, FP_GPART, FP_KTAB = 3200, G_WINDOWS * 11, 65 * 58
-FP_KEYCOMB = 65 * KTAB_ADD + 23
+LL_TABLES = os.environ.get("BH_LL", "1") != "0"
+FP_LADDER, FP_GPART = 3200, G_WINDOWS * 11
+FP_KTAB = 222 * 8 + 120 * 16 if LL_TABLES else 65 * 58
+FP_KEYCOMB = (36 * 8 + 37 * 16 if LL_TABLES else 65 * 16) + 23
 MACS_PER_VERIFY = FP_LADDER * MAC_PER_FP
 KERNELS = {"build_ladder_ms": "k_ktab_ladder", "keycomb_ms": "k_keycomb"}
 CONFIG5_TOTAL = 1 << 26

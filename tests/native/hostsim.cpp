@@ -30,6 +30,11 @@ static const uint32_t* gtab_for() {
 // 1 = k_keycomb.
 static int g_wide = 1;
 extern "C" void hs_set_wide(int L) { g_wide = L; }
+// 1: per-batch tables of the one-lane comb (g_wide == 1) are Lim-Lee combs
+// (verify.h lltab_build / q_llcomb), as the device builds them for large
+// batches; 0: the 4-bit windowed tables.
+static int g_ll = 0;
+extern "C" void hs_set_ll(int on) { g_ll = on; }
 
 template <class P, int L>
 static bool wide_keycomb(const Work& w, const uint32_t* gtab, uint32_t i, const uint32_t* tab) {
@@ -63,7 +68,7 @@ static bool keycomb_any(const Work& w, const uint32_t* gtab, uint32_t i, const u
     case 0: return stage_keycomb<P>(w, gtab, i, tab);
     default:  // the device's split: u1 G stored by list position, then the table half
       stage_gpart<P>(w, gtab, i, i);
-      return stage_keycomb_q<P>(w, i, i, tab);
+      return stage_keycomb_q<P>(w, i, i, tab, g_ll != 0);
   }
 }
 
@@ -135,7 +140,8 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
       if (tab_of[r] == kNone) {
         tab_of[r] = (uint32_t)tables.size();
         tables.emplace_back(kKTabWords);
-        ktab_build<P>(tables.back().data(), w, r);  // the device's co-Z chain
+        if (g_ll && g_wide == 1) lltab_build<P>(tables.back().data(), w, r);  // comb
+        else ktab_build<P>(tables.back().data(), w, r);  // the device's co-Z chain
       }
       ok = keycomb_any<P>(w, gtab, i, tables[tab_of[r]].data());
       combs++;

@@ -151,7 +151,7 @@ def test_hostsim_two_span_messages(hs, family):
     assert (l1 == 0).any() and (l2 == 0).any() and ((l1 > 64) & (l2 > 64)).any()
 
 
-def _p256_crafted_u2_records():
+def _p256_crafted_u2_records(extra=()):
     """P-256 signatures built for chosen u2 at key-table window boundaries
     (digit carries of the carry-scan recoding, the offset recoding's borrow
     edges, the top window, n - 1, n/2) -- R = u1 G + u2 Q, r = x(R) mod n,
@@ -166,7 +166,7 @@ def _p256_crafted_u2_records():
     u2s = [1, 7, 8, 9, 15, 16, 17, 0x88, 0x8888, 0x7777, 2**252, 2**256 - n, n - 1, n - 2,
            n // 2, n // 2 + 1, (16**64 - 1) % n, sum(8 * 16**k for k in range(64)) % n,
            sum(9 * 16**k for k in range(64)) % n, sum(7 * 16**k for k in range(64)) % n]
-    u2s += [rng.randrange(1, n) for _ in range(6)]
+    u2s += [rng.randrange(1, n) for _ in range(6)] + list(extra)
     recs = []
     for u2 in u2s:
         u1 = rng.randrange(1, n)
@@ -226,3 +226,55 @@ def test_multi_device_shard_split(hs, n):
                                ctypes.byref(ns))
         assert rc == 0, (n, nd, rc)
         assert ns.value == min(nd, (n + 63) // 64)
+
+
+# scalars at the Lim-Lee comb's edges (7 teeth, 37-bit spacing): a single
+# tooth, the top column empty or full, every column equal, the last tooth's
+# 34 bits, a lone column
+_LL_U2 = [2**36, 2**37, 2**74, 2**222, 2**255, 2**222 + 2**221, 2**37 - 1,
+          sum(2**(37 * t) for t in range(7)), sum(2**(37 * t + 36) for t in range(6)),
+          sum(2**(37 * t + 36) for t in range(6)) + 2**255, (2**37 - 1) << 185,
+          sum((2**37 - 1) << (37 * t) for t in range(6))]
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_hostsim_golden_llcomb(hs, golden, fused):
+    """Per-batch Lim-Lee comb tables (lltab_build / q_llcomb: what the device
+    builds for one-lane-per-record batches): bit-exact on every golden record."""
+    recs = [r for r in golden if (not fused) or "msg" in r]
+    hs.hs_set_ll(1)
+    try:
+        out, ncomb = run2(hs, pack(recs, fused), fused, 1)
+    finally:
+        hs.hs_set_ll(0)
+    assert ncomb > 0
+    bad = [(r["tag"], int(o), r["reason"]) for r, o in zip(recs, out) if o != r["reason"]]
+    assert not bad
+
+
+def test_hostsim_p256_crafted_u2_llcomb(hs):
+    """The comb on crafted scalars (window edges and the comb's own: empty top
+    column, single teeth, full columns): every signature verifies, every
+    flipped-digest twin fails."""
+    recs = _p256_crafted_u2_records(_LL_U2)
+    pub = np.frombuffer(b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big")
+                                 for x, y, _, _ in recs), np.uint8)
+    sigs, dgs = [t[2] for t in recs], [t[3] for t in recs]
+    sl = np.array([len(x) for x in sigs], np.uint32)
+    dl = np.array([len(x) for x in dgs], np.uint32)
+    so = np.concatenate([[0], np.cumsum(sl[:-1])]).astype(np.uint64)
+    do = np.concatenate([[0], np.cumsum(dl[:-1])]).astype(np.uint64)
+    sig = np.frombuffer(b"".join(sigs), np.uint8)
+    dg = np.frombuffer(b"".join(dgs), np.uint8)
+    out = np.zeros(len(recs), np.uint8)
+    ncomb = ctypes.c_uint32()
+    hs.hs_set_ll(1)
+    try:
+        hs.hs_verify2(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
+                      dg.ctypes.data, do.ctypes.data, dl.ctypes.data, len(recs), 2, 4, 1,
+                      out.ctypes.data, ctypes.byref(ncomb))
+    finally:
+        hs.hs_set_ll(0)
+    assert ncomb.value > 0
+    assert [int(o) for o in out[0::2]] == [0] * (len(recs) // 2)
+    assert all(int(o) == 9 for o in out[1::2])

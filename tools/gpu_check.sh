@@ -20,9 +20,10 @@ for s in $STEPS; do
     hostinfo) (nproc; python -c "import os; print(os.cpu_count(), len(os.sched_getaffinity(0)))"; cat /sys/fs/cgroup/cpu.max 2>/dev/null; lscpu | head -20) > gpurun_out/hostinfo.txt 2>&1; cat gpurun_out/hostinfo.txt ;;
     bench)  timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err; ok_or_stop $rc bench ;;
     prof)   export TMPDIR=/tmp; timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1; rc=$?; tail -3 gpurun_out/prof.log; ok_or_stop $rc prof ;;
-    exp)    for so in build/exp/libbdlship_*.so; do v=$(basename $so .so); BDLS_HIP_LIB=$PWD/$so timeout -k 10 300 python bench.py --steps ${EXP_STEPS:-10} --warmup 2 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/exp_$v.json 2> gpurun_out/exp_$v.err; rc=$?; echo "$v rc=$rc"; case $rc in 0|3) ;; *) echo "STOP after exp $v (exit $rc)"; exit $rc ;; esac; done ;;
+    exp)    for so in build/exp/libbdlship_*.so; do v=$(basename $so .so); BDLS_HIP_LIB=$PWD/$so timeout -k 10 300 python bench.py --steps ${EXP_STEPS:-10} --warmup 2 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/exp_$v.json 2> gpurun_out/exp_$v.err; rc=$?; echo "$v rc=$rc"; case $rc in 0|3) ;; *) echo "STOP after exp $v (exit $rc)"; exit $rc ;; esac; done ;;
     lanes1) BH_LANES=1 timeout -k 10 600 python bench.py --steps ${EXP_STEPS:-20} --warmup 2 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/bench_lanes1.json 2> gpurun_out/bench_lanes1.err; rc=$?; cat gpurun_out/bench_lanes1.json; ok_or_stop $rc lanes1 ;;
     nostagger) BH_LANE_STAGGER=0 timeout -k 10 600 python bench.py --steps ${EXP_STEPS:-20} --warmup 2 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/bench_nostagger.json 2> gpurun_out/bench_nostagger.err; rc=$?; cat gpurun_out/bench_nostagger.json; ok_or_stop $rc nostagger ;;
+    noll) BH_LL=0 timeout -k 10 600 python bench.py --steps ${EXP_STEPS:-20} --warmup 2 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/bench_noll.json 2> gpurun_out/bench_noll.err; rc=$?; cat gpurun_out/bench_noll.json; ok_or_stop $rc noll ;;
     probe)  timeout -k 10 180 python -u tools/small_probe.py 1 8 64 256 > gpurun_out/small_probe.json 2> gpurun_out/small_probe.err; rc=$?; cat gpurun_out/small_probe.json; ok_or_stop $rc probe ;;
     probeprof) export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_small -o small -- python3 tools/small_probe.py 1 64 > gpurun_out/probeprof.log 2>&1; rc=$?; tail -2 gpurun_out/probeprof.log; ok_or_stop $rc probeprof ;;
     pmclist) export TMPDIR=/tmp; timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc_list.txt 2>&1; rc=$?; ok_or_stop $rc pmclist ;;
