@@ -825,6 +825,9 @@ BH_HD uint32_t bits6(const uint32_t v[5], uint32_t b) {
 
 template <class P>
 BH_HD void j_acc(J30& A, bool& a_inf, const J30& T, bool t_inf);  // below
+template <class P>
+BH_HD void j_acc_aff(J30& A, bool& a_inf, const uint32_t tx[9], const uint32_t ty[9],
+                     const uint32_t one[9], bool t_inf);  // below
 
 // parts: bit 0 = the k1 Q half, bit 1 = the k2 phi(Q) half (3 = all of u2 Q;
 // the 2-lane ladder runs one half per lane and adds the two results).
@@ -1068,72 +1071,211 @@ BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint3
 // Per-batch key tables of LARGE batches (one lane per record, o.wide == 1;
 // round 3). A Lim-Lee comb with 7 teeth spaced 37 bits apart:
 //   T[b] = sum over the set bits i of b of 2^(37 i) Q,   b in [1, 128)
-// (127 Jacobian entries, 28 words each, entry b at index b - 1), and
+// stored AFFINE (x, y: 20 words at word 20 (b - 1)), and
 //   u2 Q = sum_{j < 37} 2^j T[b_j],  b_j = bits j, j + 37, ..., j + 222 of u2,
-// by Horner: 36 doublings + 37 table additions per record instead of the 65
-// additions of the 4-bit windows (a doubling, 3M + 5S, issues ~1,440 VALU
-// instructions against ~2,950 for an addition). Build, one lane per table:
-// B_k = 2^(37 k) Q by 222 doublings, then every T[b] along a Gray-code walk
-// (each step adds or subtracts one B_k: 120 additions) -- about the windowed
-// build's chain length (3,696 vs 3,770 F_p ops), a quarter of its table
-// bytes. No step of the walk can degenerate: every T[b] is a sum of distinct
-// 2^(37 i) Q with 37 i <= 222, never +-B_k for k outside it (the integers
-// differ and stay below n). Registry tables and small batches keep the
-// windowed tables (their lanes split the windows; a comb's doublings cannot).
+// by Horner: 36 doublings + 37 mixed additions per record instead of the 65
+// full additions of the 4-bit windows (a doubling, 3M + 5S, and a mixed
+// addition, 8M + 3S, issue ~1,440 and ~2,100 VALU instructions against ~2,950
+// for a full addition). Build: one lane per table (one build wave per SIMD,
+// beside the u1 G waves: the kernel runs at 2 waves per SIMD, so more build
+// lanes per table only take the slots those waves fill). 222 doublings give
+// B_k = 2^(37 k) Q, made affine by one inversion; a Gray-code walk then reaches
+// every other T[b] by one mixed addition of +-B_k, storing raw Jacobian entries
+// and the running product of their Z; one more inversion and a backward pass
+// (Montgomery's trick) make them affine. About 4,100 F_p ops per table (the
+// Jacobian comb of round 3's first cut: 3,696), 127 x 80 B = 10 KB, a
+// sixth of the windowed table's bytes. No walk step can degenerate: every T[b]
+// is a sum of distinct 2^(37 i) Q with 37 i <= 222, never +-B_k for k outside
+// it (the integers differ and stay below n). Registry tables and small
+// batches keep the windowed tables (their lanes split the windows; a comb's
+// doubling chain cannot be split).
 constexpr int kLLTeeth = 7, kLLSpace = 37;
 constexpr uint32_t kLLEnt = (1u << kLLTeeth) - 1u;
-static_assert(kLLTeeth * kLLSpace >= 256 && kLLEnt * kQPt <= kKTabWords, "comb table");
+constexpr uint32_t kLLAff = 20;                 // words per affine entry
+constexpr uint32_t kLLRaw = 2560;               // raw Jacobian entries (28 words) while building
+constexpr uint32_t kLLPre = kLLRaw + 28u * 128u; // running Z products (12 words per step)
+static_assert(kLLTeeth * kLLSpace >= 256 && kLLAff * kLLEnt <= kLLRaw &&
+                  kLLPre + 12u * 128u <= kKTabWords && kLLPre % 4 == 0, "comb table layout");
 
-BH_HD void lltab_store(uint32_t* tab, uint32_t b, const J30& P) {
-  ktab_store(tab, 0, b - 1, P);  // entry b - 1 (window 0 addressing, 28 words each)
+BH_HD void llraw_store(uint32_t* tab, uint32_t b, const J30& P) { ktab_store(tab + kLLRaw, 0, b, P); }
+BH_HD void llraw_load(J30& P, const uint32_t* tab, uint32_t b) { ktab_load(P, tab + kLLRaw, 0, b); }
+
+BH_HD void llpre_store(uint32_t* tab, uint32_t m, const uint32_t z[9]) {
+  W4* d = reinterpret_cast<W4*>(tab + kLLPre + 12u * m);
+  d[0] = W4{z[0], z[1], z[2], z[3]};
+  d[1] = W4{z[4], z[5], z[6], z[7]};
+  d[2] = W4{z[8], 0u, 0u, 0u};
 }
 
-BH_HD void lltab_load(J30& P, const uint32_t* tab, uint32_t b) { ktab_load(P, tab, 0, b - 1); }
+BH_HD void llpre_load(uint32_t z[9], const uint32_t* tab, uint32_t m) {
+  const W4* s = reinterpret_cast<const W4*>(tab + kLLPre + 12u * m);
+  const W4 a = s[0], b = s[1], c = s[2];
+  z[0] = a.x; z[1] = a.y; z[2] = a.z; z[3] = a.w;
+  z[4] = b.x; z[5] = b.y; z[6] = b.z; z[7] = b.w;
+  z[8] = c.x;
+}
+
+BH_HD void llaff_store(uint32_t* tab, uint32_t b, const uint32_t x[9], const uint32_t y[9]) {
+  W4* d = reinterpret_cast<W4*>(tab + (size_t)(b - 1) * kLLAff);
+  d[0] = W4{x[0], x[1], x[2], x[3]};
+  d[1] = W4{x[4], x[5], x[6], x[7]};
+  d[2] = W4{x[8], y[0], y[1], y[2]};
+  d[3] = W4{y[3], y[4], y[5], y[6]};
+  d[4] = W4{y[7], y[8], 0u, 0u};
+}
+
+BH_HD void llaff_load(uint32_t x[9], uint32_t y[9], const uint32_t* tab, uint32_t b) {
+  const W4* s = reinterpret_cast<const W4*>(tab + (size_t)(b - 1) * kLLAff);
+  const W4 a = s[0], c = s[1], d = s[2], e = s[3], f = s[4];
+  x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+  x[4] = c.x; x[5] = c.y; x[6] = c.z; x[7] = c.w;
+  x[8] = d.x; y[0] = d.y; y[1] = d.z; y[2] = d.w;
+  y[3] = e.x; y[4] = e.y; y[5] = e.z; y[6] = e.w;
+  y[7] = f.x; y[8] = f.y;
+}
+
+// Field inverse by safegcd (fe.h mod_inv_sg, constant iteration so the lanes
+// of a wave stay together): a R -> a^-1 R for the radix-2^30 field (any beta
+// f_reduce accepts, a != 0 mod p). The divsteps run on the canonical value
+// (a R)^-1, and one product with R^3 returns to the Montgomery domain. About a
+// third of the Fermat chain's instructions (255 squarings + 12 products).
+template <class P>
+BH_HD void f_inv_sg(uint32_t r[9], const uint32_t a[9]) {
+  uint32_t c[9], c8[8], i8[8], r3[9];
+  f_reduce<P>(c, a);
+  f_to_u256(c8, c);
+  mod_inv_sg<typename P::M32>(i8, c8);
+  f_from_u256(c, i8);
+  f_const(r3, P::r3);
+  f_mul<P>(r, c, r3);
+}
+
+// Walk position m (1..127) -> table index gray(m); the base points B_k sit at
+// m = 2^(k+1) - 1 (gray(m) = 2^k).
+BH_HD uint32_t ll_gray(uint32_t m) { return m ^ (m >> 1); }
+BH_HD bool ll_is_base(uint32_t m) { return (m & (m + 1u)) == 0u; }
+// the affine point step m reads: B_k itself at a base step, else the B_k it adds
+BH_HD uint32_t ll_walk_src(uint32_t m) {
+  return ll_is_base(m) ? ll_gray(m) : 1u << __builtin_ctz(m);
+}
 
 template <class P>
 BH_HD void lltab_build(uint32_t* tab, const Work& w, uint32_t rec) {
+  uint32_t one[9];
+  f_const(one, P::r1);
+  // 1. B_k = 2^(37 k) Q (222 doublings; raw Jacobian copies of B_1..B_6 and
+  //    the running product of their Z), then all six made affine with one
+  //    inversion (Montgomery's trick) and written to their final slots T[2^k]
   J30 B;
   ld9(B.X, w.qx, rec, w.ns);
   ld9(B.Y, w.qy, rec, w.ns);
-  f_const(B.Z, P::r1);
-  lltab_store(tab, 1, B);                       // B_0 = Q
+  llaff_store(tab, 1, B.X, B.Y);
+  f_copy(B.Z, one);
+  uint32_t z[9];
   for (uint32_t k = 1; k < (uint32_t)kLLTeeth; k++) {
 #pragma unroll 1
     for (int d = 0; d < kLLSpace; d++) j_dbl<P>(B, B);
-    lltab_store(tab, 1u << k, B);               // B_k = 2^(37 k) Q
+    llraw_store(tab, 1u << k, B);
+    if (k == 1) f_copy(z, B.Z);
+    else f_mul<P>(z, z, B.Z);
+    llpre_store(tab, k, z);  // prod_{1 <= i <= k} Z_i (slots reused below)
   }
-  // Gray-code walk: g_i = i ^ (i >> 1) flips bit ctz(i) at step i
-  J30 A, Bk, Bn;
-  lltab_load(A, tab, 1);
-  lltab_load(Bn, tab, 2);                       // the base point of step 2
+  uint32_t inv[9];
+  f_inv_sg<P>(inv, z);
 #pragma unroll 1
-  for (uint32_t i = 2; i <= kLLEnt; i++) {
-    const uint32_t k = (uint32_t)__builtin_ctz(i);
-    const uint32_t g = i ^ (i >> 1), gp = (i - 1) ^ ((i - 1) >> 1);
-    j_copy(Bk, Bn);
-    if (i < kLLEnt) {
-      const uint32_t kn = (uint32_t)__builtin_ctz(i + 1);
-      lltab_load(Bn, tab, 1u << kn);            // prefetch the next step's base point
+  for (uint32_t k = kLLTeeth - 1; k >= 1; k--) {
+    J30 E;
+    llraw_load(E, tab, 1u << k);
+    uint32_t zi[9], z2[9], z3[9];
+    if (k > 1) {
+      uint32_t pre[9];
+      llpre_load(pre, tab, k - 1);
+      f_mul<P>(zi, inv, pre);
+      f_mul<P>(inv, inv, E.Z);
+    } else {
+      f_copy(zi, inv);
     }
-    if ((g & (g - 1u)) == 0u) {                 // a base point: stored by phase A
-      lltab_load(A, tab, g);
-      continue;
+    f_sqr<P>(z2, zi);
+    f_mul<P>(z3, z2, zi);
+    f_mul<P>(E.X, E.X, z2);
+    f_mul<P>(E.Y, E.Y, z3);
+    llaff_store(tab, 1u << k, E.X, E.Y);
+  }
+  // 2. The Gray walk m = 1..127: a base step restarts from B_k (affine, Z = 1);
+  //    every other step adds or subtracts one B_k (mixed addition) and stores
+  //    the raw Jacobian entry. pre[m] = product of the Z of the non-base
+  //    entries up to m (pre[1] = 1). The next step's point is loaded one step
+  //    ahead, off the dependency chain.
+  J30 A;
+  f_copy(A.Z, one);
+  f_copy(z, one);
+  llpre_store(tab, 1, z);
+  uint32_t nx[9], ny[9];
+  llaff_load(A.X, A.Y, tab, 1);  // m = 1: T[1] = Q
+  llaff_load(nx, ny, tab, ll_walk_src(2));
+#pragma unroll 1
+  for (uint32_t m = 2; m <= kLLEnt; m++) {
+    uint32_t bx[9], by[9];
+    f_copy(bx, nx);
+    f_copy(by, ny);
+    if (m < kLLEnt) llaff_load(nx, ny, tab, ll_walk_src(m + 1));
+    if (ll_is_base(m)) {
+      f_copy(A.X, bx);
+      f_copy(A.Y, by);
+      f_copy(A.Z, one);
+    } else {
+      const uint32_t g = ll_gray(m);
+      if (g < ll_gray(m - 1)) f_neg<P, 64>(by, by);  // bit cleared: subtract B_k
+      J30 R;
+      bool same;
+      (void)j_madd<P>(R, A, bx, by, &same);  // never degenerate (see above)
+      j_copy(A, R);
+      llraw_store(tab, g, A);
+      f_mul<P>(z, z, A.Z);
     }
-    if (g < gp) f_neg<P, 64>(Bk.Y, Bk.Y);       // bit k cleared: subtract B_k
-    J30 R;
-    bool same;
-    (void)j_add<P>(R, A, Bk, &same);            // never degenerate (see above)
-    j_copy(A, R);
-    lltab_store(tab, g, A);
+    llpre_store(tab, m, z);
+  }
+  // 3. Montgomery's trick over the non-base entries, backwards from m = 126
+  //    (127 is a base step): inv = (prod Z)^-1; Z_m^-1 = inv pre[m - 1],
+  //    inv *= Z_m; (x, y) = (X Z^-2, Y Z^-3). The next entry and prefix are
+  //    loaded one step ahead. No two base steps are adjacent below 127.
+  f_inv_sg<P>(inv, z);
+  J30 E;
+  uint32_t pre[9];
+  llraw_load(E, tab, ll_gray(kLLEnt - 1u));
+  llpre_load(pre, tab, kLLEnt - 2u);
+  uint32_t m = kLLEnt - 1u;
+#pragma unroll 1
+  for (;;) {
+    const uint32_t mn = ll_is_base(m - 1u) ? m - 2u : m - 1u;  // next non-base step
+    J30 En;
+    uint32_t pn[9];
+    if (mn >= 2u) {
+      llraw_load(En, tab, ll_gray(mn));
+      llpre_load(pn, tab, mn - 1u);
+    }
+    uint32_t zi[9], z2[9], z3[9];
+    f_mul<P>(zi, inv, pre);   // Z_m^-1
+    f_mul<P>(inv, inv, E.Z);  // (prod_{<m})^-1
+    f_sqr<P>(z2, zi);
+    f_mul<P>(z3, z2, zi);
+    f_mul<P>(E.X, E.X, z2);
+    f_mul<P>(E.Y, E.Y, z3);
+    llaff_store(tab, ll_gray(m), E.X, E.Y);
+    if (mn < 2u) break;
+    j_copy(E, En);
+    f_copy(pre, pn);
+    m = mn;
   }
 }
 
-// u2 Q from a Lim-Lee comb table (Horner over the 37 columns, top first).
+// u2 Q from an affine Lim-Lee comb table (Horner over the 37 columns, top first).
 template <class P>
 BH_HD void q_llcomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab) {
-  uint32_t k2[8];
+  uint32_t k2[8], one[9];
   ld8(k2, w.r, i, w.ns);
-  uint64_t sl[kLLTeeth];  // bits [37 s, 37 s + 37) of u2
+  f_const(one, P::r1);
+  uint64_t sl[kLLTeeth];  // bits [37 t, 37 t + 37) of u2
 #pragma unroll
   for (int t = 0; t < kLLTeeth; t++) {
     const int lo = kLLSpace * t, wd = lo >> 5, sh = lo & 31;
@@ -1143,18 +1285,18 @@ BH_HD void q_llcomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32
     sl[t] = x & ((1ull << kLLSpace) - 1ull);
   }
   a_inf = true;
-  f_const(A.X, P::r1);
-  f_const(A.Y, P::r1);
-  f_const(A.Z, P::r1);
+  f_copy(A.X, one);
+  f_copy(A.Y, one);
+  f_copy(A.Z, one);
 #pragma unroll 1
   for (int j = kLLSpace - 1; j >= 0; j--) {
     uint32_t b = 0;
 #pragma unroll
     for (int t = 0; t < kLLTeeth; t++) b |= (uint32_t)((sl[t] >> j) & 1ull) << t;
     j_dbl<P>(A, A);  // (while a_inf, A is a placeholder the next point replaces)
-    J30 T;
-    lltab_load(T, tab, b ? b : 1u);
-    j_acc<P>(A, a_inf, T, b == 0);
+    uint32_t tx[9], ty[9];
+    llaff_load(tx, ty, tab, b ? b : 1u);
+    j_acc_aff<P>(A, a_inf, tx, ty, one, b == 0);
   }
 }
 

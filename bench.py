@@ -59,8 +59,14 @@ G_COMB_BITS = 10
 G_WINDOWS = (257 + G_COMB_BITS - 1) // G_COMB_BITS
 LL_TABLES = os.environ.get("BH_LL", "1") != "0"
 FP_LADDER, FP_GPART = 3200, G_WINDOWS * 11
-FP_KTAB = 222 * 8 + 120 * 16 if LL_TABLES else 65 * 58
-FP_KEYCOMB = (36 * 8 + 37 * 16 if LL_TABLES else 65 * 16) + 23
+# Lim-Lee comb table (verify.h lltab_build): 222 doublings, B_1..B_6 made affine
+# (5 + 34 products), 120 Gray-walk mixed additions (8 M + 3 S) + 120 running
+# Z products, the backward pass (6 per entry), and two safegcd inversions
+# (~14k VALU instructions each, ~85 F_p-op equivalents at 169 per op); the key
+# comb is 36 doublings + 37 mixed additions against 65 full additions
+FP_INV_SG = 85
+FP_KTAB = (222 * 8 + 5 + 34 + 120 * 12 + 120 * 6 + 2 * FP_INV_SG) if LL_TABLES else 65 * 58
+FP_KEYCOMB = (36 * 8 + 37 * 11 if LL_TABLES else 65 * 16) + 23
 MACS_PER_VERIFY = FP_LADDER * MAC_PER_FP
 KERNELS = {"build_ladder_ms": "k_ktab_ladder", "keycomb_ms": "k_keycomb"}
 CONFIG5_TOTAL = 1 << 26

@@ -140,8 +140,11 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
       if (tab_of[r] == kNone) {
         tab_of[r] = (uint32_t)tables.size();
         tables.emplace_back(kKTabWords);
-        if (g_ll && g_wide == 1) lltab_build<P>(tables.back().data(), w, r);  // comb
-        else ktab_build<P>(tables.back().data(), w, r);  // the device's co-Z chain
+        if (g_ll && g_wide == 1) {  // comb: the device's two build lanes, one after the other
+          lltab_build<P>(tables.back().data(), w, r);
+        } else {
+          ktab_build<P>(tables.back().data(), w, r);  // the device's co-Z chain
+        }
       }
       ok = keycomb_any<P>(w, gtab, i, tables[tab_of[r]].data());
       combs++;

@@ -242,3 +242,19 @@ def test_two_lanes_with_registry_writes(L):
     _lib.check(L.bh_keys_count(0, 0, ctypes.byref(cnt)))
     assert cnt.value > 0
     _lib.check(L.bh_keys_clear(0, 0))
+
+
+def test_comb_and_window_tables_agree(L):
+    """A large batch (one lane per record) uses per-batch Lim-Lee comb tables
+    (verify.h lltab_build / q_llcomb); BH_LL=0 forces the 4-bit windowed
+    tables. Both give the expected bitmap and reasons, record for record."""
+    w = workload.generate(200_000, 8_000, 64, 16, seed=46)
+    bits1, r1, tm1 = dev_verify(L, w)
+    os.environ["BH_LL"] = "0"
+    try:
+        bits0, r0, tm0 = dev_verify(L, w)
+    finally:
+        del os.environ["BH_LL"]
+    assert tm1.n_keytables > 0 and tm1.n_keycomb > 0.9 * w.n * 15 / 16
+    for bits, r in ((bits1, r1), (bits0, r0)):
+        assert (r == w.reason).all() and (bits == w.expected_valid).all()
