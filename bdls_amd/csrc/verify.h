@@ -1089,7 +1089,10 @@ BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint3
 // it (the integers differ and stay below n). Registry tables and small
 // batches keep the windowed tables (their lanes split the windows; a comb's
 // doubling chain cannot be split).
-constexpr int kLLTeeth = 7, kLLSpace = 37;
+#ifndef BH_LL_T
+#define BH_LL_T 7  // teeth (experiments: 6 = 43-bit spacing, 63 entries)
+#endif
+constexpr int kLLTeeth = BH_LL_T, kLLSpace = (256 + kLLTeeth - 1) / kLLTeeth;
 constexpr uint32_t kLLEnt = (1u << kLLTeeth) - 1u;
 constexpr uint32_t kLLAff = 20;                 // words per affine entry
 constexpr uint32_t kLLRaw = 2560;               // raw Jacobian entries (28 words) while building
@@ -1275,13 +1278,13 @@ BH_HD void q_llcomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32
   uint32_t k2[8], one[9];
   ld8(k2, w.r, i, w.ns);
   f_const(one, P::r1);
-  uint64_t sl[kLLTeeth];  // bits [37 t, 37 t + 37) of u2
+  uint64_t sl[kLLTeeth];  // bits [37 t, 37 t + 37) of u2 (kLLSpace = 37)
 #pragma unroll
   for (int t = 0; t < kLLTeeth; t++) {
     const int lo = kLLSpace * t, wd = lo >> 5, sh = lo & 31;
     uint64_t x = (uint64_t)k2[wd] >> sh;
     if (wd + 1 < 8) x |= (uint64_t)k2[wd + 1] << (32 - sh);
-    if (wd + 2 < 8 && sh > 27) x |= (uint64_t)k2[wd + 2] << (64 - sh);
+    if (wd + 2 < 8 && sh + kLLSpace > 64) x |= (uint64_t)k2[wd + 2] << (64 - sh);
     sl[t] = x & ((1ull << kLLSpace) - 1ull);
   }
   a_inf = true;

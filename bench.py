@@ -688,6 +688,9 @@ def bench_throughput(a, rank, world, local):
         "hbm_resident": resident,
         "host_path": {"single_batch_ms": round(single_ms, 3), "batch_bytes": batch_bytes,
                       "h2d_gbps_pinned": round(h2d_gbps, 2),
+                      # the host path's own roofline: every batch crosses PCIe once
+                      "pcie_bound_verifies_per_s": round(world * n * h2d_gbps * 1e9 / batch_bytes, 1),
+                      "pcie_frac": round(value / (world * n * h2d_gbps * 1e9 / batch_bytes), 3),
                       "note": "value amortises the first batch's upload (pipeline fill) "
                               "over --steps batches"},
         "kernel_ms_per_step": {k: round(v / a.steps, 3) for k, v in kern.items()},
