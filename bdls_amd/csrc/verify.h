@@ -1090,7 +1090,7 @@ BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint3
 // batches keep the windowed tables (their lanes split the windows; a comb's
 // doubling chain cannot be split).
 #ifndef BH_LL_T
-#define BH_LL_T 7  // teeth (experiments: 6 = 43-bit spacing, 63 entries)
+#define BH_LL_T 6  // teeth: 6 x 43 bits, 63 entries (7 x 37: profiles/r03/v8)
 #endif
 constexpr int kLLTeeth = BH_LL_T, kLLSpace = (256 + kLLTeeth - 1) / kLLTeeth;
 constexpr uint32_t kLLEnt = (1u << kLLTeeth) - 1u;
@@ -1278,7 +1278,7 @@ BH_HD void q_llcomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32
   uint32_t k2[8], one[9];
   ld8(k2, w.r, i, w.ns);
   f_const(one, P::r1);
-  uint64_t sl[kLLTeeth];  // bits [37 t, 37 t + 37) of u2 (kLLSpace = 37)
+  uint64_t sl[kLLTeeth];  // bits [s t, s t + s) of u2, s = kLLSpace
 #pragma unroll
   for (int t = 0; t < kLLTeeth; t++) {
     const int lo = kLLSpace * t, wd = lo >> 5, sh = lo & 31;

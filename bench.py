@@ -59,14 +59,20 @@ G_COMB_BITS = 10
 G_WINDOWS = (257 + G_COMB_BITS - 1) // G_COMB_BITS
 LL_TABLES = os.environ.get("BH_LL", "1") != "0"
 FP_LADDER, FP_GPART = 3200, G_WINDOWS * 11
-# Lim-Lee comb table (verify.h lltab_build): 222 doublings, B_1..B_6 made affine
-# (5 + 34 products), 120 Gray-walk mixed additions (8 M + 3 S) + 120 running
-# Z products, the backward pass (6 per entry), and two safegcd inversions
-# (~14k VALU instructions each, ~85 F_p-op equivalents at 169 per op); the key
-# comb is 36 doublings + 37 mixed additions against 65 full additions
+# Lim-Lee comb, LL_T teeth spaced LL_S bits (verify.h BH_LL_T, 6 x 43): the
+# table (lltab_build) is (LL_T - 1) LL_S doublings, B_1..B_{T-1} made affine
+# (T - 2 + 4 (T - 1) + 2 (T - 2) products), the Gray walk's 2^T - 1 - T non-base
+# steps (mixed addition 8 M + 3 S + one running Z product), the backward pass
+# (6 per entry) and two safegcd inversions (~14k VALU instructions each, ~85
+# F_p-op equivalents at 169 per op); the key comb is LL_S - 1 doublings + LL_S
+# mixed additions against 65 full additions of the 4-bit windows
+LL_T = 6
+LL_S = -(-256 // LL_T)
 FP_INV_SG = 85
-FP_KTAB = (222 * 8 + 5 + 34 + 120 * 12 + 120 * 6 + 2 * FP_INV_SG) if LL_TABLES else 65 * 58
-FP_KEYCOMB = (36 * 8 + 37 * 11 if LL_TABLES else 65 * 16) + 23
+_LL_WALK = 2**LL_T - 1 - LL_T
+FP_KTAB = ((LL_T - 1) * LL_S * 8 + (LL_T - 2) + 4 * (LL_T - 1) + 2 * (LL_T - 2)
+           + _LL_WALK * 12 + _LL_WALK * 6 + 2 * FP_INV_SG) if LL_TABLES else 65 * 58
+FP_KEYCOMB = ((LL_S - 1) * 8 + LL_S * 11 if LL_TABLES else 65 * 16) + 23
 MACS_PER_VERIFY = FP_LADDER * MAC_PER_FP
 KERNELS = {"build_ladder_ms": "k_ktab_ladder", "keycomb_ms": "k_keycomb"}
 CONFIG5_TOTAL = 1 << 26

@@ -35,6 +35,8 @@ extern "C" void hs_set_wide(int L) { g_wide = L; }
 // batches; 0: the 4-bit windowed tables.
 static int g_ll = 0;
 extern "C" void hs_set_ll(int on) { g_ll = on; }
+// the comb's shape as built (teeth << 8 | spacing), for the crafted-scalar tests
+extern "C" uint32_t hs_ll_shape() { return ((uint32_t)kLLTeeth << 8) | (uint32_t)kLLSpace; }
 
 template <class P, int L>
 static bool wide_keycomb(const Work& w, const uint32_t* gtab, uint32_t i, const uint32_t* tab) {

@@ -10,7 +10,7 @@ import pytest
 
 from tests.conftest import ROOT, pack
 
-LIB = os.path.join(ROOT, "tests", "native", "build", "libhostsim.so")
+LIB = os.environ.get("HOSTSIM_LIB") or os.path.join(ROOT, "tests", "native", "build", "libhostsim.so")
 
 
 @pytest.fixture(scope="module")
@@ -228,13 +228,17 @@ def test_multi_device_shard_split(hs, n):
         assert ns.value == min(nd, (n + 63) // 64)
 
 
-# scalars at the Lim-Lee comb's edges (7 teeth, 37-bit spacing): a single
-# tooth, the top column empty or full, every column equal, the last tooth's
-# 34 bits, a lone column
-_LL_U2 = [2**36, 2**37, 2**74, 2**222, 2**255, 2**222 + 2**221, 2**37 - 1,
-          sum(2**(37 * t) for t in range(7)), sum(2**(37 * t + 36) for t in range(6)),
-          sum(2**(37 * t + 36) for t in range(6)) + 2**255, (2**37 - 1) << 185,
-          sum((2**37 - 1) << (37 * t) for t in range(6))]
+# scalars at the Lim-Lee comb's edges (t teeth spaced s bits: 7 x 37 as
+# shipped): a single tooth, the top column empty or full, every column equal,
+# the last tooth's partial width, a lone column
+def _ll_u2(t, s):
+    top = 256 - s * (t - 1)  # bits of the last tooth
+    return [2**(s - 1), 2**s, 2**(2 * s), 2**(s * (t - 1)), 2**255,
+            2**(s * (t - 1)) + 2**(s * (t - 1) - 1), 2**s - 1,
+            sum(2**(s * k) for k in range(t)), sum(2**(s * k + s - 1) for k in range(t - 1)),
+            sum(2**(s * k + s - 1) for k in range(t - 1)) + 2**255,
+            (2**s - 1) << (256 - top - s), sum((2**s - 1) << (s * k) for k in range(t - 1))]
+
 
 
 @pytest.mark.parametrize("fused", [False, True])
@@ -256,7 +260,8 @@ def test_hostsim_p256_crafted_u2_llcomb(hs):
     """The comb on crafted scalars (window edges and the comb's own: empty top
     column, single teeth, full columns): every signature verifies, every
     flipped-digest twin fails."""
-    recs = _p256_crafted_u2_records(_LL_U2)
+    sh = hs.hs_ll_shape()
+    recs = _p256_crafted_u2_records(_ll_u2(sh >> 8, sh & 0xFF))
     pub = np.frombuffer(b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big")
                                  for x, y, _, _ in recs), np.uint8)
     sigs, dgs = [t[2] for t in recs], [t[3] for t in recs]
