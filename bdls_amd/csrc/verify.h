@@ -1069,11 +1069,12 @@ BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint3
 
 // ---------------------------------------------------------------- per-key Lim-Lee comb
 // Per-batch key tables of LARGE batches (one lane per record, o.wide == 1;
-// round 3). A Lim-Lee comb with 7 teeth spaced 37 bits apart:
-//   T[b] = sum over the set bits i of b of 2^(37 i) Q,   b in [1, 128)
+// round 3). A Lim-Lee comb with t = 6 teeth spaced s = 43 bits apart
+// (BH_LL_T; 7 x 37 measured slower overall):
+//   T[b] = sum over the set bits i of b of 2^(s i) Q,   b in [1, 2^t)
 // stored AFFINE (x, y: 20 words at word 20 (b - 1)), and
-//   u2 Q = sum_{j < 37} 2^j T[b_j],  b_j = bits j, j + 37, ..., j + 222 of u2,
-// by Horner: 36 doublings + 37 mixed additions per record instead of the 65
+//   u2 Q = sum_{j < s} 2^j T[b_j],  b_j = bits j, j + s, ..., j + (t - 1) s of u2,
+// by Horner: s - 1 doublings + s mixed additions per record instead of the 65
 // full additions of the 4-bit windows (a doubling, 3M + 5S, and a mixed
 // addition, 8M + 3S, issue ~1,440 and ~2,100 VALU instructions against ~2,950
 // for a full addition). Build: one lane per table (one build wave per SIMD,
@@ -1082,10 +1083,9 @@ BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint3
 // B_k = 2^(37 k) Q, made affine by one inversion; a Gray-code walk then reaches
 // every other T[b] by one mixed addition of +-B_k, storing raw Jacobian entries
 // and the running product of their Z; one more inversion and a backward pass
-// (Montgomery's trick) make them affine. About 4,100 F_p ops per table (the
-// Jacobian comb of round 3's first cut: 3,696), 127 x 80 B = 10 KB, a
-// sixth of the windowed table's bytes. No walk step can degenerate: every T[b]
-// is a sum of distinct 2^(37 i) Q with 37 i <= 222, never +-B_k for k outside
+// (Montgomery's trick) make them affine. About 2,950 F_p ops per table at
+// 6 x 43, 63 x 80 B = 5 KB. No walk step can degenerate: every T[b]
+// is a sum of distinct 2^(s i) Q with s i <= 215, never +-B_k for k outside
 // it (the integers differ and stay below n). Registry tables and small
 // batches keep the windowed tables (their lanes split the windows; a comb's
 // doubling chain cannot be split).
