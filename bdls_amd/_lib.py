@@ -31,7 +31,7 @@ EXPORTS = (
     "bh_verify_submit", "bh_verify_wait", "bh_host_alloc", "bh_host_free", "bh_csp_stats",
     "bh_fabric_block_preverify", "bh_verify_x509", "bh_signature_sets_verify",
     "bh_envelopes_preverify", "bh_block_signatures_preverify",
-    "bh_block_signatures_preverify_bft", "bh_fabric_block_preverify_refs",
+    "bh_block_signatures_preverify_bft", "bh_fabric_block_preverify_refs", "bh_device_stats",
 )
 KEY_FULL = 255  # bh_keys_register status: registry full
 
@@ -178,6 +178,11 @@ def lib() -> ctypes.CDLL:
         L.bh_verify_x509.restype = i32
         L.bh_csp_stats.argtypes = [vp]
         L.bh_csp_stats.restype = i32
+        try:  # (an A/B run may load a library built before this entry point)
+            L.bh_device_stats.argtypes = [vp]
+            L.bh_device_stats.restype = i32
+        except AttributeError:
+            pass
         L.bh_parse_der_sig.argtypes = [vp, sz, vp, vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         L.bh_parse_der_sig.restype = i32
         L.bh_verify_bdls.argtypes = [i32, ctypes.POINTER(BhBdlsBatch), sz, vp, vp]
@@ -302,3 +307,12 @@ class DeviceArray:
             self.free()
         except Exception:  # noqa: BLE001 (interpreter shutdown)
             pass
+
+
+def device_stats() -> tuple[int, int]:
+    """(device batches launched, records they carried) since bh_init, over
+    every entry point (bh_device_stats)."""
+    import numpy as _np
+    out = _np.zeros(2, _np.uint64)
+    check(lib().bh_device_stats(out.ctypes.data))
+    return int(out[0]), int(out[1])

@@ -48,6 +48,9 @@ hipError_t launch_register(int curve, const uint8_t* pub, const Work& w, const P
 namespace {
 
 thread_local std::string g_err;
+// Device batches launched (one per run_dev call, one per latency-path batch)
+// and the records they carried, over the process (bh_device_stats).
+std::atomic<uint64_t> g_dev_batches{0}, g_dev_records{0};
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -514,6 +517,8 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
     if (rc) return rc;
   }
   const bool l1 = lane == 1;
+  g_dev_batches.fetch_add(1, std::memory_order_relaxed);
+  g_dev_records.fetch_add(n, std::memory_order_relaxed);
   if (lane < 0) {
     HIPCHK(wait_lanes(d, s));
   } else if (!l1) {
@@ -863,25 +868,42 @@ int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, si
     if (ml) std::memcpy(h + o_msg + mp, b->msg + b->msg_off[lo + i], ml);
     mp += ml;
   }
-  hipStream_t s = d.stream;  // lane 0: its workspace, and registry writes are ordered on it
-  if (d.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.done, 0));
+  // Small batches alternate between the two compute lanes like host batches:
+  // a latency batch occupies a few CUs for ~50-90 us (its records' prep and
+  // inverses are one serial lane each), so the coalescer's two batches in
+  // flight run side by side instead of one after the other. Each lane has its
+  // own workspace; both wait for the last registry write.
+  const bool l1 = lanes() > 1 && (d.next_lane++ % lanes()) == 1;
+  hipStream_t s = l1 ? d.l1.stream : d.stream;
+  if (l1) {
+    if (d.l1.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.l1.done, 0));
+  } else if (d.done_recorded) {
+    HIPCHK(hipStreamWaitEvent(s, d.done, 0));
+  }
   if (d.reg_written_recorded) HIPCHK(hipStreamWaitEvent(s, d.reg_written, 0));
   char* dv = (char*)sl.stage.p;
   HIPCHK(hipMemcpyAsync(dv, h, total, hipMemcpyHostToDevice, s));
   bh::Work w;
   bh::Plan pl;
-  if ((rc = carve_work(d, m, &w, &pl))) return rc;
+  if ((rc = carve_work(d, m, &w, &pl, false, l1 ? &d.l1.ws : nullptr))) return rc;
   const bh::BatchIn in{(const uint8_t*)(dv + o_pub), (const uint8_t*)(dv + o_sig),
                        (const uint64_t*)(dv + o_soff), (const uint32_t*)(dv + o_slen),
                        (const uint8_t*)(dv + o_msg), (const uint64_t*)(dv + o_moff),
                        (const uint32_t*)(dv + o_mlen), flags};
   const uint32_t small_block = env_block("BH_SMALL_BLOCK", 64);
+  g_dev_batches.fetch_add(1, std::memory_order_relaxed);
+  g_dev_records.fetch_add(m, std::memory_order_relaxed);
   HIPCHK(bh::launch_small(curve, in, w, d.reg[curve].g, d.gtab[curve], (uint32_t)m,
                           (uint8_t*)sl.out.p, s, small_block));
   HIPCHK(hipMemcpyAsync(sl.host_out.p, sl.out.p, m, hipMemcpyDeviceToHost, s));
   HIPCHK(hipEventRecord(sl.done, s));
-  HIPCHK(hipEventRecord(d.done, s));
-  d.done_recorded = true;
+  if (l1) {
+    HIPCHK(hipEventRecord(d.l1.done, s));
+    d.l1.done_recorded = true;
+  } else {
+    HIPCHK(hipEventRecord(d.done, s));
+    d.done_recorded = true;
+  }
   sl.owner = j;
   sl.owner_part = j->parts.size();
   Part part{&d, k, lo, m, false};
@@ -895,6 +917,19 @@ int wait_job(bh_job* j) {
   std::string err = j->err;
   for (size_t k = 0; k < j->parts.size(); k++) {
     Dev& d = *j->parts[k].d;
+    // wait for the part's pass WITHOUT the device lock, so other threads keep
+    // enqueueing meanwhile (the coalescer's submitter while its completer
+    // waits); if another enqueue collected this part first and re-recorded
+    // the slot's event, this only waits longer, and finish_part sees it done
+    hipEvent_t ev = nullptr;
+    {
+      std::lock_guard<std::mutex> g(d.mu);
+      if (!j->parts[k].done) ev = d.slot[j->parts[k].slot].done;
+    }
+    if (ev) {
+      HIPCHK(hipSetDevice(d.id));
+      (void)hipEventSynchronize(ev);  // errors are reported by finish_part
+    }
     std::lock_guard<std::mutex> g(d.mu);
     int r = finish_part(j, k);
     if (r && rc == BH_OK) {
@@ -1071,15 +1106,15 @@ struct CspBatch {
 
 struct Coalescer {
   std::mutex mu;
-  std::condition_variable cv_work, cv_done;
+  std::condition_variable cv_work, cv_done, cv_inflight;
   std::unique_ptr<CspBatch> filling{new CspBatch()};
   std::deque<std::unique_ptr<CspBatch>> inflight;
   std::vector<std::unique_ptr<CspBatch>> spare;
-  std::thread th;
+  std::thread th, th_done;
   bool running = false, stop = false;
   uint64_t n_req = 0, n_batch = 0, max_batch = 0;
   size_t cap = 65536;      // records per batch at most
-  size_t max_inflight = 2; // = pipeline slots per device
+  size_t max_inflight = 2; // < pipeline slots per device (kSlots)
   long linger_us = 0;
   // Keys are registered in the device key registry on their register_after-th
   // sighting (0 = never): the device-side twin of the MSP identity cache, so a
@@ -1087,7 +1122,9 @@ struct Coalescer {
   // doublings) instead of the ladder. The registration pass is queued before
   // the batch that sees the key, which then already uses the table; a full
   // registry leaves new keys on the ladder (results are the same either way).
-  int register_after = 1;
+  // Default 2: a one-shot key never costs a table build nor a
+  // registry slot that a long-lived identity would use.
+  int register_after = 2;
   std::unordered_map<std::string, uint8_t> sightings;  // 255 = registered (or tried)
 
   void keys_to_register(const CspBatch& b, std::vector<uint8_t>* keys) {
@@ -1121,62 +1158,78 @@ struct Coalescer {
 
   std::vector<uint8_t> new_keys;
 
+  // Submitter: takes the filling batch whenever fewer than max_inflight are in
+  // flight -- it never waits for a pass, so callers arriving while batch k
+  // runs are submitted as batch k + 1 at once (its upload and launch overlap
+  // batch k's pass) instead of after batch k completes.
   void run() {
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      cv_work.wait(lk, [&] { return stop || !filling->reqs.empty() || !inflight.empty(); });
-      if (stop && filling->reqs.empty() && inflight.empty()) return;
-      if (!filling->reqs.empty() && inflight.size() < max_inflight) {
-        if (inflight.empty() && linger_us > 0 && filling->reqs.size() < cap && !stop) {
-          const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(linger_us);
-          cv_work.wait_until(lk, until, [&] { return stop || filling->reqs.size() >= cap; });
-        }
-        std::unique_ptr<CspBatch> b = std::move(filling);
-        if (spare.empty()) {
-          filling.reset(new CspBatch());
-        } else {
-          filling = std::move(spare.back());
-          spare.pop_back();
-        }
-        filling->clear();
-        cv_done.notify_all();  // callers waiting for room in a full batch
-        const size_t n = b->reqs.size();
-        n_req += n;
-        n_batch++;
-        max_batch = std::max<uint64_t>(max_batch, n);
-        lk.unlock();
-        b->bitmap.assign((n + 7) / 8, 0);
-        b->reason.assign(n, 0);
-        b->b = bh_batch{b->pub.data(), b->sig.data(), b->sig_off.data(), b->sig_len.data(),
-                        b->dg.data(), b->dg_off.data(), b->dg_len.data()};
-        keys_to_register(*b, &new_keys);
-        if (!new_keys.empty()) register_async(BH_CURVE_P256, new_keys.data(), new_keys.size() / 64);
-        int rc = submit_job(BH_CURVE_P256, &b->b, n, 0u, b->bitmap.data(), b->reason.data(),
-                            &b->job);
-        const std::string err = rc ? g_err : std::string();
-        lk.lock();
-        if (rc) {
-          complete(*b, rc, err);
-          spare.push_back(std::move(b));
-          cv_done.notify_all();
-        } else {
-          inflight.push_back(std::move(b));
-        }
-        continue;
+      cv_work.wait(lk, [&] {
+        return (stop && filling->reqs.empty()) ||
+               (!filling->reqs.empty() && inflight.size() < max_inflight);
+      });
+      if (stop && filling->reqs.empty()) return;
+      if (inflight.empty() && linger_us > 0 && filling->reqs.size() < cap && !stop) {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(linger_us);
+        cv_work.wait_until(lk, until, [&] { return stop || filling->reqs.size() >= cap; });
       }
-      if (!inflight.empty()) {
-        std::unique_ptr<CspBatch> b = std::move(inflight.front());
-        inflight.pop_front();
-        lk.unlock();
-        int rc = wait_job(b->job);
-        const std::string err = rc ? g_err : std::string();
-        lk.lock();
+      std::unique_ptr<CspBatch> b = std::move(filling);
+      if (spare.empty()) {
+        filling.reset(new CspBatch());
+      } else {
+        filling = std::move(spare.back());
+        spare.pop_back();
+      }
+      filling->clear();
+      cv_done.notify_all();  // callers waiting for room in a full batch
+      const size_t n = b->reqs.size();
+      n_req += n;
+      n_batch++;
+      max_batch = std::max<uint64_t>(max_batch, n);
+      lk.unlock();
+      b->bitmap.assign((n + 7) / 8, 0);
+      b->reason.assign(n, 0);
+      b->b = bh_batch{b->pub.data(), b->sig.data(), b->sig_off.data(), b->sig_len.data(),
+                      b->dg.data(), b->dg_off.data(), b->dg_len.data()};
+      keys_to_register(*b, &new_keys);
+      if (!new_keys.empty()) register_async(BH_CURVE_P256, new_keys.data(), new_keys.size() / 64);
+      int rc = submit_job(BH_CURVE_P256, &b->b, n, 0u, b->bitmap.data(), b->reason.data(),
+                          &b->job);
+      const std::string err = rc ? g_err : std::string();
+      lk.lock();
+      if (rc) {
         complete(*b, rc, err);
         spare.push_back(std::move(b));
         cv_done.notify_all();
+      } else {
+        inflight.push_back(std::move(b));
+        cv_inflight.notify_one();
       }
     }
   }
+
+  // Completer: waits for the oldest batch in flight, hands its results out and
+  // frees its place in the pipeline.
+  void run_done() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv_inflight.wait(lk, [&] { return !inflight.empty() || (stop && !th_submit_alive); });
+      if (inflight.empty()) return;
+      CspBatch* b = inflight.front().get();
+      lk.unlock();
+      int rc = wait_job(b->job);
+      const std::string err = rc ? g_err : std::string();
+      lk.lock();
+      std::unique_ptr<CspBatch> done = std::move(inflight.front());
+      inflight.pop_front();
+      complete(*done, rc, err);
+      spare.push_back(std::move(done));
+      cv_done.notify_all();
+      cv_work.notify_one();  // room in the pipeline
+    }
+  }
+  bool th_submit_alive = false;
 
   int verify(const uint8_t* pub, const uint8_t* sig, size_t sl, const uint8_t* dg, size_t dl,
              int* valid, int* reason) {
@@ -1186,9 +1239,16 @@ struct Coalescer {
       if (!running) {
         stop = false;
         running = true;
-        th = std::thread([this] { run(); });
+        th_submit_alive = true;
+        th = std::thread([this] {
+          run();
+          std::lock_guard<std::mutex> g(mu);
+          th_submit_alive = false;
+          cv_inflight.notify_all();
+        });
+        th_done = std::thread([this] { run_done(); });
       }
-      // a full batch (cap records) waits until the flusher takes it
+      // a full batch (cap records) waits until the submitter takes it
       cv_done.wait(lk, [&] { return filling->reqs.size() < cap; });
       CspBatch& b = *filling;
       b.pub.insert(b.pub.end(), pub, pub + 64);
@@ -1216,6 +1276,8 @@ struct Coalescer {
     }
     cv_work.notify_all();
     th.join();
+    cv_inflight.notify_all();
+    th_done.join();
     std::lock_guard<std::mutex> lk(mu);
     running = false;
     stop = false;
@@ -1382,6 +1444,13 @@ int bh_csp_stats(uint64_t out[3]) {
   out[0] = c.n_req;
   out[1] = c.n_batch;
   out[2] = c.max_batch;
+  return BH_OK;
+}
+
+int bh_device_stats(uint64_t out[2]) {
+  if (!out) return fail(BH_E_INVALID, "null argument");
+  out[0] = g_dev_batches.load(std::memory_order_relaxed);
+  out[1] = g_dev_records.load(std::memory_order_relaxed);
   return BH_OK;
 }
 

@@ -16,6 +16,8 @@
 // value, limb-major with stride `ns`), so every per-limb access by a wave is one
 // coalesced 256-byte transaction.
 #pragma once
+#include <type_traits>
+
 #include "blake2b.h"
 #include "der.h"
 #include "fe.h"
@@ -1067,38 +1069,49 @@ BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint3
   }
 }
 
-// ---------------------------------------------------------------- per-key Lim-Lee comb
-// Per-batch key tables of LARGE batches (one lane per record, o.wide == 1;
-// round 3). A Lim-Lee comb with t = 6 teeth spaced s = 43 bits apart
-// (BH_LL_T; 7 x 37 measured slower overall):
-//   T[b] = sum over the set bits i of b of 2^(s i) Q,   b in [1, 2^t)
-// stored AFFINE (x, y: 20 words at word 20 (b - 1)), and
-//   u2 Q = sum_{j < s} 2^j T[b_j],  b_j = bits j, j + s, ..., j + (t - 1) s of u2,
-// by Horner: s - 1 doublings + s mixed additions per record instead of the 65
-// full additions of the 4-bit windows (a doubling, 3M + 5S, and a mixed
-// addition, 8M + 3S, issue ~1,440 and ~2,100 VALU instructions against ~2,950
-// for a full addition). Build: one lane per table (one build wave per SIMD,
-// beside the u1 G waves: the kernel runs at 2 waves per SIMD, so more build
-// lanes per table only take the slots those waves fill). 222 doublings give
-// B_k = 2^(37 k) Q, made affine by one inversion; a Gray-code walk then reaches
-// every other T[b] by one mixed addition of +-B_k, storing raw Jacobian entries
-// and the running product of their Z; one more inversion and a backward pass
-// (Montgomery's trick) make them affine. About 2,950 F_p ops per table at
-// 6 x 43, 63 x 80 B = 5 KB. No walk step can degenerate: every T[b]
-// is a sum of distinct 2^(s i) Q with s i <= 215, never +-B_k for k outside
-// it (the integers differ and stay below n). Registry tables and small
-// batches keep the windowed tables (their lanes split the windows; a comb's
-// doubling chain cannot be split).
+// ---------------------------------------------------------------- per-key signed Lim-Lee comb
+// Per-batch key tables of LARGE batches (one lane per record, o.wide == 1).
+// A SIGNED Lim-Lee comb (round 4; round 3 had the unsigned 6 x 43 comb): t =
+// BH_LL_T teeth spaced s = ceil(257 / t) bits. For odd k < 2^257 put
+//   c = (k >> 1) | 2^(t s - 1),   d_(i,j) = 2 c_(s i + j) - 1 in {-1, +1};
+// then k = sum_(j < s) 2^j V_j with V_j = sum_(i < t) d_(i,j) 2^(s i): every
+// column is a nonzero signed sum (sum 2^(s i + j) (2 c - 1) = 2 c - 2^(t s) + 1
+// = k). With B_i = 2^(s i) Q the table holds the 2^(t-1) points
+//   E[m] = B_(t-1) + sum_(i < t-1) (2 m_i - 1) B_i,
+// and V_j Q = +E[m_j] when column j's top tooth is set, else -E[~m_j] (m_j =
+// the column's lower t - 1 bits). u2 Q = k Q with k = u2 (u2 odd) or u2 + n
+// (u2 even; n Q = 0), by Horner from the top column, whose top bit is the set
+// bit t s - 1 (so it is +E): s - 1 doublings + s - 1 mixed additions per record
+// and no empty columns -- at t = 7 (s = 37) 36 + 36 instead of the unsigned
+// 6 x 43 comb's 42 + 43 with a zero-column select, for a table of the same 64
+// entries.
+// Build, one lane per table (one build wave per SIMD beside the u1 G waves):
+// (t - 1) s doublings give D_i = 2 B_i and B_(i+1) = 2^(s-1) D_i; those
+// 2 (t - 1) points are made affine with one inversion (Montgomery's trick);
+// E[0] = B_(t-1) - sum_(i < t-1) B_i (t - 1 mixed additions); a Gray-code walk
+// reaches every other E[g] by one mixed addition of +-D_i (flipping digit i
+// from -1 to +1 adds 2 B_i), storing raw Jacobian entries and the running
+// product of their Z; one more inversion and a backward pass make them affine.
+// No build step can degenerate: every scalar involved lies in (0, n / 2) and
+// the walk's partial sums e_m = 2^(s(t-1)) +- ... exceed every d_i = 2^(s i+1)
+// with e_m + d_i < n. The Horner additions keep explicit degenerate handling
+// (A = +-V_j only for crafted scalars), as a branch the lanes skip together.
+// Registry tables and small batches keep the windowed tables (their lanes
+// split the windows; a comb's doubling chain cannot be split).
 #ifndef BH_LL_T
-#define BH_LL_T 6  // teeth: 6 x 43 bits, 63 entries (7 x 37: profiles/r03/v8)
+#define BH_LL_T 7  // teeth: 7 x 37 bits, 64 entries (signed)
 #endif
-constexpr int kLLTeeth = BH_LL_T, kLLSpace = (256 + kLLTeeth - 1) / kLLTeeth;
-constexpr uint32_t kLLEnt = (1u << kLLTeeth) - 1u;
-constexpr uint32_t kLLAff = 20;                 // words per affine entry
-constexpr uint32_t kLLRaw = 2560;               // raw Jacobian entries (28 words) while building
-constexpr uint32_t kLLPre = kLLRaw + 28u * 128u; // running Z products (12 words per step)
-static_assert(kLLTeeth * kLLSpace >= 256 && kLLAff * kLLEnt <= kLLRaw &&
-                  kLLPre + 12u * 128u <= kKTabWords && kLLPre % 4 == 0, "comb table layout");
+constexpr int kLLTeeth = BH_LL_T, kLLSpace = (257 + kLLTeeth - 1) / kLLTeeth;
+constexpr int kLLTS = kLLTeeth * kLLSpace;        // >= 257: c < 2^(t s)
+constexpr uint32_t kLLEnt = 1u << (kLLTeeth - 1);  // entries E[0 .. 2^(t-1))
+constexpr uint32_t kLLAff = 20;                    // words per affine point
+constexpr uint32_t kLLAux = kLLEnt;                // affine B_0..B_(t-1), D_0..D_(t-2)
+constexpr uint32_t kLLChain = 2u * (kLLTeeth - 1); // Jacobian D_i / B_(i+1) of the chain
+constexpr uint32_t kLLRaw = ((kLLAux + 2u * kLLTeeth - 1u) * kLLAff + 3u) & ~3u;
+constexpr uint32_t kLLPre = kLLRaw + 28u * (kLLEnt + kLLChain);  // running Z products
+static_assert(kLLTS >= 257 && kLLTS <= 288 && kLLSpace < 64 && kLLTeeth >= 2 &&
+                  kLLPre + 12u * kLLEnt <= kKTabWords && kLLChain <= kLLEnt,
+              "comb table layout");
 
 BH_HD void llraw_store(uint32_t* tab, uint32_t b, const J30& P) { ktab_store(tab + kLLRaw, 0, b, P); }
 BH_HD void llraw_load(J30& P, const uint32_t* tab, uint32_t b) { ktab_load(P, tab + kLLRaw, 0, b); }
@@ -1118,8 +1131,9 @@ BH_HD void llpre_load(uint32_t z[9], const uint32_t* tab, uint32_t m) {
   z[8] = c.x;
 }
 
+// affine point slot b (entries E[b], b < kLLEnt; then the aux points)
 BH_HD void llaff_store(uint32_t* tab, uint32_t b, const uint32_t x[9], const uint32_t y[9]) {
-  W4* d = reinterpret_cast<W4*>(tab + (size_t)(b - 1) * kLLAff);
+  W4* d = reinterpret_cast<W4*>(tab + (size_t)b * kLLAff);
   d[0] = W4{x[0], x[1], x[2], x[3]};
   d[1] = W4{x[4], x[5], x[6], x[7]};
   d[2] = W4{x[8], y[0], y[1], y[2]};
@@ -1128,7 +1142,7 @@ BH_HD void llaff_store(uint32_t* tab, uint32_t b, const uint32_t x[9], const uin
 }
 
 BH_HD void llaff_load(uint32_t x[9], uint32_t y[9], const uint32_t* tab, uint32_t b) {
-  const W4* s = reinterpret_cast<const W4*>(tab + (size_t)(b - 1) * kLLAff);
+  const W4* s = reinterpret_cast<const W4*>(tab + (size_t)b * kLLAff);
   const W4 a = s[0], c = s[1], d = s[2], e = s[3], f = s[4];
   x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
   x[4] = c.x; x[5] = c.y; x[6] = c.z; x[7] = c.w;
@@ -1153,153 +1167,208 @@ BH_HD void f_inv_sg(uint32_t r[9], const uint32_t a[9]) {
   f_mul<P>(r, c, r3);
 }
 
-// Walk position m (1..127) -> table index gray(m); the base points B_k sit at
-// m = 2^(k+1) - 1 (gray(m) = 2^k).
-BH_HD uint32_t ll_gray(uint32_t m) { return m ^ (m >> 1); }
-BH_HD bool ll_is_base(uint32_t m) { return (m & (m + 1u)) == 0u; }
-// the affine point step m reads: B_k itself at a base step, else the B_k it adds
-BH_HD uint32_t ll_walk_src(uint32_t m) {
-  return ll_is_base(m) ? ll_gray(m) : 1u << __builtin_ctz(m);
+// (X, Y, Z) -> affine (X / Z^2, Y / Z^3) given zi = Z^-1
+template <class P>
+BH_HD void ll_to_affine(uint32_t x[9], uint32_t y[9], const J30& E, const uint32_t zi[9]) {
+  uint32_t z2[9], z3[9];
+  f_sqr<P>(z2, zi);
+  f_mul<P>(z3, z2, zi);
+  f_mul<P>(x, E.X, z2);
+  f_mul<P>(y, E.Y, z3);
 }
+
+// Walk position m (0..2^(t-1) - 1) -> entry gray(m); step m flips digit ctz(m).
+BH_HD uint32_t ll_gray(uint32_t m) { return m ^ (m >> 1); }
 
 template <class P>
 BH_HD void lltab_build(uint32_t* tab, const Work& w, uint32_t rec) {
   uint32_t one[9];
   f_const(one, P::r1);
-  // 1. B_k = 2^(37 k) Q (222 doublings; raw Jacobian copies of B_1..B_6 and
-  //    the running product of their Z), then all six made affine with one
-  //    inversion (Montgomery's trick) and written to their final slots T[2^k]
+  // 1. The doubling chain: chain point 2i = D_i = 2 B_i, 2i + 1 = B_(i+1);
+  //    raw Jacobian copies and the running product of their Z, then all made
+  //    affine with one inversion. B_0 = Q is affine already.
   J30 B;
   ld9(B.X, w.qx, rec, w.ns);
   ld9(B.Y, w.qy, rec, w.ns);
-  llaff_store(tab, 1, B.X, B.Y);
+  llaff_store(tab, kLLAux, B.X, B.Y);
   f_copy(B.Z, one);
   uint32_t z[9];
-  for (uint32_t k = 1; k < (uint32_t)kLLTeeth; k++) {
 #pragma unroll 1
-    for (int d = 0; d < kLLSpace; d++) j_dbl<P>(B, B);
-    llraw_store(tab, 1u << k, B);
-    if (k == 1) f_copy(z, B.Z);
+  for (uint32_t i = 0; i + 1 < (uint32_t)kLLTeeth; i++) {
+    j_dbl<P>(B, B);
+    llraw_store(tab, kLLEnt + 2u * i, B);
+    if (i == 0) f_copy(z, B.Z);
     else f_mul<P>(z, z, B.Z);
-    llpre_store(tab, k, z);  // prod_{1 <= i <= k} Z_i (slots reused below)
+    llpre_store(tab, 2u * i, z);
+#pragma unroll 1
+    for (int d = 1; d < kLLSpace; d++) j_dbl<P>(B, B);
+    llraw_store(tab, kLLEnt + 2u * i + 1u, B);
+    f_mul<P>(z, z, B.Z);
+    llpre_store(tab, 2u * i + 1u, z);
   }
   uint32_t inv[9];
   f_inv_sg<P>(inv, z);
 #pragma unroll 1
-  for (uint32_t k = kLLTeeth - 1; k >= 1; k--) {
+  for (uint32_t c = kLLChain; c-- > 0;) {
     J30 E;
-    llraw_load(E, tab, 1u << k);
-    uint32_t zi[9], z2[9], z3[9];
-    if (k > 1) {
+    llraw_load(E, tab, kLLEnt + c);
+    uint32_t zi[9], x[9], y[9];
+    if (c > 0) {
       uint32_t pre[9];
-      llpre_load(pre, tab, k - 1);
+      llpre_load(pre, tab, c - 1u);
       f_mul<P>(zi, inv, pre);
       f_mul<P>(inv, inv, E.Z);
     } else {
       f_copy(zi, inv);
     }
-    f_sqr<P>(z2, zi);
-    f_mul<P>(z3, z2, zi);
-    f_mul<P>(E.X, E.X, z2);
-    f_mul<P>(E.Y, E.Y, z3);
-    llaff_store(tab, 1u << k, E.X, E.Y);
+    ll_to_affine<P>(x, y, E, zi);
+    // D_i -> aux slot t + i; B_(i+1) -> aux slot i + 1
+    llaff_store(tab, (c & 1u) ? kLLAux + (c >> 1) + 1u : kLLAux + kLLTeeth + (c >> 1), x, y);
   }
-  // 2. The Gray walk m = 1..127: a base step restarts from B_k (affine, Z = 1);
-  //    every other step adds or subtracts one B_k (mixed addition) and stores
-  //    the raw Jacobian entry. pre[m] = product of the Z of the non-base
-  //    entries up to m (pre[1] = 1). The next step's point is loaded one step
-  //    ahead, off the dependency chain.
+  // 2. E[0] = B_(t-1) - B_0 - ... - B_(t-2), then the Gray walk: step m adds
+  //    +-D_i (i = ctz(m); + when digit i of gray(m) is set). Raw entries at
+  //    their final index; pre[m] = prod of the Z of entries 0..m. The next
+  //    step's point is loaded one step ahead, off the dependency chain.
   J30 A;
+  llaff_load(A.X, A.Y, tab, kLLAux + kLLTeeth - 1u);
   f_copy(A.Z, one);
-  f_copy(z, one);
-  llpre_store(tab, 1, z);
-  uint32_t nx[9], ny[9];
-  llaff_load(A.X, A.Y, tab, 1);  // m = 1: T[1] = Q
-  llaff_load(nx, ny, tab, ll_walk_src(2));
+  bool same;
 #pragma unroll 1
-  for (uint32_t m = 2; m <= kLLEnt; m++) {
+  for (uint32_t i = 0; i + 1 < (uint32_t)kLLTeeth; i++) {
     uint32_t bx[9], by[9];
-    f_copy(bx, nx);
-    f_copy(by, ny);
-    if (m < kLLEnt) llaff_load(nx, ny, tab, ll_walk_src(m + 1));
-    if (ll_is_base(m)) {
-      f_copy(A.X, bx);
-      f_copy(A.Y, by);
-      f_copy(A.Z, one);
-    } else {
-      const uint32_t g = ll_gray(m);
-      if (g < ll_gray(m - 1)) f_neg<P, 64>(by, by);  // bit cleared: subtract B_k
-      J30 R;
-      bool same;
-      (void)j_madd<P>(R, A, bx, by, &same);  // never degenerate (see above)
-      j_copy(A, R);
-      llraw_store(tab, g, A);
-      f_mul<P>(z, z, A.Z);
-    }
+    llaff_load(bx, by, tab, kLLAux + i);
+    f_neg<P, 64>(by, by);
+    (void)j_madd<P>(A, A, bx, by, &same);  // never degenerate (see above)
+  }
+  llraw_store(tab, 0, A);
+  f_copy(z, A.Z);
+  llpre_store(tab, 0, z);
+  uint32_t nx[9], ny[9];
+  llaff_load(nx, ny, tab, kLLAux + kLLTeeth);  // D_0 for m = 1
+#pragma unroll 1
+  for (uint32_t m = 1; m < kLLEnt; m++) {
+    uint32_t dx[9], dy[9];
+    f_copy(dx, nx);
+    f_copy(dy, ny);
+    if (m + 1u < kLLEnt) llaff_load(nx, ny, tab, kLLAux + kLLTeeth + __builtin_ctz(m + 1u));
+    const uint32_t g = ll_gray(m);
+    if (!((g >> __builtin_ctz(m)) & 1u)) f_neg<P, 64>(dy, dy);  // digit back to -1
+    (void)j_madd<P>(A, A, dx, dy, &same);                        // never degenerate
+    llraw_store(tab, g, A);
+    f_mul<P>(z, z, A.Z);
     llpre_store(tab, m, z);
   }
-  // 3. Montgomery's trick over the non-base entries, backwards from m = 126
-  //    (127 is a base step): inv = (prod Z)^-1; Z_m^-1 = inv pre[m - 1],
-  //    inv *= Z_m; (x, y) = (X Z^-2, Y Z^-3). The next entry and prefix are
-  //    loaded one step ahead. No two base steps are adjacent below 127.
+  // 3. Montgomery's trick backwards over m = 2^(t-1) - 1 .. 0: inv = (prod Z)^-1;
+  //    Z_m^-1 = inv pre[m - 1], inv *= Z_m. The next entry and prefix are
+  //    loaded one step ahead.
   f_inv_sg<P>(inv, z);
   J30 E;
   uint32_t pre[9];
   llraw_load(E, tab, ll_gray(kLLEnt - 1u));
   llpre_load(pre, tab, kLLEnt - 2u);
-  uint32_t m = kLLEnt - 1u;
 #pragma unroll 1
-  for (;;) {
-    const uint32_t mn = ll_is_base(m - 1u) ? m - 2u : m - 1u;  // next non-base step
+  for (uint32_t m = kLLEnt - 1u;; m--) {
     J30 En;
     uint32_t pn[9];
-    if (mn >= 2u) {
-      llraw_load(En, tab, ll_gray(mn));
-      llpre_load(pn, tab, mn - 1u);
+    if (m >= 2u) {
+      llraw_load(En, tab, ll_gray(m - 1u));
+      llpre_load(pn, tab, m - 2u);
+    } else if (m == 1u) {
+      llraw_load(En, tab, 0);
     }
-    uint32_t zi[9], z2[9], z3[9];
-    f_mul<P>(zi, inv, pre);   // Z_m^-1
-    f_mul<P>(inv, inv, E.Z);  // (prod_{<m})^-1
-    f_sqr<P>(z2, zi);
-    f_mul<P>(z3, z2, zi);
-    f_mul<P>(E.X, E.X, z2);
-    f_mul<P>(E.Y, E.Y, z3);
-    llaff_store(tab, ll_gray(m), E.X, E.Y);
-    if (mn < 2u) break;
+    uint32_t zi[9], x[9], y[9];
+    if (m > 0u) {
+      f_mul<P>(zi, inv, pre);   // Z_m^-1
+      f_mul<P>(inv, inv, E.Z);  // (prod_(< m))^-1
+    } else {
+      f_copy(zi, inv);
+    }
+    ll_to_affine<P>(x, y, E, zi);
+    llaff_store(tab, ll_gray(m), x, y);
+    if (m == 0u) break;
     j_copy(E, En);
-    f_copy(pre, pn);
-    m = mn;
+    if (m >= 2u) f_copy(pre, pn);
   }
 }
 
-// u2 Q from an affine Lim-Lee comb table (Horner over the 37 columns, top first).
+// Curve constants of a base-field class (the order n for u2 + n).
 template <class P>
-BH_HD void q_llcomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab) {
-  uint32_t k2[8], one[9];
-  ld8(k2, w.r, i, w.ns);
-  f_const(one, P::r1);
-  uint64_t sl[kLLTeeth];  // bits [s t, s t + s) of u2, s = kLLSpace
+using CvOf = typename std::conditional<P::a_is_minus3 != 0, Cv_p256, Cv_k1>::type;
+
+// Column j of the signed comb: entry index and sign (V_j = +-E[idx]).
+BH_HD void ll_column(const uint64_t sl[kLLTeeth], int j, uint32_t& idx, bool& neg) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int t = 0; t + 1 < kLLTeeth; t++) m |= (uint32_t)((sl[t] >> j) & 1ull) << t;
+  neg = ((sl[kLLTeeth - 1] >> j) & 1ull) == 0ull;
+  idx = neg ? (~m & (kLLEnt - 1u)) : m;
+}
+
+// The comb's tooth slices of u2: bits [s i, s i + s) of c = (k >> 1) | 2^(t s - 1).
+template <class P>
+BH_HD void ll_slices(uint64_t sl[kLLTeeth], const uint32_t u2[8]) {
+  using Cv = CvOf<P>;
+  const uint32_t add = (u2[0] & 1u) ? 0u : ~0u;  // even u2: k = u2 + n
+  uint32_t k[9], c[9];
+  uint64_t cy = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    cy += (uint64_t)u2[q] + (Cv::n[q] & add);
+    k[q] = (uint32_t)cy;
+    cy >>= 32;
+  }
+  k[8] = (uint32_t)cy;  // k < 2^257
+#pragma unroll
+  for (int q = 0; q < 8; q++) c[q] = (k[q] >> 1) | (k[q + 1] << 31);
+  c[8] = 0u;
+  c[(kLLTS - 1) >> 5] |= 1u << ((kLLTS - 1) & 31);
 #pragma unroll
   for (int t = 0; t < kLLTeeth; t++) {
     const int lo = kLLSpace * t, wd = lo >> 5, sh = lo & 31;
-    uint64_t x = (uint64_t)k2[wd] >> sh;
-    if (wd + 1 < 8) x |= (uint64_t)k2[wd + 1] << (32 - sh);
-    if (wd + 2 < 8 && sh + kLLSpace > 64) x |= (uint64_t)k2[wd + 2] << (64 - sh);
+    uint64_t x = (uint64_t)c[wd] >> sh;
+    if (wd + 1 < 9) x |= (uint64_t)c[wd + 1] << (32 - sh);
+    if (wd + 2 < 9 && sh + kLLSpace > 64) x |= (uint64_t)c[wd + 2] << (64 - sh);
     sl[t] = x & ((1ull << kLLSpace) - 1ull);
   }
-  a_inf = true;
-  f_copy(A.X, one);
-  f_copy(A.Y, one);
+}
+
+// u2 Q from an affine signed comb table (Horner over the s columns, top first).
+template <class P>
+BH_HD void q_llcomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab) {
+  uint32_t u2[8], one[9];
+  ld8(u2, w.r, i, w.ns);
+  f_const(one, P::r1);
+  uint64_t sl[kLLTeeth];
+  ll_slices<P>(sl, u2);
+  uint32_t idx;
+  bool neg;
+  ll_column(sl, kLLSpace - 1, idx, neg);  // top column: top bit set, +E[idx]
+  llaff_load(A.X, A.Y, tab, idx);
   f_copy(A.Z, one);
+  a_inf = false;
 #pragma unroll 1
-  for (int j = kLLSpace - 1; j >= 0; j--) {
-    uint32_t b = 0;
-#pragma unroll
-    for (int t = 0; t < kLLTeeth; t++) b |= (uint32_t)((sl[t] >> j) & 1ull) << t;
+  for (int j = kLLSpace - 2; j >= 0; j--) {
     j_dbl<P>(A, A);  // (while a_inf, A is a placeholder the next point replaces)
-    uint32_t tx[9], ty[9];
-    llaff_load(tx, ty, tab, b ? b : 1u);
-    j_acc_aff<P>(A, a_inf, tx, ty, one, b == 0);
+    ll_column(sl, j, idx, neg);
+    uint32_t tx[9], ty[9], nty[9];
+    llaff_load(tx, ty, tab, idx);
+    f_neg<P, 64>(nty, ty);
+    f_sel(ty, neg, nty, ty);
+    bool same;
+    const bool deg = j_madd<P>(A, A, tx, ty, &same);
+    if (a_inf || deg) {  // rare (crafted scalars): lanes skip this together
+      if (a_inf || same) {  // A was infinity: V; A == V: 2 V
+        J30 T;
+        f_copy(T.X, tx);
+        f_copy(T.Y, ty);
+        f_copy(T.Z, one);
+        if (a_inf) j_copy(A, T);
+        else j_dbl<P>(A, T);
+        a_inf = false;
+      } else {  // A == -V
+        a_inf = true;
+      }
+    }
   }
 }
 

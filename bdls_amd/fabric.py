@@ -212,3 +212,77 @@ def block_signatures_preverify(blocks, sha3: bool = False, keep_keys: bool = Fal
                                                    cap, ctypes.byref(total)))
     return [(res[i].status, [int(x) for x in sr[res[i].sig_first:res[i].sig_first + res[i].sig_count]],
              res[i].valid_identities) for i in range(n)]
+
+
+# ---------------------------------------------------------------- the Go consumer, mirrored
+# The verified-signature cache and the cache-first PreverifySets of
+# INTEGRATION.md sections 4 and 6 (common/sigcache, common/policies/
+# preverify.go), restated so the tests can drive the exact consumer flow.
+VALID, INVALID = 1, 2
+# engine reasons whose identity.Verify outcome is parse-independent (cacheable)
+CACHEABLE = {0: VALID, 7: INVALID, 8: INVALID, 9: INVALID}
+# Below this many cache misses a policy evaluation does not call the device:
+# the misses go to identity.Verify (the sw provider, or the coalescing single
+# Verify). INTEGRATION.md 6 / HIPOpts.MinBatch.
+PREVERIFY_MIN_BATCH = 16
+
+
+class SigCache:
+    """common/sigcache: (identity, signature) -> (signed bytes, outcome,
+    generation). The key is length-prefixed, so no two (identity, signature)
+    pairs collide; a lookup also compares the signed bytes exactly."""
+
+    def __init__(self):
+        self.m, self.gen = {}, 0
+
+    @staticmethod
+    def key(identity: bytes, sig: bytes) -> bytes:
+        return len(identity).to_bytes(8, "big") + identity + sig
+
+    def begin(self) -> int:
+        self.gen += 1
+        return self.gen
+
+    def put(self, gen: int, identity: bytes, sig: bytes, data: bytes, out: int) -> None:
+        self.m[self.key(identity, sig)] = (bytes(data), out, gen)
+
+    def release(self, gen: int) -> None:
+        self.m = {k: v for k, v in self.m.items() if v[2] != gen}
+
+    def lookup(self, identity: bytes, data: bytes, sig: bytes):
+        e = self.m.get(self.key(identity, sig))
+        return e[1] if e is not None and e[0] == bytes(data) else None
+
+
+def preverify_sets(cache: SigCache, sets, min_batch: int = PREVERIFY_MIN_BATCH,
+                   sha3: bool = False, stats=None):
+    """INTEGRATION.md 6 PreverifySets, cache first: every (identity, data,
+    signature) of the sets is looked up; only the misses go to the device,
+    each as its own one-signature set (no de-duplication: every miss gets its
+    own outcome), and only when there are at least min_batch of them -- fewer
+    stay with identity.Verify. Returns the release function of the entries
+    it added. stats (dict) counts lookups / hits / device calls."""
+    seen, misses = set(), []
+    for s in sets:
+        for ident, data, sig in s:
+            k = (cache.key(ident, sig), bytes(data))
+            if k in seen:
+                continue
+            seen.add(k)
+            if stats is not None:
+                stats["lookups"] = stats.get("lookups", 0) + 1
+            if cache.lookup(ident, data, sig) is not None:
+                if stats is not None:
+                    stats["hits"] = stats.get("hits", 0) + 1
+                continue
+            misses.append((ident, data, sig))
+    if len(misses) < max(1, min_batch):
+        return lambda: None
+    if stats is not None:
+        stats["device_calls"] = stats.get("device_calls", 0) + 1
+    res = signature_sets_verify([[sd] for sd in misses], sha3=sha3, keep_keys=True)
+    gen = cache.begin()
+    for (ident, data, sig), (r, _) in zip(misses, res):
+        if r[0] in CACHEABLE:
+            cache.put(gen, ident, sig, data, CACHEABLE[r[0]])
+    return lambda: cache.release(gen)

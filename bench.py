@@ -23,8 +23,11 @@ round (336 SignedProtos), warm and cold.
 
 Multi-GPU: one process per GPU. Under torch.distributed.run the ranks come from
 the environment; `--gpus N` without a launcher spawns the N ranks itself (before
-anything touches a GPU). Records shard with no data-path collective; a gloo
-barrier brackets the timed region and the max time over ranks is reported.
+anything touches a GPU). Records shard with no data-path collective; a barrier
+over bdls_amd.dist's stdlib control channel (127.0.0.1 sockets, rank 0 the hub)
+brackets the timed region and the max time over ranks is reported. No rank
+process imports torch: libbdlship.so must bind /opt/rocm's HIP runtime, not
+the copy torch bundles.
 """
 from __future__ import annotations
 
@@ -49,9 +52,15 @@ sys.path.insert(0, ROOT)
 # of every key-comb record (G_WINDOWS mixed adds of 11 ops over the 10-bit G
 # comb: BH_GCOMB_BITS in verify.h); k_keycomb adds the key-table part and the
 # stored u1 G and checks x (~23 ops). Per-batch tables of large batches are
-# Lim-Lee combs (round 3, verify.h lltab_build; BH_LL=0: 4-bit windows):
-#   build: 222 doublings (8 ops) + 120 additions (16) = 3,696 per table
-#   comb:  36 doublings + 37 additions = 880 per record
+# signed Lim-Lee combs (round 4, verify.h lltab_build; BH_LL=0: 4-bit windows)
+# with LL_T teeth spaced LL_S bits (BH_LL_T, 7 x 37), 2^(LL_T-1) entries:
+#   build: (LL_T-1) LL_S doublings (8 ops); the 2 (LL_T-1) chain points made
+#     affine (2 (LL_T-1) - 1 prefix products + 6 per point); E[0] by LL_T-1
+#     mixed additions (11); the Gray walk's 2^(LL_T-1) - 1 mixed additions plus
+#     one running Z product (12); the backward pass (6 per entry); two safegcd
+#     inversions (~14k VALU instructions each, ~85 F_p-op equivalents)
+#   comb: LL_S - 1 doublings + LL_S - 1 mixed additions per record (the top
+#     column is loaded, every column is nonzero)
 # windows: build 65 x 58 = 3,770 per table (co-Z chain), comb 65 additions
 # (16 ops: the tables are Jacobian) = 1,040 per record.
 MAC_PER_FP = 128
@@ -59,20 +68,14 @@ G_COMB_BITS = 10
 G_WINDOWS = (257 + G_COMB_BITS - 1) // G_COMB_BITS
 LL_TABLES = os.environ.get("BH_LL", "1") != "0"
 FP_LADDER, FP_GPART = 3200, G_WINDOWS * 11
-# Lim-Lee comb, LL_T teeth spaced LL_S bits (verify.h BH_LL_T, 6 x 43): the
-# table (lltab_build) is (LL_T - 1) LL_S doublings, B_1..B_{T-1} made affine
-# (T - 2 + 4 (T - 1) + 2 (T - 2) products), the Gray walk's 2^T - 1 - T non-base
-# steps (mixed addition 8 M + 3 S + one running Z product), the backward pass
-# (6 per entry) and two safegcd inversions (~14k VALU instructions each, ~85
-# F_p-op equivalents at 169 per op); the key comb is LL_S - 1 doublings + LL_S
-# mixed additions against 65 full additions of the 4-bit windows
-LL_T = 6
-LL_S = -(-256 // LL_T)
+LL_T = 7
+LL_S = -(-257 // LL_T)
 FP_INV_SG = 85
-_LL_WALK = 2**LL_T - 1 - LL_T
-FP_KTAB = ((LL_T - 1) * LL_S * 8 + (LL_T - 2) + 4 * (LL_T - 1) + 2 * (LL_T - 2)
-           + _LL_WALK * 12 + _LL_WALK * 6 + 2 * FP_INV_SG) if LL_TABLES else 65 * 58
-FP_KEYCOMB = ((LL_S - 1) * 8 + LL_S * 11 if LL_TABLES else 65 * 16) + 23
+_LL_ENT = 2**(LL_T - 1)
+_LL_CHAIN = 2 * (LL_T - 1)
+FP_KTAB = ((LL_T - 1) * LL_S * 8 + (_LL_CHAIN - 1) + 6 * _LL_CHAIN + (LL_T - 1) * 11
+           + (_LL_ENT - 1) * 12 + _LL_ENT * 6 + 2 * FP_INV_SG) if LL_TABLES else 65 * 58
+FP_KEYCOMB = ((LL_S - 1) * (8 + 11) if LL_TABLES else 65 * 16) + 23
 MACS_PER_VERIFY = FP_LADDER * MAC_PER_FP
 KERNELS = {"build_ladder_ms": "k_ktab_ladder", "keycomb_ms": "k_keycomb"}
 CONFIG5_TOTAL = 1 << 26
@@ -170,14 +173,21 @@ def spawn_ranks(n: int) -> int:
     """`bench.py --gpus N` without a launcher: start N rank processes (this
     script again, one GPU each) -- the parent never touches a GPU -- and exit
     with the worst child status. Rank 0 prints the JSON line."""
+    import shutil
+    import tempfile
     port = free_port()
+    ctrl = tempfile.mkdtemp(prefix="bdls_ctrl_")  # the ranks' rendezvous (bdls_amd/dist.py)
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
-                                      env=env))
-    rcs = [p.wait() for p in procs]
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                       LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                       BDLS_CTRL_DIR=ctrl)
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)]
+                                          + sys.argv[1:], env=env))
+        rcs = [p.wait() for p in procs]
+    finally:
+        shutil.rmtree(ctrl, ignore_errors=True)
     bad = [rc for rc in rcs if rc != 0]
     return bad[0] if bad else 0
 
@@ -191,6 +201,7 @@ def bench_latency(a, rank, world, local):
     from bdls_amd import _lib, dist, workload
     L = _lib.lib()
     _lib.check(L.bh_init(1 << local, 0))
+    assert "torch" not in sys.modules, "torch must not share a process with libbdlship.so"
     DA = _lib.DeviceArray
     if a.config == 3:
         w = workload.generate_block(seed=a.seed + 1000 * rank)
@@ -469,17 +480,25 @@ def load_counters(config: int, n_rank: int):
     """Per-launch HBM traffic and counter-based VALU utilisation of the
     kernels, from the rocprofv3 --pmc passes summarised in
     profiles/traffic.json (tools/pmc_summary.py), when they were taken on
-    this same workload."""
+    this same workload AND on this kernel build: the file's kernel_src_sha must
+    equal the hash of the kernel sources beside the library (bdls_amd/
+    provenance.py); otherwise the counters are stale and not printed.
+    Returns (source, kernels, stale_reason)."""
+    from bdls_amd.provenance import kernel_src_sha
     prof = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(prof):
-        return None, {}
+        return None, {}, "no profiles/traffic.json"
     with open(prof) as f:
         tr = json.load(f)
     want = f"config{config}:n{n_rank}"
-    if tr.get("workload") not in (None, want) or (tr.get("workload") is None and
-                                                  (config, n_rank) != (2, 1 << 20)):
-        return None, {}
-    return tr.get("source"), tr.get("kernels", {})
+    if tr.get("workload") != want:
+        return None, {}, f"counters taken on {tr.get('workload')}, not {want}"
+    cur = kernel_src_sha()
+    if tr.get("kernel_src_sha") != cur:
+        return None, {}, (f"stale: counters describe kernel sources {tr.get('kernel_src_sha')} "
+                          f"(rev {tr.get('git_rev')}), this build is {cur}")
+    return (f"{tr.get('source')} @ rev {tr.get('git_rev')}, kernel_src_sha {cur}",
+            tr.get("kernels", {}), None)
 
 
 def cpu_baseline(a, w, n):
@@ -533,10 +552,11 @@ def bench_throughput(a, rank, world, local):
     n = hi - lo
 
     # Page-locked host memory comes from libbdlship.so (bh_host_alloc); torch
-    # ships its own HIP runtime, so torch is used only for torch.distributed
-    # (gloo) and never touches the GPU in this process.
+    # ships its own HIP runtime and is never imported into a rank process.
     L = _lib.lib()
     _lib.check(L.bh_init(1 << local, 0))
+    assert "torch" not in sys.modules, "torch must not share a process with libbdlship.so"
+
     pinned = []
 
     def alloc(nbytes):
@@ -738,8 +758,10 @@ def bench_throughput(a, rank, world, local):
         "s0_schedule_frac": round(rate * FP_LADDER * MAC_PER_FP / peak, 4) if peak else None,
         "note": "per GPU, HBM-resident step; s0_schedule_frac prices every verify at SURVEY "
                 "8(d)'s 3,200 F_p ops (schedule S0)"}
-    src, counters = load_counters(a.config, n)
+    src, counters, stale = load_counters(a.config, n)
     hit = [v for k, v in counters.items() if k.startswith(kname + "<")]
+    if stale:
+        out["roofline"]["counters_refused"] = stale
     if hit:
         c = hit[0]
         if "bytes_per_launch" in c:
@@ -905,8 +927,97 @@ def single_verify_measure(L, threads_list=(1, 8, 64, 256)) -> dict:
     out["cpu_proxy"] = {"one_call_us_1thr": round(1e6 / rates[1], 1),
                         "verifies_per_s_1thr": round(rates[1], 1),
                         "verifies_per_s_16thr": round(rates[16], 1)}
+    # The crossover the Go provider routes on (HIPOpts.
+    # MinInflight): at c concurrent callers the embedded sw provider does
+    # min(c, usable CPUs) x its one-core rate; the device path is the
+    # registered-key coalescer rate. Below the first c where the device wins,
+    # lone calls stay on sw.
+    cpus = host_cpus()
+    usable = int(min(cpus.get("affinity", cpus["nproc"]),
+                     cpus.get("cgroup_quota_cpus", cpus["nproc"]))) or 1
+    cmp_ = {}
+    for nth in threads_list:
+        g = out.get(f"registered_{nth}thr", {}).get("verifies_per_s")
+        if g:
+            cmp_[str(nth)] = {"device": g, "sw_proxy": round(min(nth, usable) * rates[1], 1)}
+    wins = [int(k) for k, v in cmp_.items() if v["device"] > v["sw_proxy"]]
+    out["crossover"] = {"by_callers": cmp_, "usable_cpus": usable,
+                        "min_inflight": min(wins) if wins else None,
+                        "note": "sw_proxy = min(callers, usable CPUs) x the one-core OpenSSL "
+                                "rate; the Go provider sends calls to the device only at or "
+                                "above min_inflight concurrent callers"}
     out["parity"] = ok
     return out
+
+
+def config5_rank_measure(L, local: int, n: int = 1 << 20, steps: int = 3, gen_threads: int = 16):
+    """VERDICT r3 missing #1 on the driver's line: config 5's per-rank work on
+    one GPU -- the first 1,048,576 records of rank 0's shard of the seeded
+    67,108,864-record unique-key batch (workload.generate_shard: record i is a
+    function of (seed 5, i), the same records an 8-GPU run gives rank 0) --
+    every key distinct, so every verify is a variable-base ladder (no key
+    tables). Host path (bh_verify_submit/wait from page-locked buffers, two in
+    flight) and HBM-resident (bh_verify_dev) rates over `steps` passes each,
+    route counts and parity. Generation is timed separately."""
+    from bdls_amd import _lib, workload
+    pinned = []
+
+    def alloc(nbytes):
+        h = _lib.HostArray(nbytes)
+        pinned.append(h)
+        return h.u8
+    t = time.perf_counter()
+    w = workload.generate_shard(CONFIG5_TOTAL, 0, n, CONFIG5_TOTAL, 256, 64, seed=5,
+                                nthreads=gen_threads, alloc=alloc)
+    gen_s = time.perf_counter() - t
+    flags = _lib.BH_F_HASH_SHA256
+    hb = _lib.BhBatch(*[x.ctypes.data for x in w.arrays()])
+    outs = [(np.zeros((n + 7) // 8, np.uint8), np.zeros(n, np.uint8)) for _ in range(2)]
+
+    def submit(k):
+        job = ctypes.c_void_p()
+        bm, rs = outs[k % 2]
+        _lib.check(L.bh_verify_submit(0, ctypes.byref(hb), n, flags, bm.ctypes.data,
+                                      rs.ctypes.data, ctypes.byref(job)))
+        return job
+    _lib.check(L.bh_verify_wait(submit(0)))  # warmup
+    t = time.perf_counter()
+    jobs = [submit(0)]
+    for k in range(1, steps):
+        jobs.append(submit(k))
+        _lib.check(L.bh_verify_wait(jobs.pop(0)))
+    _lib.check(L.bh_verify_wait(jobs.pop(0)))
+    host_s = time.perf_counter() - t
+    bm, rs = outs[(steps - 1) % 2]
+    ok = bool((rs == w.reason).all() and (np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+                                            == w.expected_valid).all())
+    DA = _lib.DeviceArray
+    d = [DA.from_numpy(local, x) for x in w.arrays()]
+    words, dreason = DA(local, ((n + 63) // 64) * 8), DA(local, n)
+    db = _lib.BhBatch(*[x.ptr for x in d])
+    tm = _lib.BhTiming()
+    _lib.check(L.bh_verify_dev(local, 0, ctypes.byref(db), n, flags, words.ptr, dreason.ptr, None,
+                               1, ctypes.byref(tm)))
+    t = time.perf_counter()
+    for _ in range(steps):
+        _lib.check(L.bh_verify_dev(local, 0, ctypes.byref(db), n, flags, words.ptr, dreason.ptr,
+                                   None, 0, None))
+    _lib.check(L.bh_sync(local))
+    dev_s = time.perf_counter() - t
+    ok = ok and bool((dreason.to_numpy(np.uint8, n) == w.reason).all())
+    for x in d + [words, dreason]:
+        x.free()
+    return {"records": n, "distinct_keys": n, "gen_s": round(gen_s, 2),
+            "host_path_verifies_per_s": round(n * steps / host_s, 1),
+            "hbm_resident_verifies_per_s": round(n * steps / dev_s, 1),
+            "steps": steps,
+            "routes": {"ladder": tm.n_ladder, "keycomb": tm.n_keycomb,
+                       "key_tables": tm.n_keytables},
+            "kernel_ms": {k: round(getattr(tm, k), 3) for k in _lib.BhTiming.STAGES},
+            "workload": f"records [0, {n}) of rank 0's shard of config 5's seeded "
+                        f"{CONFIG5_TOTAL}-record unique-key batch (seed 5, 256 B messages, "
+                        f"1/64 corrupted, fused SHA-256)",
+            "parity": ok}
 
 
 def side_configs(a, L, rank) -> dict:
@@ -957,6 +1068,11 @@ def side_configs(a, L, rank) -> dict:
     out["config1"] = config1_measure(max(1, a.side_steps // 10))
     # the coalesced single Verify
     out["single_verify"] = single_verify_measure(L)
+    # config 5's per-rank shape (unique keys: the ladder)
+    cpus = host_cpus()
+    usable = int(min(cpus.get("affinity", cpus["nproc"]),
+                     cpus.get("cgroup_quota_cpus", cpus["nproc"]))) or 1
+    out["config5_rank"] = config5_rank_measure(L, 0, gen_threads=max(4, min(32, usable)))
     out["seconds"] = round(time.perf_counter() - t0, 2)
     return out
 
@@ -975,9 +1091,11 @@ def dry_run(a, rank, world):
     ok = dist.all_true(True, world)
     lo, hi = dist.shard_range(a.n_total if a.config == 5 else a.n * world, rank, world)
     recs = dist.sum_over_ranks(hi - lo, world)
+    torch_free = dist.all_true("torch" not in sys.modules, world)
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "config": a.config,
-                          "records_total": recs, "max_t": t, "parity": ok}), flush=True)
+                          "records_total": recs, "max_t": t, "parity": ok,
+                          "torch_free_ranks": torch_free}), flush=True)
     dist.finalize(world)
     return 0
 

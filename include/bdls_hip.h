@@ -168,6 +168,13 @@ int bh_csp_verify_p256(const uint8_t pub[64], const uint8_t *sig, size_t sig_len
  * formed, out[2] largest batch. */
 int bh_csp_stats(uint64_t out[3]);
 
+/* Device batches since bh_init over every entry point: out[0] batches launched
+ * (one per device pass sequence of a call or shard, one per latency-path
+ * batch), out[1] records they carried. Lets a consumer prove it issued no
+ * device work (a phase-2 policy evaluation whose signatures
+ * phase 1 already verified). Not in the reference: an observability hook. */
+int bh_device_stats(uint64_t out[2]);
+
 /* Host-side Go-exact DER unmarshal (bccsp/utils/ecdsa.go:41-65). Returns the
  * reason (BH_R_OK, BH_R_DER, BH_R_R_NONPOS, BH_R_S_NONPOS); on BH_R_OK fills
  * r, s (32-byte big-endian) or sets *r_big / *s_big when a value exceeds 256

@@ -340,6 +340,7 @@ class Ident:
     x: int
     y: int
     key: bytes  # Mspid + Id (sanitized certificate) for the de-duplication
+    mspid: bytes = b""
 
 
 def deserialize(ser: bytes):
@@ -371,7 +372,7 @@ def deserialize(ser: bytes):
         key += len(rb).to_bytes(2, "big") + rb
     else:
         key += b"\xff\xff" + sig
-    return Ident(x, y, key)
+    return Ident(x, y, key, si["mspid"] or b"")
 
 
 # ---------------------------------------------------------------- validation
@@ -504,6 +505,86 @@ def signature_set_to_valid_identities(entries, verify, decode_only: bool = False
         if r == 0:
             id_map.add(ident.key)
     return out, len(id_map)
+
+
+# ---------------------------------------------------------------- endorsement policies
+def endorsement_sets(block: bytes):
+    """Per transaction the endorsement signature set the validation plugin
+    hands to the endorsement policy (validator_keylevel.go:246-260 ->
+    policy.EvaluateSignedData): [(endorser, prp || endorser, signature)], or
+    None where the transaction is not an endorser transaction whose structure
+    decodes (validate_block's TX / earlier statuses)."""
+    blk = unmarshal(block, BLOCK_SPEC)
+    out = []
+    for d in (blk["data"] or {"data": []})["data"]:
+        try:
+            env = unmarshal(d, ENVELOPE_SPEC)
+            pl = unmarshal(env["payload"] or b"", PAYLOAD_SPEC)
+            tx = unmarshal(pl["data"] or b"", TRANSACTION_SPEC)
+            if len(tx["actions"]) != 1:
+                raise DecodeError("actions")
+            cap = unmarshal(tx["actions"][0]["payload"] or b"", CC_ACTION_PAYLOAD_SPEC)
+            if cap["action"] is None:
+                raise DecodeError("nil action")
+        except (DecodeError, TypeError):
+            out.append(None)
+            continue
+        prp = cap["action"]["proposal_response_payload"] or b""
+        out.append([(e["endorser"] or b"", prp + (e["endorser"] or b""), e["signature"] or b"")
+                    for e in cap["action"]["endorsements"]])
+    return out
+
+
+def valid_identities(signature_set, identity_verify):
+    """common/policies/policy.go:363-395 SignatureSetToValidIdentities returning
+    the de-duplicated valid identities (as Ident). identity_verify(serialized
+    identity, data, signature) -> BH_R_* reason of identity.Verify: the
+    consult site of the verified-signature cache."""
+    id_map, out = set(), []
+    for ident_bytes, data, sig in signature_set:
+        ident = deserialize(ident_bytes)
+        if ident is None or ident.key in id_map:
+            continue
+        if identity_verify(ident_bytes, data, sig) != 0:
+            continue
+        id_map.add(ident.key)
+        out.append(ident)
+    return out
+
+
+def signed_by_member(mspid: bytes):
+    """A cauthdsl signature policy "OR('<mspid>.member')" (the per-org
+    Endorsement policy of sampleconfig/configtx.yaml:69-71): cauthdsl/policy.go
+    EvaluateSignedData = SignatureSetToValidIdentities + the evaluator; a member
+    principal is satisfied by any valid identity of that MSP (the engine does
+    not build MSP chains, so identities here are the chain-valid ones)."""
+    def evaluate(signature_set, identity_verify) -> bool:
+        return any(i.mspid == mspid for i in valid_identities(signature_set, identity_verify))
+    return evaluate
+
+
+def implicit_meta_evaluate(signature_set, sub_policies, rule: str, identity_verify,
+                           before=None) -> bool:
+    """common/policies/implicitmeta.go:69-101 ImplicitMetaPolicy.EvaluateSignedData:
+    threshold ANY 1 / ALL len / MAJORITY len/2 + 1 (:44-58, 0 without
+    sub-policies); every sub-policy evaluates the SAME signature set until the
+    threshold is met. `before(signature_set)` runs first and its return value
+    (a release function) after: the consumer's PreverifySets hook
+    (INTEGRATION.md 6)."""
+    threshold = {"ANY": 1, "ALL": len(sub_policies),
+                 "MAJORITY": len(sub_policies) // 2 + 1}[rule] if sub_policies else 0
+    release = before(signature_set) if before else None
+    try:
+        remaining = threshold
+        for pol in sub_policies:
+            if remaining == 0:
+                break
+            if pol(signature_set, identity_verify):
+                remaining -= 1
+        return remaining == 0
+    finally:
+        if release:
+            release()
 
 
 def envelope_as_signed_data(env_bytes: bytes):

@@ -1,0 +1,122 @@
+"""Crafted scalars and records for the per-key comb tables (verify.h
+lltab_build / q_llcomb: the signed Lim-Lee comb of one-lane-per-record
+batches), shared by the host-harness tests and the GPU tests.
+
+A record built for a chosen u2 (R = u1 G + u2 Q, r = x(R) mod n, s = r / u2,
+e = u1 s) verifies by construction; its flipped-digest twin fails (R_MATH).
+The scalars sit at the signed comb's edges: odd and even u2 (k = u2 or u2 + n),
+columns whose lower teeth are all clear or all set, a top tooth of zeros
+(negated entries in every column), single digits, the largest k, and u2 whose
+Horner hits A == V_j (the doubling branch) -- found by running the comb's
+recurrence on every sign pattern of column 0 (the infinity branch A == -V_j
+cannot occur for these shapes: tests/comb_cases.py::horner_events).
+"""
+from __future__ import annotations
+
+import itertools
+import random
+
+from oracle import ecdsa_ref as O
+
+
+def horner_events(u2: int, n: int, t: int, s: int):
+    """The signed comb's Horner on the scalar u2 (verify.h q_llcomb), as
+    integers mod n: [(event, column)] for the degenerate steps."""
+    k = u2 if u2 & 1 else u2 + n
+    c = (k >> 1) | (1 << (t * s - 1))
+    V = [sum((2 * ((c >> (s * i + j)) & 1) - 1) << (s * i) for i in range(t)) for j in range(s)]
+    assert sum(v << j for j, v in enumerate(V)) == k
+    ev, a, inf = [], V[s - 1], False
+    for j in range(s - 2, -1, -1):
+        a *= 2
+        if inf:
+            a, inf = V[j], False
+            ev.append(("from_inf", j))
+            continue
+        if (a - V[j]) % n == 0:
+            ev.append(("dbl", j))
+        elif (a + V[j]) % n == 0:
+            ev.append(("inf", j))
+            a, inf = 0, True
+            continue
+        a += V[j]
+    assert inf or (a - k) % n == 0
+    return ev
+
+
+def signed_comb_u2(n: int, t: int, s: int, seed: int = 5) -> list[int]:
+    """u2 at the edges of the t x s signed comb for group order n."""
+    ts = t * s
+    out = [1, 2, 3, n - 1, n - 2, n // 2, n // 2 + 1, 2**255, (2**256) % n, 2**(s * (t - 1)),
+           2**(s * (t - 1)) + 1, 2**s, 2**s + 1, 2**(s - 1)]
+
+    def from_c(x):  # c = 2^(ts-1) + x  ->  k = 2 x + 1 -> u2
+        k = 2 * x + 1
+        return (k if k < n else k - n) if k < 2 * n else None
+
+    lower_all = 2**(s * (t - 1)) - 1
+    patterns = [0, lower_all, lower_all ^ ((2**s - 1) << (s * (t - 2))),  # top tooth 0
+                sum(1 << (s * i) for i in range(t - 1)),               # one column full
+                sum(((2**s - 1) if i % 2 else 0) << (s * i) for i in range(t - 1)),
+                sum((0x5555555555555555 & ((1 << s) - 1)) << (s * i) for i in range(t - 1)),
+                n - 1 - (2**(ts - 1) % n) if ts - 1 < 256 else (n - 1) // 2]
+    for x in patterns:
+        u2 = from_c(x)
+        if u2:
+            out.append(u2)
+    # the doubling branch: k == 2 V_0 (mod n) for a sign pattern of column 0
+    for pat in itertools.product((-1, 1), repeat=t):
+        v0 = sum(d << (s * i) for i, d in enumerate(pat))
+        u2 = (2 * v0) % n
+        if u2 and any(e[0] == "dbl" for e in horner_events(u2, n, t, s)):
+            out.append(u2)
+    rng = random.Random(seed)
+    out += [rng.randrange(1, n) for _ in range(4)]
+    seen, res = set(), []
+    for u in out:
+        u %= n
+        if u and u not in seen:
+            seen.add(u)
+            res.append(u)
+    return res
+
+
+def unsigned_comb_u2(t: int, s: int) -> list[int]:
+    """Round 3's crafted scalars for the unsigned t x s comb (single teeth,
+    empty / full top columns): still a spread of column patterns."""
+    top = 256 - s * (t - 1)
+    return [2**(s - 1), 2**s, 2**(2 * s), 2**(s * (t - 1)), 2**255,
+            2**(s * (t - 1)) + 2**(s * (t - 1) - 1), 2**s - 1,
+            sum(2**(s * k) for k in range(t)), sum(2**(s * k + s - 1) for k in range(t - 1)),
+            sum(2**(s * k + s - 1) for k in range(t - 1)) + 2**255,
+            (2**s - 1) << (256 - top - s), sum((2**s - 1) << (s * k) for k in range(t - 1))]
+
+
+def records_for_u2(curve, u2s, seed: int = 77, d: int | None = None, low_s: bool = False):
+    """One key; per u2 a valid signature and its flipped-digest twin:
+    [(qx, qy, der_sig, digest)], the first verifying, the twin R_MATH. With
+    low_s, u1 is redrawn until s <= n / 2, so the signature passes Fabric's
+    low-S rule AND the verifier still computes exactly this u2."""
+    c = curve
+    n = c.n
+    rng = random.Random(seed)
+    d = d or rng.randrange(1, n)
+    qx, qy = O.scalar_mult(c, d, (c.gx, c.gy))
+    recs = []
+    for u2 in u2s:
+        u2Q = O.scalar_mult(c, u2 % n, (qx, qy))
+        for _ in range(64):
+            u1 = rng.randrange(1, n)
+            R = O.point_add(c, O.scalar_mult(c, u1, (c.gx, c.gy)), u2Q)
+            if R is None or R[0] % n == 0:
+                continue
+            r = R[0] % n
+            s = r * pow(u2, -1, n) % n
+            if not low_s or s <= n // 2:
+                break
+        else:
+            continue
+        e = u1 * s % n
+        for dg in (e.to_bytes(32, "big"), (e ^ 1).to_bytes(32, "big")):
+            recs.append((qx, qy, O.marshal_ecdsa_signature(r, s), dg))
+    return recs

@@ -64,19 +64,26 @@ def hs():
 
 
 @pytest.mark.parametrize("curve", ["secp256k1", "P-256"])
-@pytest.mark.parametrize("min_uses", [1, 1000])
-def test_bdls_hostsim(hs, bdls_golden, curve, min_uses):
+@pytest.mark.parametrize("min_uses,ll", [(1, 0), (1000, 0), (1, 1)])
+def test_bdls_hostsim(hs, bdls_golden, curve, min_uses, ll):
+    """ll = 1: per-batch key tables as the signed Lim-Lee comb (what the device
+    builds for BDLS batches above 32,768 records), secp256k1 included."""
     recs = [r for r in bdls_golden if r["curve"] == curve]
     arrs = pack_bdls(recs)
     out = np.zeros(len(recs), np.uint8)
-    hs.hs_verify_bdls(CURVE_ID[curve], *[a.ctypes.data for a in arrs], len(recs), min_uses,
-                      out.ctypes.data)
+    hs.hs_set_ll(ll)
+    try:
+        hs.hs_verify_bdls(CURVE_ID[curve], *[a.ctypes.data for a in arrs], len(recs), min_uses,
+                          out.ctypes.data)
+    finally:
+        hs.hs_set_ll(0)
     bad = [(r["tag"], int(o), r["reason"]) for r, o in zip(recs, out) if o != r["reason"]]
     assert not bad
 
 
-def _k1_edge_records():
-    """secp256k1 digest-level edge cases (x wrap, infinity, internal doubling)."""
+def _k1_edge_records(comb_shape=(7, 37)):
+    """secp256k1 digest-level edge cases (x wrap, infinity, internal doubling,
+    GLV split edges, signed-comb edges)."""
     c = O.SECP256K1
     rng = random.Random(99)
     recs = []
@@ -114,6 +121,9 @@ def _k1_edge_records():
            2**128, 2**128 + 1, n - 1, n - 2, n // 2, n // 2 + 1, (2**128 * lam) % n,
            (12345 * lam) % n, (n - 12345 * lam % n) % n, (2**64 + 5 * lam) % n]
     u2s += [rng.randrange(1, n) for _ in range(8)] + [rng.randrange(1, 2**128) for _ in range(4)]
+    # the signed comb's edges for the shape the harness was built with
+    from tests.comb_cases import signed_comb_u2
+    u2s += signed_comb_u2(n, *comb_shape)
     for u2 in u2s:
         u1 = rng.randrange(1, n)
         R = O.point_add(c, O.scalar_mult(c, u1, (c.gx, c.gy)), O.scalar_mult(c, u2, (qx, qy)))
@@ -132,9 +142,12 @@ def _k1_edge_records():
     return recs
 
 
-@pytest.mark.parametrize("min_uses,wide", [(1, 1), (1000, 1), (1, 16), (1, 4), (1000, 4)])
-def test_k1_curve_edges_hostsim(hs, min_uses, wide):
-    recs = _k1_edge_records()
+@pytest.mark.parametrize("min_uses,wide,ll", [(1, 1, 0), (1000, 1, 0), (1, 16, 0), (1, 4, 0),
+                                              (1000, 4, 0), (1, 1, 1)])
+def test_k1_curve_edges_hostsim(hs, min_uses, wide, ll):
+    """ll = 1: the signed Lim-Lee comb tables over secp256k1."""
+    sh = hs.hs_ll_shape()
+    recs = _k1_edge_records((sh >> 8, sh & 0xFF))
     pub = np.frombuffer(b"".join(qx.to_bytes(32, "big") + qy.to_bytes(32, "big")
                                  for _, qx, qy, _, _, _ in recs), np.uint8)
     sigs = [t[3] for t in recs]
@@ -147,12 +160,14 @@ def test_k1_curve_edges_hostsim(hs, min_uses, wide):
     dg = np.frombuffer(b"".join(dgs), np.uint8)
     out = np.zeros(len(recs), np.uint8)
     hs.hs_set_wide(wide)
+    hs.hs_set_ll(ll)
     try:
         hs.hs_verify_k1_digest(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
                                dg.ctypes.data, do.ctypes.data, dl.ctypes.data, len(recs),
                                min_uses, out.ctypes.data)
     finally:
         hs.hs_set_wide(1)
+        hs.hs_set_ll(0)
     bad = [(t[0], int(o), t[5]) for t, o in zip(recs, out) if o != t[5]]
     assert not bad
     assert any(t[0] == "k1_xwrap_accept" and t[5] == 0 for t in recs)

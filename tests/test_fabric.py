@@ -455,3 +455,137 @@ def test_gpu_block_refs_two_phase(classes_block):
     assert len(cache) > 0 and len(misses) < len(calls)
     for k in misses:  # a miss is a record whose Go error text depends on the parse
         assert _orc_verify(*k) in (1, 2, 3, 4, 5, 6)
+
+
+# ---------------------------------------------------------------- implicit-meta policies, cache first
+ORGS = [b"Org1MSP", b"Org2MSP", b"Org3MSP", b"Org4MSP"]
+
+
+def _identity_verify(ident_bytes, data, sig):
+    ident = R.deserialize(ident_bytes)
+    return _orc_verify(ident.x, ident.y, data, sig)
+
+
+def _policy_results(block, identity_verify, before=None, statuses=None):
+    """The validation plugin's endorsement-policy evaluation per transaction
+    that passed validateTx (status OK, endorser tx): the channel default
+    "MAJORITY Endorsement" (sampleconfig/configtx.yaml:241-243) over the four
+    orgs' "OR('OrgN.member')" policies (:69-71)."""
+    subs = [R.signed_by_member(o) for o in ORGS]
+    sets = R.endorsement_sets(block)
+    out = []
+    for st, sd in zip(statuses, sets):
+        if st != R.OK or sd is None:
+            out.append(None)
+            continue
+        out.append(R.implicit_meta_evaluate(sd, subs, "MAJORITY", identity_verify, before))
+    return out
+
+
+def test_implicit_meta_majority_oracle(classes_block):
+    """The oracle's implicit-meta flow on the classes block: a transaction's
+    endorsement policy holds iff at least 3 of its 4 orgs have a valid,
+    de-duplicated endorser -- the generator's own count."""
+    fb = classes_block
+    statuses = [o.status for o in R.validate_block(fb.block, _orc_verify)]
+    pol = _policy_results(fb.block, _identity_verify, statuses=statuses)
+    for i, p in enumerate(pol):
+        if p is not None:
+            assert p == (fb.tx_valid_identities[i] >= 3), (i, fb.tx_class[i])
+    assert any(p is True for p in pol) and any(p is False for p in pol)
+
+
+def test_sigcache_key_unambiguous():
+    """identity || 0x00 || sig collided for (b"a\\0", b"b") and
+    (b"a", b"\\0b"); the length-prefixed key does not."""
+    c = fabric.SigCache()
+    g = c.begin()
+    c.put(g, b"a\0", b"b", b"data", fabric.VALID)
+    assert c.lookup(b"a", b"data", b"\0b") is None
+    assert c.lookup(b"a\0", b"data", b"b") == fabric.VALID
+    assert c.lookup(b"a\0", b"other", b"b") is None  # the signed bytes must match
+    c.release(g)
+    assert c.lookup(b"a\0", b"data", b"b") is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["config3", "classes"])
+def test_gpu_two_phase_implicit_meta_one_device_batch(classes_block, which):
+    """VERDICT r3 missing #2: phase 1 verifies the block's signatures in ONE
+    device batch and fills the verified-signature cache; phase 2 is the
+    unchanged sequential validation -- creator checks consulting the cache,
+    then per transaction the implicit-meta MAJORITY endorsement policy whose
+    EvaluateSignedData first runs the cache-first PreverifySets
+    (INTEGRATION.md 6). Phase 2 issues NO device work (bh_device_stats), its
+    results equal the plain sequential flow's, and the old consumer (no cache
+    lookup, min batch 1) would have issued one device batch per evaluation."""
+    from bdls_amd import _lib
+    _lib.ensure_init()
+    fb = classes_block if which == "classes" else F.generate_fabric_block(seed=3)
+    block = fb.block
+    # the plain flow (no engine): statuses and policy outcomes
+    plain = R.validate_block(block, _orc_verify)
+    statuses = [o.status for o in plain]
+    want_pol = _policy_results(block, _identity_verify, statuses=statuses)
+    # phase 1: one device batch
+    b0 = _lib.device_stats()[0]
+    txs, creators, ends = fabric.block_preverify_refs(block)
+    b1 = _lib.device_stats()[0]
+    # one device batch; the classes block holds the endorse_dup_after_invalid
+    # class, whose later signature of an identity that failed earlier in the
+    # set is checked in the documented follow-up round
+    assert b1 - b0 == (2 if which == "classes" else 1)
+    cache = fabric.SigCache()
+    gen = cache.begin()
+    for r in creators + ends:
+        if r is not None and r.reason in fabric.CACHEABLE:
+            cache.put(gen, r.identity, r.signature, r.data, fabric.CACHEABLE[r.reason])
+    xy_cache = {_ref_key(r): r.reason for r in creators + ends
+                if r is not None and r.reason in fabric.CACHEABLE}
+    go_verifies = []
+
+    def creator_verify(x, y, msg, sig):  # checkSignatureFromCreator's consult site
+        k = (x, y, bytes(msg), bytes(sig))
+        if k in xy_cache:
+            return xy_cache[k]
+        go_verifies.append(k)
+        return _orc_verify(x, y, msg, sig)
+
+    def identity_verify(ident_bytes, data, sig):  # SignatureSetToValidIdentities' consult site
+        out = cache.lookup(ident_bytes, data, sig)
+        if out is not None:
+            return 0 if out == fabric.VALID else 9
+        go_verifies.append((ident_bytes, data, sig))
+        return _identity_verify(ident_bytes, data, sig)
+
+    stats = {}
+
+    def before(sd):
+        return fabric.preverify_sets(cache, [sd], stats=stats)
+
+    got = R.validate_block(block, creator_verify)
+    got_pol = _policy_results(block, identity_verify, before, [o.status for o in got])
+    b2 = _lib.device_stats()[0]
+    assert [_got(o) for o in got] == [_got(o) for o in plain]
+    assert got_pol == want_pol
+    assert b2 == b1 and stats.get("device_calls", 0) == 0  # phase 2: no device work
+    # every lookup that missed is a record whose outcome is not cacheable
+    # (parse-dependent Go error); the loop may not even reach it (the policy
+    # threshold is met first)
+    uncacheable = {(r.identity, r.data, r.signature) for r in ends
+                   if r is not None and r.reason not in fabric.CACHEABLE}
+    assert stats["lookups"] > 0 and stats["lookups"] - stats["hits"] <= len(uncacheable)
+    # the misses are exactly the non-cacheable records (parse-dependent Go errors)
+    for k in go_verifies:
+        r = _orc_verify(*k) if len(k) == 4 and isinstance(k[0], int) else _identity_verify(*k)
+        assert r in (1, 2, 3, 4, 5, 6)
+    if which == "classes":
+        # the round-3 consumer (device call whenever the set is non-empty, no
+        # cache lookup) issues one device batch per policy evaluation
+        empty = fabric.SigCache()
+        n_eval = sum(p is not None for p in want_pol)
+        b3 = _lib.device_stats()[0]
+        _policy_results(block, identity_verify,
+                        lambda sd: fabric.preverify_sets(empty, [sd], min_batch=1),
+                        [o.status for o in got])
+        assert _lib.device_stats()[0] - b3 == n_eval

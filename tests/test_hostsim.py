@@ -228,19 +228,6 @@ def test_multi_device_shard_split(hs, n):
         assert ns.value == min(nd, (n + 63) // 64)
 
 
-# scalars at the Lim-Lee comb's edges (t teeth spaced s bits: 7 x 37 as
-# shipped): a single tooth, the top column empty or full, every column equal,
-# the last tooth's partial width, a lone column
-def _ll_u2(t, s):
-    top = 256 - s * (t - 1)  # bits of the last tooth
-    return [2**(s - 1), 2**s, 2**(2 * s), 2**(s * (t - 1)), 2**255,
-            2**(s * (t - 1)) + 2**(s * (t - 1) - 1), 2**s - 1,
-            sum(2**(s * k) for k in range(t)), sum(2**(s * k + s - 1) for k in range(t - 1)),
-            sum(2**(s * k + s - 1) for k in range(t - 1)) + 2**255,
-            (2**s - 1) << (256 - top - s), sum((2**s - 1) << (s * k) for k in range(t - 1))]
-
-
-
 @pytest.mark.parametrize("fused", [False, True])
 def test_hostsim_golden_llcomb(hs, golden, fused):
     """Per-batch Lim-Lee comb tables (lltab_build / q_llcomb: what the device
@@ -257,11 +244,17 @@ def test_hostsim_golden_llcomb(hs, golden, fused):
 
 
 def test_hostsim_p256_crafted_u2_llcomb(hs):
-    """The comb on crafted scalars (window edges and the comb's own: empty top
-    column, single teeth, full columns): every signature verifies, every
-    flipped-digest twin fails."""
+    """The signed comb on crafted scalars (odd / even u2, columns with the
+    lower teeth clear or set, a top tooth of zeros, the largest k, the Horner
+    doubling branch A == V_j) plus round 3's unsigned-comb edges and the
+    window edges: every signature verifies, every flipped-digest twin fails."""
+    from oracle import ecdsa_ref as O
+    from tests.comb_cases import horner_events, signed_comb_u2, unsigned_comb_u2
     sh = hs.hs_ll_shape()
-    recs = _p256_crafted_u2_records(_ll_u2(sh >> 8, sh & 0xFF))
+    t, s = sh >> 8, sh & 0xFF
+    u2s = signed_comb_u2(O.P256.n, t, s) + unsigned_comb_u2(6, 43) + unsigned_comb_u2(7, 37)
+    assert any(e[0] == "dbl" for u in u2s for e in horner_events(u, O.P256.n, t, s))
+    recs = _p256_crafted_u2_records(u2s)
     pub = np.frombuffer(b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big")
                                  for x, y, _, _ in recs), np.uint8)
     sigs, dgs = [t[2] for t in recs], [t[3] for t in recs]

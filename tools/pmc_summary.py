@@ -55,9 +55,19 @@ def main():
     with open(dst, "w") as f:
         json.dump(s, f, indent=1, sort_keys=True)
     if "--traffic" in sys.argv:
-        tr = {"source": f"{root} (rocprofv3 --pmc: FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU + "
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bdls_amd.provenance import build_info, kernel_src_sha
+        src = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--source=")), root)
+        bi = build_info()
+        if bi.get("kernel_src_sha") not in (None, kernel_src_sha()):
+            raise SystemExit("BUILD_INFO.json describes other kernel sources: rebuild first")
+        tr = {"source": f"{src} (rocprofv3 --pmc: FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU + "
                         f"GRBM_GUI_ACTIVE, separate passes)",
               "workload": tag,
+              # the kernel build these counters describe (bench.py refuses them
+              # for any other): hash of the kernel sources + the library's rev
+              "kernel_src_sha": kernel_src_sha(),
+              "git_rev": bi.get("git_rev"), "lib_sha256": bi.get("sha256"),
               "correction": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half "
                             "of 16-B/lane read bytes); WRITE_SIZE as reported",
               "kernels": {}}
