@@ -150,12 +150,15 @@ BH_HD size_t gpart_slots(size_t ns) {
 // G comb table: kGW-bit signed windows. Window w in [0, kCombWindows), entry
 // j in [0, kCombEntries): (j+1) * 2^(kGW w) * G, affine, canonical radix-2^30
 // Montgomery x (limbs 0..8) and y (limbs 9..17), padded to kGEntry words.
-// kGW = 10: 26 windows x 512 entries x 72 B = 958 KB per curve (L2-resident).
+// kGW = 13 (round 4): 20 windows x 4,096 entries x 72 B = 5.9 MB per curve
+// (L2 + MALL); same-box A/B at config 2 (profiles/r04/v4): HBM-resident
+// 140.0-142.5 M verifies/s at 10 bits (26 windows, 958 KB), 144.2-146.5 at 12,
+// 146.8-148.3 at 13, 147.2-148.2 at 14 (19 windows, 11.2 MB).
 #ifndef BH_GCOMB_BITS
-#define BH_GCOMB_BITS 10
+#define BH_GCOMB_BITS 13
 #endif
 constexpr int kGW = BH_GCOMB_BITS;
-static_assert(kGW >= 8 && kGW <= 12, "G comb window width");
+static_assert(kGW >= 8 && kGW <= 14, "G comb window width");
 // digits of k + M (M = sum 2^(kGW-1) 2^(kGW w)) minus 2^(kGW-1) are k's signed
 // digits in [-2^(kGW-1), 2^(kGW-1)); k < 2^256 needs kGW * windows >= 257.
 constexpr int kCombWindows = (257 + kGW - 1) / kGW;
@@ -606,7 +609,10 @@ BH_HD void recode_goff(uint32_t v[9], const uint32_t k[8]) {
 }
 
 // ---- shared tail: u1 G by the fixed-base comb, then A + B and the x check
-// u1 G: 8-bit signed windows over the L2-resident affine table (33 mixed adds).
+// u1 G: kGW-bit signed windows over the affine table (kCombWindows mixed
+// adds). The common step is one in-place mixed addition; a zero digit (odd
+// 2^-kGW per window), B still at infinity, and the degenerate additions of
+// crafted scalars take a side branch that the lanes skip together.
 template <class P>
 BH_HD void g_comb(J30& B, bool& b_inf, const uint32_t* gtab, const uint32_t u1[8]) {
   uint32_t one[9];
@@ -617,6 +623,7 @@ BH_HD void g_comb(J30& B, bool& b_inf, const uint32_t* gtab, const uint32_t u1[8
   f_copy(B.Z, one);
   uint32_t v[9];
   recode_goff(v, u1);
+#pragma unroll 1
   for (int win = 0; win < kCombWindows; win++) {
     const int d = (int)(v[0] & (2u * kCombEntries - 1u)) - kCombEntries;
     shr_const<kGW>(v);
@@ -630,31 +637,27 @@ BH_HD void g_comb(J30& B, bool& b_inf, const uint32_t* gtab, const uint32_t u1[8
       ty[k] = te[9 + k];
     }
     if (neg) f_neg<P, 64>(ty, ty);
-    J30 R;
-    bool same;
-    const bool deg = j_madd<P>(R, B, tx, ty, &same);
-    const bool take = mag != 0;
-    const bool use_t = take && b_inf;
-    const bool use_r = take && !b_inf && !deg;
-    const bool rare = take && !b_inf && deg;
-    j_sel(B, use_r, R, B);
-    if (use_t) {
-      f_copy(B.X, tx);
-      f_copy(B.Y, ty);
-      f_copy(B.Z, one);
-    }
-    if (rare) {
-      if (same) {
-        J30 Tj;
-        f_copy(Tj.X, tx);
-        f_copy(Tj.Y, ty);
-        f_copy(Tj.Z, one);
-        j_dbl<P>(B, Tj);
-      } else {
-        b_inf = true;
+    if (mag == 0u || b_inf) {  // zero digit: B unchanged; B at infinity: B = T
+      if (mag != 0u) {
+        f_copy(B.X, tx);
+        f_copy(B.Y, ty);
+        f_copy(B.Z, one);
+        b_inf = false;
+      }
+    } else {
+      bool same;
+      if (j_madd<P>(B, B, tx, ty, &same)) {  // rare: x(B) == x(T)
+        if (same) {
+          J30 Tj;
+          f_copy(Tj.X, tx);
+          f_copy(Tj.Y, ty);
+          f_copy(Tj.Z, one);
+          j_dbl<P>(B, Tj);
+        } else {
+          b_inf = true;
+        }
       }
     }
-    if (use_t) b_inf = false;
   }
 }
 

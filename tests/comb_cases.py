@@ -92,7 +92,23 @@ def unsigned_comb_u2(t: int, s: int) -> list[int]:
             (2**s - 1) << (256 - top - s), sum((2**s - 1) << (s * k) for k in range(t - 1))]
 
 
-def records_for_u2(curve, u2s, seed: int = 77, d: int | None = None, low_s: bool = False):
+def g_comb_u1(n: int, gw: int) -> list[int]:
+    """u1 at the edges of the kGW-bit signed-window G comb (verify.h g_comb):
+    zero windows (digit 0 keeps B), the most negative digit -2^(kGW-1) (the
+    table's last entry), all-ones windows (carries through the recoding),
+    single windows, n - 1."""
+    nw = -(-257 // gw)
+    half, full = 2**(gw - 1), 2**gw - 1
+    out = [1, 2, 3, n - 1, n - 2, n // 2, 2**gw, 2**(gw * (nw - 1)), 2**255,
+           sum(half << (gw * w) for w in range(nw - 1)) % n,          # every digit -2^(kGW-1)
+           sum(full << (gw * w) for w in range(nw - 1)) % n,          # carries all the way
+           sum((half if w % 2 else 0) << (gw * w) for w in range(nw - 1)) % n,
+           sum(1 << (gw * w) for w in range(0, nw - 1, 3)) % n]       # zero windows between
+    return [u % n for u in out if u % n]
+
+
+def records_for_u2(curve, u2s, seed: int = 77, d: int | None = None, low_s: bool = False,
+                   u1s=None):
     """One key; per u2 a valid signature and its flipped-digest twin:
     [(qx, qy, der_sig, digest)], the first verifying, the twin R_MATH. With
     low_s, u1 is redrawn until s <= n / 2, so the signature passes Fabric's
@@ -103,10 +119,16 @@ def records_for_u2(curve, u2s, seed: int = 77, d: int | None = None, low_s: bool
     d = d or rng.randrange(1, n)
     qx, qy = O.scalar_mult(c, d, (c.gx, c.gy))
     recs = []
-    for u2 in u2s:
+    for k, u2 in enumerate(u2s):
         u2Q = O.scalar_mult(c, u2 % n, (qx, qy))
-        for _ in range(64):
-            u1 = rng.randrange(1, n)
+        for tries in range(64):
+            if u1s:  # chosen u1: for low-S, redraw u2 instead
+                u1 = u1s[k % len(u1s)]
+                if tries:
+                    u2 = rng.randrange(1, n)
+                    u2Q = O.scalar_mult(c, u2, (qx, qy))
+            else:
+                u1 = rng.randrange(1, n)
             R = O.point_add(c, O.scalar_mult(c, u1, (c.gx, c.gy)), u2Q)
             if R is None or R[0] % n == 0:
                 continue

@@ -37,6 +37,8 @@ static int g_ll = 0;
 extern "C" void hs_set_ll(int on) { g_ll = on; }
 // the comb's shape as built (teeth << 8 | spacing), for the crafted-scalar tests
 extern "C" uint32_t hs_ll_shape() { return ((uint32_t)kLLTeeth << 8) | (uint32_t)kLLSpace; }
+// the G comb's window width as built (BH_GCOMB_BITS)
+extern "C" uint32_t hs_gcomb_bits() { return (uint32_t)kGW; }
 
 template <class P, int L>
 static bool wide_keycomb(const Work& w, const uint32_t* gtab, uint32_t i, const uint32_t* tab) {

@@ -29,7 +29,7 @@ import pytest
 from bdls_amd import _lib, workload
 from oracle import ecdsa_ref as O
 from oracle import orc
-from tests.comb_cases import records_for_u2, signed_comb_u2, unsigned_comb_u2
+from tests.comb_cases import g_comb_u1, records_for_u2, signed_comb_u2, unsigned_comb_u2
 
 pytestmark = pytest.mark.gpu
 
@@ -91,6 +91,13 @@ def p256_edge_batch(golden):
         + _window_edge_u2(c.n)
     crafted = records_for_u2(c, u2s, seed=91, low_s=True)
     assert len(crafted) >= 2 * 60
+    # the u1 G comb's edges (zero digits, most negative digit, carries) at
+    # every window width the library may be built with
+    import random
+    u1s = [u for gw in (10, 11, 12, 13, 14) for u in g_comb_u1(c.n, gw)]
+    rng = random.Random(5)
+    crafted += records_for_u2(c, [rng.randrange(1, c.n) for _ in u1s], seed=92, low_s=True,
+                              u1s=u1s)
     for qx, qy, sig, dg in crafted:
         for _ in range(4):
             recs.append((qx.to_bytes(32, "big") + qy.to_bytes(32, "big"), sig, dg))

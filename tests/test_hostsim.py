@@ -151,7 +151,7 @@ def test_hostsim_two_span_messages(hs, family):
     assert (l1 == 0).any() and (l2 == 0).any() and ((l1 > 64) & (l2 > 64)).any()
 
 
-def _p256_crafted_u2_records(extra=()):
+def _p256_crafted_u2_records(extra=(), u1s=None):
     """P-256 signatures built for chosen u2 at key-table window boundaries
     (digit carries of the carry-scan recoding, the offset recoding's borrow
     edges, the top window, n - 1, n/2) -- R = u1 G + u2 Q, r = x(R) mod n,
@@ -168,8 +168,8 @@ def _p256_crafted_u2_records(extra=()):
            sum(9 * 16**k for k in range(64)) % n, sum(7 * 16**k for k in range(64)) % n]
     u2s += [rng.randrange(1, n) for _ in range(6)] + list(extra)
     recs = []
-    for u2 in u2s:
-        u1 = rng.randrange(1, n)
+    for k, u2 in enumerate(u2s):
+        u1 = u1s[k % len(u1s)] if u1s else rng.randrange(1, n)
         R = O.point_add(c, O.scalar_mult(c, u1, (c.gx, c.gy)), O.scalar_mult(c, u2, (qx, qy)))
         if R is None or R[0] % n == 0:
             continue
@@ -267,6 +267,41 @@ def test_hostsim_p256_crafted_u2_llcomb(hs):
     out = np.zeros(len(recs), np.uint8)
     ncomb = ctypes.c_uint32()
     hs.hs_set_ll(1)
+    try:
+        hs.hs_verify2(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
+                      dg.ctypes.data, do.ctypes.data, dl.ctypes.data, len(recs), 2, 4, 1,
+                      out.ctypes.data, ctypes.byref(ncomb))
+    finally:
+        hs.hs_set_ll(0)
+    assert ncomb.value > 0
+    assert [int(o) for o in out[0::2]] == [0] * (len(recs) // 2)
+    assert all(int(o) == 9 for o in out[1::2])
+
+
+@pytest.mark.parametrize("ll", [0, 1])
+def test_hostsim_g_comb_crafted_u1(hs, ll):
+    """The u1 G comb (g_comb: zero digits skip, B at infinity takes T, the
+    most negative digit reads the table's last entry) on crafted u1, through
+    the split key-table route (stage_gpart) with both table kinds: every
+    signature verifies, every flipped-digest twin fails."""
+    from oracle import ecdsa_ref as O
+    from tests.comb_cases import g_comb_u1
+    gw = hs.hs_gcomb_bits()
+    u1s = g_comb_u1(O.P256.n, gw)
+    rng = __import__("random").Random(3)
+    recs = _p256_crafted_u2_records([rng.randrange(1, O.P256.n) for _ in range(len(u1s))], u1s)
+    pub = np.frombuffer(b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big")
+                                 for x, y, _, _ in recs), np.uint8)
+    sigs, dgs = [t[2] for t in recs], [t[3] for t in recs]
+    sl = np.array([len(x) for x in sigs], np.uint32)
+    dl = np.array([len(x) for x in dgs], np.uint32)
+    so = np.concatenate([[0], np.cumsum(sl[:-1])]).astype(np.uint64)
+    do = np.concatenate([[0], np.cumsum(dl[:-1])]).astype(np.uint64)
+    sig = np.frombuffer(b"".join(sigs), np.uint8)
+    dg = np.frombuffer(b"".join(dgs), np.uint8)
+    out = np.zeros(len(recs), np.uint8)
+    ncomb = ctypes.c_uint32()
+    hs.hs_set_ll(ll)
     try:
         hs.hs_verify2(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
                       dg.ctypes.data, do.ctypes.data, dl.ctypes.data, len(recs), 2, 4, 1,

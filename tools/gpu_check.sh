@@ -19,8 +19,8 @@ for s in $STEPS; do
     lat)    for c in 3 4; do timeout -k 10 300 python -u bench.py --config $c --steps ${LAT_STEPS:-30} --warmup 3 > gpurun_out/lat$c.json 2> gpurun_out/lat$c.err; rc=$?; cat gpurun_out/lat$c.json; tail -3 gpurun_out/lat$c.err; case $rc in 0|3) ;; *) echo "STOP after lat$c (exit $rc)"; exit $rc ;; esac; done ;;
     hostinfo) (nproc; python -c "import os; print(os.cpu_count(), len(os.sched_getaffinity(0)))"; cat /sys/fs/cgroup/cpu.max 2>/dev/null; lscpu | head -20) > gpurun_out/hostinfo.txt 2>&1; cat gpurun_out/hostinfo.txt ;;
     bench)  timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err; ok_or_stop $rc bench ;;
-    prof)   export TMPDIR=/tmp; timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1; rc=$?; tail -3 gpurun_out/prof.log; ok_or_stop $rc prof ;;
-    exp)    for pass in 1 2; do for so in bdls_amd/lib/libbdlship.so exp/libbdlship_*.so; do v=$(basename $so .so); BDLS_HIP_LIB=$PWD/$so timeout -k 10 300 python bench.py --steps ${EXP_STEPS:-20} --warmup 3 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/exp_${v}_p$pass.json 2> gpurun_out/exp_${v}_p$pass.err; rc=$?; echo "$v pass $pass rc=$rc"; case $rc in 0|3) ;; *) echo "STOP after exp $v (exit $rc)"; exit $rc ;; esac; done; done ;;
+    prof)   export TMPDIR=/tmp; timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ${BENCH_ARGS:-} > gpurun_out/prof_bench.json 2> gpurun_out/prof.log; rc=$?; tail -3 gpurun_out/prof.log; ok_or_stop $rc prof; python3 tools/prof_check.py gpurun_out/prof/run_kernel_trace.csv gpurun_out/prof_bench.json gpurun_out/prof_check.json ;;
+    exp)    for pass in $(seq ${EXP_PASSES:-2}); do for so in bdls_amd/lib/libbdlship.so exp/libbdlship_*.so; do v=$(basename $so .so); BDLS_HIP_LIB=$PWD/$so timeout -k 10 300 python bench.py --steps ${EXP_STEPS:-20} --warmup 3 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/exp_${v}_p$pass.json 2> gpurun_out/exp_${v}_p$pass.err; rc=$?; echo "$v pass $pass rc=$rc"; case $rc in 0|3) ;; *) echo "STOP after exp $v (exit $rc)"; exit $rc ;; esac; done; done ;;
     lanes1) BH_LANES=1 timeout -k 10 600 python bench.py --steps ${EXP_STEPS:-20} --warmup 2 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/bench_lanes1.json 2> gpurun_out/bench_lanes1.err; rc=$?; cat gpurun_out/bench_lanes1.json; ok_or_stop $rc lanes1 ;;
     nostagger) BH_LANE_STAGGER=0 timeout -k 10 600 python bench.py --steps ${EXP_STEPS:-20} --warmup 2 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/bench_nostagger.json 2> gpurun_out/bench_nostagger.err; rc=$?; cat gpurun_out/bench_nostagger.json; ok_or_stop $rc nostagger ;;
     noll) BH_LL=0 timeout -k 10 600 python bench.py --steps ${EXP_STEPS:-20} --warmup 2 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/bench_noll.json 2> gpurun_out/bench_noll.err; rc=$?; cat gpurun_out/bench_noll.json; ok_or_stop $rc noll ;;

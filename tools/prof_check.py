@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Tie bench.py's roofline to rocprofv3: the dominant kernel's per-dispatch
+durations from a `rocprofv3 --kernel-trace --stats` run of the same bench
+command, split by bench phase, against the line's `roofline.launch_ms`.
+
+usage: python tools/prof_check.py <kernel_trace.csv> <bench.json> <out.json>
+
+The bench runs, in order: the host path (warmup + 1 single + K timed batches,
+two compute lanes, so a kernel may share the GPU with the other lane's), then
+the HBM-resident passes (warmup + K timed, serialised), then the side
+configs (config 5's rank shard launches the one-lane kernels with no key-comb
+records: short dispatches). bench.py takes launch_ms from HIP events over the
+K timed resident passes: dispatches [2W + 1 + K, 2W + 1 + 2K) of the kernel in
+launch order. rocprof's --stats average mixes every phase.
+"""
+import csv
+import json
+import sys
+
+
+def main():
+    trace, bench, dst = sys.argv[1:4]
+    b = json.load(open(bench))
+    k = b["roofline"]["kernel"]
+    steps, warm = b["steps"], b["warmup"]
+    rows = [r for r in csv.DictReader(open(trace))
+            if f"::{k}<bh::F30_p256>" in r["Kernel_Name"] or
+            r["Kernel_Name"].startswith(f"void (anonymous namespace)::{k}<bh::F30_p256>")]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
+    host_n = warm + 1 + steps
+    lo = host_n + warm
+    timed = d[lo:lo + steps]
+    out = {
+        "kernel": k, "dispatches": len(d),
+        "all_dispatch_mean_ms": round(sum(d) / len(d), 4) if d else None,
+        "host_path_mean_ms": round(sum(d[:host_n]) / max(1, len(d[:host_n])), 4),
+        "resident_timed_mean_ms": round(sum(timed) / steps, 4) if len(timed) == steps else None,
+        "resident_timed_dispatches": [lo, lo + steps],
+        "bench_launch_ms": b["roofline"]["launch_ms"],
+        "bench_frac": b["roofline"]["frac"],
+    }
+    if out["resident_timed_mean_ms"]:
+        out["agreement"] = round(out["resident_timed_mean_ms"] / out["bench_launch_ms"], 4)
+        out["frac_from_rocprof"] = round(b["roofline"]["frac"] * out["bench_launch_ms"]
+                                         / out["resident_timed_mean_ms"], 4)
+    out["note"] = ("phases by dispatch order: host path = first warmup + 1 + steps dispatches "
+                   "(two lanes: durations include the other lane's kernels), then warmup + "
+                   "steps resident passes, the last `steps` of them timed; bench_launch_ms = "
+                   "HIP events over the same timed resident passes")
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
