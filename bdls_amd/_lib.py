@@ -32,6 +32,7 @@ EXPORTS = (
     "bh_fabric_block_preverify", "bh_verify_x509", "bh_signature_sets_verify",
     "bh_envelopes_preverify", "bh_block_signatures_preverify",
     "bh_block_signatures_preverify_bft", "bh_fabric_block_preverify_refs", "bh_device_stats",
+    "bh_verify_compact", "bh_verify_compact_submit",
 )
 KEY_FULL = 255  # bh_keys_register status: registry full
 
@@ -46,6 +47,15 @@ class BhBatch(ctypes.Structure):
         ("msg_off", ctypes.c_void_p),
         ("msg_len", ctypes.c_void_p),
     ]
+
+
+class BhCBatch(ctypes.Structure):
+    """include/bdls_hip.h bh_cbatch: the compact host layout (distinct keys +
+    u32 indices, lengths only, optional fixed message stride)."""
+    _fields_ = [("keys", ctypes.c_void_p), ("key_idx", ctypes.c_void_p),
+                ("nkeys", ctypes.c_size_t), ("sig", ctypes.c_void_p),
+                ("sig_len", ctypes.c_void_p), ("msg", ctypes.c_void_p),
+                ("msg_len", ctypes.c_void_p), ("msg_stride", ctypes.c_uint32)]
 
 
 class BhBdlsBatch(ctypes.Structure):
@@ -146,6 +156,14 @@ def lib() -> ctypes.CDLL:
         L.bh_verify_submit.restype = i32
         L.bh_verify_wait.argtypes = [vp]
         L.bh_verify_wait.restype = i32
+        try:  # (an A/B run may load a library built before these entry points)
+            L.bh_verify_compact.argtypes = [i32, ctypes.POINTER(BhCBatch), sz, u32, vp, vp]
+            L.bh_verify_compact.restype = i32
+            L.bh_verify_compact_submit.argtypes = [i32, ctypes.POINTER(BhCBatch), sz, u32, vp, vp,
+                                                   ctypes.POINTER(vp)]
+            L.bh_verify_compact_submit.restype = i32
+        except AttributeError:
+            pass
         L.bh_host_alloc.argtypes = [sz, ctypes.POINTER(vp)]
         L.bh_host_alloc.restype = i32
         L.bh_host_free.argtypes = [vp]
@@ -316,3 +334,46 @@ def device_stats() -> tuple[int, int]:
     out = _np.zeros(2, _np.uint64)
     check(lib().bh_device_stats(out.ctypes.data))
     return int(out[0]), int(out[1])
+
+
+def compact_layout(pub, sig, sig_off, sig_len, msg, msg_off, msg_len, dedup: bool = True,
+                   stride: bool = True, alloc=None):
+    """The bh_cbatch arrays of a bh_batch (numpy): distinct keys + u32 indices
+    (dedup), signatures and messages re-packed in record order with lengths
+    only, msg_len dropped when every message has one length (stride).
+    Returns (dict of arrays, BhCBatch)."""
+    import numpy as np
+    n = len(sig_len)
+    mk = alloc or (lambda nb: np.empty(nb, np.uint8))
+
+    def arr(a, dtype):
+        out = mk(a.nbytes).view(dtype)
+        out[:] = a
+        return out
+    keys64 = np.ascontiguousarray(pub[:64 * n]).reshape(n, 64)
+    if dedup:
+        uk, idx = np.unique(keys64, axis=0, return_inverse=True)
+        keys = arr(np.ascontiguousarray(uk).reshape(-1), np.uint8)
+        key_idx = arr(idx.astype(np.uint32).reshape(-1), np.uint32)
+    else:
+        keys, key_idx = arr(keys64.reshape(-1), np.uint8), None
+
+    def repack(buf, off, ln):
+        total = int(ln.sum(dtype=np.uint64))
+        if n and (np.diff(off.astype(np.int64)) == ln[:-1].astype(np.int64)).all():
+            return buf[int(off[0]):int(off[0]) + total]
+        ex = np.zeros(n, np.int64)
+        ex[1:] = np.cumsum(ln[:-1], dtype=np.int64)
+        idx = np.repeat(off.astype(np.int64) - ex, ln.astype(np.int64)) + np.arange(total)
+        return buf[idx]
+    s_b = arr(repack(sig, sig_off, sig_len), np.uint8)
+    m_b = arr(repack(msg, msg_off, msg_len), np.uint8)
+    fixed = stride and n > 0 and (msg_len == msg_len[0]).all()
+    out = {"keys": keys, "key_idx": key_idx, "sig": s_b, "sig_len": arr(sig_len, np.uint32),
+           "msg": m_b, "msg_len": None if fixed else arr(msg_len, np.uint32)}
+    cb = BhCBatch(keys.ctypes.data, key_idx.ctypes.data if key_idx is not None else None,
+                  len(keys) // 64, s_b.ctypes.data if s_b.nbytes else None,
+                  out["sig_len"].ctypes.data, m_b.ctypes.data if m_b.nbytes else None,
+                  out["msg_len"].ctypes.data if out["msg_len"] is not None else None,
+                  int(msg_len[0]) if fixed else 0)
+    return out, cb

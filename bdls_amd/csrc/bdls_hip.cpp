@@ -43,6 +43,11 @@ hipError_t launch_small(int curve, const BatchIn& in, const Work& w, const KeyRe
                         uint32_t bs);
 hipError_t launch_register(int curve, const uint8_t* pub, const Work& w, const Plan& pl,
                            const KeyReg& g, uint32_t n, uint8_t* status, hipStream_t s);
+size_t expand_temp_bytes(uint32_t m);
+hipError_t launch_expand(const uint8_t* keys, const uint32_t* key_idx, uint8_t* pub,
+                         const uint32_t* sig_len, uint64_t* sig_off, const uint32_t* msg_len,
+                         uint64_t* msg_off, uint32_t* msg_len_out, uint32_t stride, void* temp,
+                         size_t temp_bytes, uint32_t m, hipStream_t s);
 }  // namespace bh
 
 namespace {
@@ -717,6 +722,89 @@ bh_bdls_batch upload(Uploader& u, const bh_bdls_batch* b, size_t lo, size_t m,
   return d;
 }
 
+// Compact host batches (bh_verify_compact, include/bdls_hip.h bh_cbatch): the
+// distinct keys once + u32 indices, lengths only. Staged as they come; the
+// device then expands them into an ordinary bh_batch (bh::launch_expand) on
+// the compute stream, ahead of the verify passes.
+struct CompactHost {
+  bh_cbatch c;
+};
+struct CompactDev {
+  bh_batch b;  // the expanded batch (device pointers)
+  const uint8_t* keys = nullptr;
+  const uint32_t* key_idx = nullptr;
+  const uint32_t* sig_len = nullptr;
+  const uint32_t* msg_len = nullptr;
+  uint8_t* pub = nullptr;
+  uint64_t* sig_off = nullptr;
+  uint64_t* msg_off = nullptr;
+  uint32_t* msg_len_out = nullptr;
+  uint32_t stride = 0;
+  void* temp = nullptr;
+  size_t temp_bytes = 0;
+};
+
+// the staging bytes of a compact shard, in Uploader::put's rounding, with the
+// shard's first signature / message byte (sums of the lengths before lo)
+HostFields fields(const CompactHost* h, size_t lo, size_t m) {
+  const bh_cbatch& c = h->c;
+  HostFields f;
+  uint64_t s0 = 0, s1 = 0, m0 = 0, m1 = 0;
+  for (size_t i = 0; i < lo; i++) s0 += c.sig_len[i];
+  for (size_t i = lo; i < lo + m; i++) s1 += c.sig_len[i];
+  if (c.msg_len) {
+    for (size_t i = 0; i < lo; i++) m0 += c.msg_len[i];
+    for (size_t i = lo; i < lo + m; i++) m1 += c.msg_len[i];
+  } else {
+    m0 = (uint64_t)lo * c.msg_stride;
+    m1 = (uint64_t)m * c.msg_stride;
+  }
+  f.var.push_back(VarField{s0, s1});
+  f.var.push_back(VarField{m0, m1});
+  auto r = [](size_t b) { return round256(b + 1); };
+  f.bytes = r(c.key_idx ? c.nkeys * 64 : m * 64) + (c.key_idx ? r(m * 4) + r(m * 64) : 0) +
+            r(s1) + r(m * 4) + r(m1) + r(m * 4) + 2 * r(m * 8) +
+            r(bh::expand_temp_bytes((uint32_t)m));
+  return f;
+}
+
+CompactDev upload(Uploader& u, const CompactHost* h, size_t lo, size_t m, const HostFields& f) {
+  const bh_cbatch& c = h->c;
+  CompactDev d;
+  d.keys = c.key_idx ? u.put(c.keys, c.nkeys * 64) : u.put(c.keys + lo * 64, m * 64);
+  d.key_idx = c.key_idx ? u.put(c.key_idx + lo, m) : nullptr;
+  const uint8_t* sig = u.put<uint8_t>(c.sig ? c.sig + f.var[0].lo : nullptr, f.var[0].bytes);
+  d.sig_len = u.put(c.sig_len + lo, m);
+  const uint8_t* msg = u.put<uint8_t>(c.msg ? c.msg + f.var[1].lo : nullptr, f.var[1].bytes);
+  d.msg_len = c.msg_len ? u.put(c.msg_len + lo, m) : nullptr;
+  d.msg_len_out = c.msg_len ? nullptr : const_cast<uint32_t*>(u.put<uint32_t>(nullptr, m));
+  d.pub = c.key_idx ? const_cast<uint8_t*>(u.put<uint8_t>(nullptr, m * 64)) : nullptr;
+  d.sig_off = const_cast<uint64_t*>(u.put<uint64_t>(nullptr, m));
+  d.msg_off = const_cast<uint64_t*>(u.put<uint64_t>(nullptr, m));
+  d.temp_bytes = bh::expand_temp_bytes((uint32_t)m);
+  d.temp = const_cast<uint8_t*>(u.put<uint8_t>(nullptr, d.temp_bytes));
+  d.stride = c.msg_stride;
+  d.b = bh_batch{c.key_idx ? d.pub : d.keys, sig, d.sig_off, d.sig_len, msg, d.msg_off,
+                 c.msg_len ? d.msg_len : d.msg_len_out};
+  return d;
+}
+
+// device-side preparation of an uploaded shard: compact batches expand, the
+// other kinds are ready as staged
+hipError_t expand_dev(const CompactDev& d, size_t m, hipStream_t s) {
+  return bh::launch_expand(d.keys, d.key_idx, d.pub, d.sig_len, d.sig_off, d.msg_len, d.msg_off,
+                           d.msg_len_out, d.stride, d.temp, d.temp_bytes, (uint32_t)m, s);
+}
+template <class T>
+hipError_t expand_dev(const T&, size_t, hipStream_t) {
+  return hipSuccess;
+}
+const bh_batch* dev_batch(const CompactDev& d) { return &d.b; }
+template <class T>
+const T* dev_batch(const T& d) {
+  return &d;
+}
+
 struct Part {
   Dev* d;
   int slot;
@@ -785,7 +873,7 @@ int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, 
   if ((rc = sl.out.ensure(out_bytes))) return rc;
   if ((rc = sl.host_out.ensure(out_bytes))) return rc;
   Uploader u{(char*)sl.stage.p, d.copy};
-  const B db = upload(u, b, lo, m, f);
+  const auto db = upload(u, b, lo, m, f);
   HIPCHK(u.err);
   HIPCHK(hipEventRecord(sl.uploaded, d.copy));
   // alternate the compute lanes (BH_LANES=1: lane 0 only); registry writers
@@ -793,9 +881,10 @@ int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, 
   const int lane = (flags & BH_F_KEEP_KEYS) ? -1 : (int)(d.next_lane++ % lanes());
   hipStream_t s = lane == 1 ? d.l1.stream : d.stream;
   HIPCHK(hipStreamWaitEvent(s, sl.uploaded, 0));
+  HIPCHK(expand_dev(db, m, s));
   uint64_t* dbm = (uint64_t*)sl.out.p;
   uint8_t* drs = (uint8_t*)(dbm + round64(m) / 64);
-  if ((rc = run_dev(d, curve, &db, m, flags, dbm, drs, s, nullptr, lane))) return rc;
+  if ((rc = run_dev(d, curve, dev_batch(db), m, flags, dbm, drs, s, nullptr, lane))) return rc;
   HIPCHK(hipMemcpyAsync(sl.host_out.p, dbm, round64(m) / 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync((uint8_t*)sl.host_out.p + round64(m) / 8, drs, m,
                         hipMemcpyDeviceToHost, s));
@@ -822,6 +911,7 @@ bool small_ok(int curve, const bh_batch* b, size_t n, uint32_t flags) {
 }
 bool small_ok(int, const SegBatch*, size_t, uint32_t) { return false; }
 bool small_ok(int, const bh_bdls_batch*, size_t, uint32_t) { return false; }
+bool small_ok(int, const CompactHost*, size_t, uint32_t) { return false; }
 
 int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, size_t m,
                   uint32_t flags) {
@@ -1403,6 +1493,45 @@ int bh_verify_submit(int curve, const bh_batch* b, size_t n, uint32_t flags, uin
   if (int rc = check_flags(flags)) return rc;
   if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
   return submit_job(curve, b, n, flags, bitmap, reason, job);
+}
+
+// bh_cbatch checks: required fields, key indices in range (one host pass)
+static int check_compact(const bh_cbatch* b, size_t n, const uint8_t* bitmap,
+                         const uint8_t* reason) {
+  if (!b) return fail(BH_E_INVALID, "null batch");
+  if (!n) return BH_OK;
+  if (!b->keys || !b->sig_len || !bitmap || !reason)
+    return fail(BH_E_INVALID, "null pointer in batch");
+  if (b->key_idx) {
+    if (!b->nkeys || b->nkeys > 0xffffffffull) return fail(BH_E_INVALID, "bad nkeys");
+    uint32_t mx = 0;
+    for (size_t i = 0; i < n; i++) mx = std::max(mx, b->key_idx[i]);
+    if (mx >= b->nkeys) return fail(BH_E_INVALID, "key index out of range");
+  }
+  return BH_OK;
+}
+
+int bh_verify_compact(int curve, const bh_cbatch* b, size_t n, uint32_t flags, uint8_t* bitmap,
+                      uint8_t* reason) {
+  if (curve != BH_CURVE_P256) return fail(BH_E_INVALID, "curve not supported by bh_verify_compact");
+  if (int rc = check_flags(flags)) return rc;
+  if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
+  if (int rc = check_compact(b, n, bitmap, reason)) return rc;
+  const CompactHost h{*b};
+  return host_verify(curve, &h, n, flags, bitmap, reason);
+}
+
+int bh_verify_compact_submit(int curve, const bh_cbatch* b, size_t n, uint32_t flags,
+                             uint8_t* bitmap, uint8_t* reason, bh_job** job) {
+  if (!job) return fail(BH_E_INVALID, "null job");
+  *job = nullptr;
+  if (curve != BH_CURVE_P256)
+    return fail(BH_E_INVALID, "curve not supported by bh_verify_compact_submit");
+  if (int rc = check_flags(flags)) return rc;
+  if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
+  if (int rc = check_compact(b, n, bitmap, reason)) return rc;
+  const CompactHost h{*b};
+  return submit_job(curve, &h, n, flags, bitmap, reason, job);
 }
 
 int bh_verify_wait(bh_job* job) {

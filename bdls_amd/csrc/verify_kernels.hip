@@ -24,6 +24,7 @@
 // butterfly, x check) after it.
 // plus k_gtab_build once per device at bh_init (fixed-base comb table for G)
 // and k_reg_prep / k_reg_status for bh_keys_register.
+#include <algorithm>
 #include <type_traits>
 
 #include <hipcub/hipcub.hpp>
@@ -703,6 +704,67 @@ __global__ __launch_bounds__(256) void k_reg_status(Work w, Plan pl, uint32_t n,
 // Launchers (C++ linkage, used by bdls_hip.cpp)
 namespace bh {
 
+// ---- compact host batches (bh_verify_compact): expansion on the device ----
+// pub[i] = keys[key_idx[i]] (64 B), and the u64 offsets as exclusive prefix
+// sums of the u32 lengths (or i * stride with a fixed message length), so the
+// verify passes read an ordinary bh_batch. Runs on the compute stream after
+// the upload; key indices were range-checked on the host.
+__global__ __launch_bounds__(256) void k_expand_keys(const uint8_t* __restrict__ keys,
+                                                     const uint32_t* __restrict__ idx,
+                                                     uint8_t* __restrict__ pub, uint32_t m) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint4* src = reinterpret_cast<const uint4*>(keys + (size_t)idx[i] * 64);
+  uint4* dst = reinterpret_cast<uint4*>(pub + (size_t)i * 64);
+  const uint4 a = src[0], b = src[1], c = src[2], d = src[3];
+  dst[0] = a;
+  dst[1] = b;
+  dst[2] = c;
+  dst[3] = d;
+}
+
+__global__ __launch_bounds__(256) void k_stride_offsets(uint64_t* __restrict__ off,
+                                                        uint32_t* __restrict__ len,
+                                                        uint32_t stride, uint32_t m) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  off[i] = (uint64_t)i * stride;
+  len[i] = stride;
+}
+
+struct ToU64 {
+  __host__ __device__ uint64_t operator()(uint32_t x) const { return x; }
+};
+
+size_t expand_temp_bytes(uint32_t m) {
+  size_t t = 0;
+  hipcub::TransformInputIterator<uint64_t, ToU64, const uint32_t*> it(nullptr, ToU64());
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, t, it, (uint64_t*)nullptr, (int)m) != hipSuccess)
+    return 0;
+  return t;
+}
+
+hipError_t launch_expand(const uint8_t* keys, const uint32_t* key_idx, uint8_t* pub,
+                         const uint32_t* sig_len, uint64_t* sig_off, const uint32_t* msg_len,
+                         uint64_t* msg_off, uint32_t* msg_len_out, uint32_t stride, void* temp,
+                         size_t temp_bytes, uint32_t m, hipStream_t s) {
+  if (!m) return hipSuccess;
+  const dim3 grd((m + 255) / 256), blk(256);
+  if (key_idx) hipLaunchKernelGGL(k_expand_keys, grd, blk, 0, s, keys, key_idx, pub, m);
+  hipError_t e;
+  size_t t = temp_bytes;
+  hipcub::TransformInputIterator<uint64_t, ToU64, const uint32_t*> sl(sig_len, ToU64());
+  if ((e = hipcub::DeviceScan::ExclusiveSum(temp, t, sl, sig_off, (int)m, s))) return e;
+  if (msg_len) {
+    t = temp_bytes;
+    hipcub::TransformInputIterator<uint64_t, ToU64, const uint32_t*> ml(msg_len, ToU64());
+    if ((e = hipcub::DeviceScan::ExclusiveSum(temp, t, ml, msg_off, (int)m, s))) return e;
+  } else {
+    hipLaunchKernelGGL(k_stride_offsets, grd, blk, 0, s, msg_off, msg_len_out, stride, m);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s) {
   const int nt = kCombWindows * kCombEntries;
   if (curve == 0)
@@ -724,13 +786,30 @@ static void launch_key_count(const Work& w, const Plan& pl, const uint8_t* pub, 
     hipLaunchKernelGGL(k_key_count<false>, grd, blk, 0, s, w, pl, pub, n);
 }
 
+// The dedup table's reset (slot_hash 0, slot_rep / slot_tab kNone, slot_cnt 0,
+// the counters 0) in ONE launch: 16-byte stores, a grid-stride loop over the
+// hc / 4 quads (hc is a power of two >= 256) -- instead of five memset
+// kernels, each with its own launch gap (round 4).
+__global__ __launch_bounds__(256) void k_plan_reset(Plan pl) {
+  const uint32_t nq = pl.hc / 4u;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += stride) {
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u), f = make_uint4(kNone, kNone, kNone, kNone);
+    reinterpret_cast<uint4*>(pl.slot_hash)[2u * q] = z;
+    reinterpret_cast<uint4*>(pl.slot_hash)[2u * q + 1u] = z;
+    reinterpret_cast<uint4*>(pl.slot_rep)[q] = f;
+    reinterpret_cast<uint4*>(pl.slot_cnt)[q] = z;
+    reinterpret_cast<uint4*>(pl.slot_tab)[q] = f;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 4) pl.counters[threadIdx.x] = 0u;
+}
+
 static hipError_t plan_reset(const Plan& pl, hipStream_t s) {
-  hipError_t e;
-  if ((e = hipMemsetAsync(pl.slot_hash, 0, (size_t)pl.hc * 8, s))) return e;
-  if ((e = hipMemsetAsync(pl.slot_rep, 0xff, (size_t)pl.hc * 4, s))) return e;
-  if ((e = hipMemsetAsync(pl.slot_cnt, 0, (size_t)pl.hc * 4, s))) return e;
-  if ((e = hipMemsetAsync(pl.slot_tab, 0xff, (size_t)pl.hc * 4, s))) return e;
-  return hipMemsetAsync(pl.counters, 0, 16, s);
+  // (carve_work takes every plan array at a 256-byte boundary, hc >= 256)
+  const uint32_t nq = pl.hc / 4u;
+  hipLaunchKernelGGL(k_plan_reset, dim3(std::min<uint32_t>((nq + 255) / 256, 2048)), dim3(256),
+                     0, s, pl);
+  return hipGetLastError();
 }
 
 // Group the comb list by table id so the (on average 16) records of one key

@@ -111,6 +111,9 @@ def parse(argv=None):
     ap.add_argument("--msg-len", type=int, default=256)
     ap.add_argument("--corrupt-den", type=int, default=16)
     ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--host-layout", choices=["compact", "plain"], default="compact",
+                    help="host path input layout: bh_cbatch (distinct keys + u32 indices, "
+                         "lengths only) or bh_batch (per-record keys, u64 offsets)")
     ap.add_argument("--hbm-resident", type=int, default=1,
                     help="also time the same passes on inputs already in HBM")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0")
@@ -483,7 +486,8 @@ def load_counters(config: int, n_rank: int):
     equal the hash of the kernel sources beside the library (bdls_amd/
     provenance.py); otherwise the counters are stale and not printed.
     Returns (source, kernels, stale_reason)."""
-    from bdls_amd.provenance import kernel_src_sha
+    from bdls_amd import _lib
+    from bdls_amd.provenance import lib_kernel_sha
     prof = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(prof):
         return None, {}, "no profiles/traffic.json"
@@ -492,10 +496,12 @@ def load_counters(config: int, n_rank: int):
     want = f"config{config}:n{n_rank}"
     if tr.get("workload") != want:
         return None, {}, f"counters taken on {tr.get('workload')}, not {want}"
-    cur = kernel_src_sha()
+    cur = lib_kernel_sha(_lib.LIB_PATH)
+    if cur is None:
+        return None, {}, "the loaded library has no build record (bdls_amd/lib/BUILD_INFO.json)"
     if tr.get("kernel_src_sha") != cur:
         return None, {}, (f"stale: counters describe kernel sources {tr.get('kernel_src_sha')} "
-                          f"(rev {tr.get('git_rev')}), this build is {cur}")
+                          f"(rev {tr.get('git_rev')}), this library was built from {cur}")
     return (f"{tr.get('source')} @ rev {tr.get('git_rev')}, kernel_src_sha {cur}",
             tr.get("kernels", {}), None)
 
@@ -578,14 +584,24 @@ def bench_throughput(a, rank, world, local):
     flags = _lib.BH_F_HASH_SHA256
     hb = _lib.BhBatch(*[x.ctypes.data for x in (w.pub, w.sig, w.sig_off, w.sig_len, w.msg,
                                                 w.msg_off, w.msg_len)])
+    compact = a.host_layout == "compact"
+    if compact:
+        # what a Go BatchVerify hands over: each distinct key once + a u32
+        # index per record, lengths only (fixed 256-byte messages: none)
+        carrs, cb = _lib.compact_layout(w.pub, w.sig, w.sig_off, w.sig_len, w.msg, w.msg_off,
+                                        w.msg_len, alloc=alloc)
     depth = 3  # batches in flight (the library keeps 3 pipeline slots per device)
     outs = [(np.zeros((n + 7) // 8, np.uint8), np.zeros(n, np.uint8)) for _ in range(depth)]
 
     def submit(k):
         job = ctypes.c_void_p()
         bm, rs = outs[k % depth]
-        _lib.check(L.bh_verify_submit(0, ctypes.byref(hb), n, flags, bm.ctypes.data,
-                                      rs.ctypes.data, ctypes.byref(job)))
+        if compact:
+            _lib.check(L.bh_verify_compact_submit(0, ctypes.byref(cb), n, flags, bm.ctypes.data,
+                                                  rs.ctypes.data, ctypes.byref(job)))
+        else:
+            _lib.check(L.bh_verify_submit(0, ctypes.byref(hb), n, flags, bm.ctypes.data,
+                                          rs.ctypes.data, ctypes.byref(job)))
         return job
 
     def run_host(steps):
@@ -613,8 +629,11 @@ def bench_throughput(a, rank, world, local):
     _lib.check(L.bh_memcpy_h2d(local, probe.ptr, w.msg.ctypes.data, w.msg.nbytes))
     h2d_gbps = w.msg.nbytes / (time.perf_counter() - t) / 1e9
     probe.free()
-    batch_bytes = sum(int(x.nbytes) for x in (w.pub, w.sig, w.sig_off, w.sig_len, w.msg,
-                                              w.msg_off, w.msg_len))
+    if compact:
+        batch_bytes = sum(int(x.nbytes) for x in carrs.values() if x is not None)
+    else:
+        batch_bytes = sum(int(x.nbytes) for x in (w.pub, w.sig, w.sig_off, w.sig_len, w.msg,
+                                                  w.msg_off, w.msg_len))
     dist.barrier(world)
     # Timed region: K host-buffer batches. The library alternates them over two
     # compute lanes (bdls_hip.cpp Lane1), so batch k+1's kernels run beside
@@ -721,10 +740,14 @@ def bench_throughput(a, rank, world, local):
         "parity": parity_ok,
         "hbm_resident": resident,
         "host_path": {"value": round(host_value, 1), "ms_per_step": round(host_ms_per_step, 3),
-                      "what": ("host C ABI BatchVerify (bh_verify_submit/wait) from page-locked "
-                               "host buffers: H2D + verify + D2H per step, three batches in "
-                               "flight over two compute lanes (SURVEY 8(d)'s config-2 timed "
-                               "quantity, PCIe-inclusive)"),
+                      "what": (("host C ABI BatchVerify (bh_verify_compact_submit / "
+                                "bh_verify_wait, the compact bh_cbatch layout: distinct keys "
+                                "+ u32 indices, lengths only) " if compact else
+                                "host C ABI BatchVerify (bh_verify_submit/wait, bh_batch) ")
+                               + "from page-locked host buffers: H2D + verify + D2H per step, "
+                               "three batches in flight over two compute lanes (SURVEY 8(d)'s "
+                               "config-2 timed quantity, PCIe-inclusive)"),
+                      "layout": a.host_layout,
                       "single_batch_ms": round(single_ms, 3), "batch_bytes": batch_bytes,
                       "h2d_gbps_pinned": round(h2d_gbps, 2),
                       # the host path's own roofline: every batch crosses PCIe once

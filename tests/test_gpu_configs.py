@@ -258,3 +258,70 @@ def test_comb_and_window_tables_agree(L):
     assert tm1.n_keytables > 0 and tm1.n_keycomb > 0.9 * w.n * 15 / 16
     for bits, r in ((bits1, r1), (bits0, r0)):
         assert (r == w.reason).all() and (bits == w.expected_valid).all()
+
+
+# ---------------------------------------------------------------- compact host layout
+def _compact_verify(L, cb, n, flags=_lib.BH_F_HASH_SHA256, submit=False):
+    bm = np.zeros((n + 7) // 8 or 1, np.uint8)
+    rs = np.zeros(n or 1, np.uint8)
+    if submit:
+        job = ctypes.c_void_p()
+        _lib.check(L.bh_verify_compact_submit(0, ctypes.byref(cb), n, flags, bm.ctypes.data,
+                                              rs.ctypes.data, ctypes.byref(job)))
+        _lib.check(L.bh_verify_wait(job))
+    else:
+        _lib.check(L.bh_verify_compact(0, ctypes.byref(cb), n, flags, bm.ctypes.data,
+                                       rs.ctypes.data))
+    return np.unpackbits(bm, bitorder="little")[:n].astype(bool), rs[:n]
+
+
+@pytest.mark.parametrize("dedup,stride", [(True, True), (True, False), (False, True),
+                                          (False, False)])
+def test_compact_layout_matches(L, dedup, stride):
+    """bh_verify_compact (distinct keys + u32 indices, lengths only, fixed
+    message stride) gives the bitmap and reasons of the same records in the
+    bh_batch layout: every corruption class, keys shared (key tables) and
+    unique, one-lane (> 32,768 records) and split path."""
+    for n, nkeys in ((70_000, 3000), (5000, 5000)):
+        w = workload.generate(n, nkeys, 96, 8, seed=61)
+        arrs, cb = _lib.compact_layout(*w.arrays(), dedup=dedup, stride=stride)
+        if dedup:
+            assert cb.nkeys < n or nkeys == n
+        for submit in (False, True):
+            bits, reason = _compact_verify(L, cb, n, submit=submit)
+            assert (reason == w.reason).all() and (bits == w.expected_valid).all(), (n, submit)
+
+
+def test_compact_layout_ragged_messages_and_passes(L, small_chunks):
+    """Variable message lengths (msg_len given) through the pass loop
+    (131,072-record passes): the device prefix sums restart per shard and the
+    passes slice the expanded batch; digest mode (flags 0) with empty digests."""
+    n = 300_000
+    w = workload.generate(n, 20_000, 64, 16, seed=62)
+    dg = [hashlib.sha256(bytes(w.msg[o:o + l])).digest()[:(i % 33)] for i, (o, l) in
+          enumerate(zip(w.msg_off, w.msg_len))]
+    dl = np.array([len(x) for x in dg], np.uint32)
+    do = np.zeros(n, np.uint64)
+    do[1:] = np.cumsum(dl[:-1], dtype=np.uint64)
+    dgb = np.frombuffer(b"".join(dg) + b"\0", np.uint8)
+    plain = (w.pub, w.sig, w.sig_off, w.sig_len, dgb, do, dl)
+    arrs, cb = _lib.compact_layout(*plain)
+    assert cb.msg_len  # lengths kept: not a fixed stride
+    want_bits, want = host_verify(L, type("W", (), {"n": n, "arrays": lambda self: plain})(), 0)
+    bits, reason = _compact_verify(L, cb, n, flags=0)
+    assert (reason == want).all() and (bits == want_bits).all()
+    assert (want == 2).sum() > 0  # empty digests -> BH_R_EMPTY_DIGEST
+
+
+def test_compact_layout_rejects_bad_input(L):
+    w = workload.generate(1000, 10, 32, 0, seed=63)
+    arrs, cb = _lib.compact_layout(*w.arrays())
+    arrs["key_idx"][500] = cb.nkeys  # out of range
+    bm = np.zeros(125, np.uint8)
+    rs = np.zeros(1000, np.uint8)
+    assert L.bh_verify_compact(0, ctypes.byref(cb), 1000, 1, bm.ctypes.data, rs.ctypes.data) != 0
+    assert b"key index" in L.bh_last_error()
+    cb0 = _lib.BhCBatch()
+    assert L.bh_verify_compact(0, ctypes.byref(cb0), 1000, 1, bm.ctypes.data, rs.ctypes.data) != 0
+    # an empty batch is fine
+    _lib.check(L.bh_verify_compact(0, ctypes.byref(cb0), 0, 1, None, None))
