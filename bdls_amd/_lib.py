@@ -18,6 +18,7 @@ BH_F_HASH_SHA256 = 1
 BH_F_NO_LOW_S = 2
 BH_F_KEEP_KEYS = 4
 BH_F_HASH_SHA3_256 = 8
+BH_F_ANY_LANE = 16
 BH_CURVE_P256 = 0
 BH_CURVE_SECP256K1 = 1
 

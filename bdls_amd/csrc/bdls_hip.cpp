@@ -1098,7 +1098,8 @@ int check_curve(int curve) {
 }
 
 int check_flags(uint32_t flags) {
-  constexpr uint32_t known = BH_F_HASH_SHA256 | BH_F_NO_LOW_S | BH_F_KEEP_KEYS | BH_F_HASH_SHA3_256;
+  constexpr uint32_t known =
+      BH_F_HASH_SHA256 | BH_F_NO_LOW_S | BH_F_KEEP_KEYS | BH_F_HASH_SHA3_256 | BH_F_ANY_LANE;
   if (flags & ~known) return fail(BH_E_INVALID, "unknown flag");
   if ((flags & BH_F_HASH_SHA256) && (flags & BH_F_HASH_SHA3_256))
     return fail(BH_E_INVALID, "BH_F_HASH_SHA256 and BH_F_HASH_SHA3_256 are exclusive");
@@ -1447,9 +1448,14 @@ int bh_verify_dev(int device, int curve, const bh_batch* b, size_t n, uint32_t f
   if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
   std::lock_guard<std::mutex> g(d->mu);
   HIPCHK(hipSetDevice(d->id));
-  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  // BH_F_ANY_LANE: alternate the two compute lanes like host batches (run_dev
+  // orders the pass after its lane's previous one only)
+  int lane = -1;
+  if ((flags & BH_F_ANY_LANE) && !stream && !timing && !(flags & BH_F_KEEP_KEYS) && lanes() > 1)
+    lane = (int)(d->next_lane++ % lanes());
+  hipStream_t s = stream ? (hipStream_t)stream : (lane == 1 ? d->l1.stream : d->stream);
   if (n == 0) return BH_OK;
-  int rc = run_dev(*d, curve, b, n, flags, bitmap_words, reason, s, timing);
+  int rc = run_dev(*d, curve, b, n, flags, bitmap_words, reason, s, timing, lane);
   if (rc) return rc;
   if (sync && !timing) HIPCHK(hipStreamSynchronize(s));
   return BH_OK;

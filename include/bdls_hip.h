@@ -62,6 +62,12 @@ extern "C" {
 #define BH_F_HASH_SHA3_256 8u /* msg[i] is a message; digest = SHA3-256(msg[i]): identity.Verify
                                  of an MSP with SignatureHashFamily SHA3 (msp/identities.go:
                                  219-227, bccsp/sw/new.go:72). Exclusive with BH_F_HASH_SHA256. */
+#define BH_F_ANY_LANE 16u   /* bh_verify_dev on the library's streams (stream NULL, no timing):
+                               the pass may run on the device's other compute lane, beside the
+                               previous call's pass, with its own workspace -- consecutive
+                               resident batches overlap as host batches do. Its outputs must
+                               not alias an in-flight call's; bh_sync waits for both lanes.
+                               Ignored elsewhere (host batches already alternate lanes). */
 
 #define BH_CURVE_P256 0
 #define BH_CURVE_SECP256K1 1

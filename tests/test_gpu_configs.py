@@ -325,3 +325,33 @@ def test_compact_layout_rejects_bad_input(L):
     assert L.bh_verify_compact(0, ctypes.byref(cb0), 1000, 1, bm.ctypes.data, rs.ctypes.data) != 0
     # an empty batch is fine
     _lib.check(L.bh_verify_compact(0, ctypes.byref(cb0), 0, 1, None, None))
+
+
+def test_resident_passes_on_two_lanes(L):
+    """BH_F_ANY_LANE: consecutive bh_verify_dev calls alternate the device's
+    two compute lanes (each with its own workspace) and overlap; with
+    distinct outputs every pass's bitmap and reasons are exact after bh_sync,
+    for batches of different shapes (key tables and ladder) in flight
+    together."""
+    DA = _lib.DeviceArray
+    ws = [workload.generate(40_000 + 5000 * k, [2000, 45_000, 500, 3000][k], 128, 8,
+                            seed=70 + k) for k in range(4)]
+    bufs = []
+    for w in ws:
+        d = [DA.from_numpy(0, x) for x in w.arrays()]
+        bufs.append((w, d, DA(0, ((w.n + 63) // 64) * 8), DA(0, w.n),
+                     _lib.BhBatch(*[x.ptr for x in d])))
+    for rep in range(2):
+        for w, d, words, reason, b in bufs:
+            _lib.check(L.bh_verify_dev(0, 0, ctypes.byref(b), w.n,
+                                       _lib.BH_F_HASH_SHA256 | _lib.BH_F_ANY_LANE, words.ptr,
+                                       reason.ptr, None, 0, None))
+        _lib.check(L.bh_sync(0))
+        for w, d, words, reason, b in bufs:
+            bits = np.unpackbits(words.to_numpy(np.uint64, (w.n + 63) // 64).view(np.uint8),
+                                 bitorder="little")[:w.n].astype(bool)
+            assert (reason.to_numpy(np.uint8, w.n) == w.reason).all(), rep
+            assert (bits == w.expected_valid).all(), rep
+    for w, d, words, reason, b in bufs:
+        for x in d + [words, reason]:
+            x.free()

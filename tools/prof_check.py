@@ -7,11 +7,13 @@ usage: python tools/prof_check.py <kernel_trace.csv> <bench.json> <out.json>
 
 The bench runs, in order: the host path (warmup + 1 single + K timed batches,
 two compute lanes, so a kernel may share the GPU with the other lane's), then
-the HBM-resident passes (warmup + K timed, serialised), then the side
-configs (config 5's rank shard launches the one-lane kernels with no key-comb
-records: short dispatches). bench.py takes launch_ms from HIP events over the
-K timed resident passes: dispatches [2W + 1 + K, 2W + 1 + 2K) of the kernel in
-launch order. rocprof's --stats average mixes every phase.
+the HBM-resident passes (warmup + K timed, alternating two lanes), K more
+resident passes serialised with HIP events on every stage (the per-kernel
+timing), then the side configs (config 5's rank shard launches the one-lane
+kernels with no key-comb records: short dispatches). bench.py takes launch_ms
+from the HIP events of the serialised passes: dispatches
+[2W + 1 + 2K, 2W + 1 + 3K) of the kernel in launch order. rocprof's --stats
+average mixes every phase.
 """
 import csv
 import json
@@ -29,12 +31,13 @@ def main():
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
     host_n = warm + 1 + steps
-    lo = host_n + warm
+    lo = host_n + warm + steps
     timed = d[lo:lo + steps]
     out = {
         "kernel": k, "dispatches": len(d),
         "all_dispatch_mean_ms": round(sum(d) / len(d), 4) if d else None,
         "host_path_mean_ms": round(sum(d[:host_n]) / max(1, len(d[:host_n])), 4),
+        "resident_lanes_mean_ms": round(sum(d[lo - steps:lo]) / steps, 4),
         "resident_timed_mean_ms": round(sum(timed) / steps, 4) if len(timed) == steps else None,
         "resident_timed_dispatches": [lo, lo + steps],
         "bench_launch_ms": b["roofline"]["launch_ms"],
@@ -46,8 +49,9 @@ def main():
                                          / out["resident_timed_mean_ms"], 4)
     out["note"] = ("phases by dispatch order: host path = first warmup + 1 + steps dispatches "
                    "(two lanes: durations include the other lane's kernels), then warmup + "
-                   "steps resident passes, the last `steps` of them timed; bench_launch_ms = "
-                   "HIP events over the same timed resident passes")
+                   "steps resident passes over two lanes (the timed `value`), then `steps` "
+                   "serialised resident passes (resident_timed_*); bench_launch_ms = HIP events "
+                   "over those serialised passes")
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out))
 
