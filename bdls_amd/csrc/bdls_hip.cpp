@@ -93,11 +93,17 @@ size_t max_chunk() {
   return x > 0 ? std::min(kMaxChunk, round64((size_t)x)) : kMaxChunk;
 }
 
-// Compute lanes for host-API batches: 2 (default) or BH_LANES=1 (one lane,
-// every pass serialised as before round 3). Read per call.
+// Compute lanes for host-API batches and BH_F_ANY_LANE resident passes:
+// BH_LANES in [1, kMaxLanes] (default 3; 1 = every pass serialised as before
+// round 3). Same box, two passes each at config 2 (profiles/r04/v7):
+// resident 159.5-164.4 M verifies/s at 2 lanes, 161.0-162.6 at 3, 154.5-158.9
+// at 4; host path (compact layout, 30 steps) 142.6-144.2 / 155.2-155.6 /
+// 141.8-144.9. Read per call.
+constexpr uint32_t kMaxLanes = 4;
 uint32_t lanes() {
   const char* e = getenv("BH_LANES");
-  return (e && atoi(e) == 1) ? 1u : 2u;
+  const long v = e ? atol(e) : 3L;
+  return (uint32_t)std::max(1L, std::min<long>((long)kMaxLanes, v));
 }
 
 size_t pow2_at_least(size_t v) {
@@ -170,13 +176,13 @@ struct Slot {
 };
 constexpr int kSlots = 3;  // up to 3 host batches in flight per device
 
-// The second compute lane of a device (round 3). Host-API batches alternate
-// between lane 0 (Dev::stream / aux / ws) and lane 1, each with its own
-// workspace, so batch k+1's kernels run beside batch k's: the table builds (one
-// lane per key, chain-bound at one build wave per SIMD) and the plan stage's
-// short kernels leave issue slots that the other batch's waves fill. Everything
-// else -- the device-resident API, BDLS batches, registry writes, the latency
-// path -- stays serialised behind both lanes (wait_lanes).
+// The extra compute lanes of a device (round 3: one; round 4: up to
+// kMaxLanes - 1). Host-API batches rotate over lane 0 (Dev::stream / aux / ws)
+// and lanes 1.., each with its own workspace, so batch k+1's kernels run beside
+// batch k's: the table builds (one lane per key, chain-bound at one build wave
+// per SIMD) and the plan stage's short kernels leave issue slots that the other
+// batch's waves fill. Registry writes, BDLS batches and the serialised
+// device-resident API stay behind every lane (wait_lanes).
 struct Lane1 {
   hipStream_t stream = nullptr, aux = nullptr;
   hipEvent_t fork = nullptr, join = nullptr, done = nullptr;
@@ -204,7 +210,7 @@ struct Dev {
   hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipEvent_t done = nullptr;  // end of the last pass on lane 0 (orders passes across streams)
   bool done_recorded = false;
-  Lane1 l1;                   // the second compute lane (host-API batches)
+  Lane1 xl[kMaxLanes - 1];    // compute lanes 1 .. kMaxLanes - 1
   hipEvent_t build = nullptr; // end of lane 0's last table-build kernel
   bool build_staggered = false;  // lane builds alternate (BH_LANE_STAGGER, default on)
   uint32_t next_lane = 0;
@@ -221,6 +227,21 @@ struct Dev {
 
 std::mutex g_mu;
 std::vector<Dev*> g_devs;
+
+// Lane l of device d: stream, aux stream, fork / join / done / build events,
+// workspace. Lane 0 is the device's own stream and workspace.
+struct LaneRef {
+  hipStream_t stream, aux;
+  hipEvent_t fork, join, done, build;
+  bool* done_recorded;
+  DevBuf* ws;  // nullptr: the device workspace (carve_work's default)
+};
+LaneRef lane_ref(Dev& d, int l) {
+  if (l <= 0) return LaneRef{d.stream, d.aux, d.fork, d.join, d.done, d.build, &d.done_recorded,
+                             nullptr};
+  Lane1& x = d.xl[l - 1];
+  return LaneRef{x.stream, x.aux, x.fork, x.join, x.done, x.build, &x.done_recorded, &x.ws};
+}
 
 // Table builds per pass: verify needs >= 2 uses per table (at most ns / 2);
 // registration builds one per key straight into the registry (no per-batch
@@ -294,14 +315,17 @@ int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl, bool reg = false,
 hipError_t wait_lanes(Dev& d, hipStream_t s) {
   hipError_t e = hipSuccess;
   if (d.done_recorded && (e = hipStreamWaitEvent(s, d.done, 0)) != hipSuccess) return e;
-  if (d.l1.done_recorded && s != d.l1.stream) e = hipStreamWaitEvent(s, d.l1.done, 0);
+  for (Lane1& x : d.xl)
+    if (x.done_recorded && s != x.stream && (e = hipStreamWaitEvent(s, x.done, 0)) != hipSuccess)
+      return e;
   return e;
 }
 
 // Host wait for every pass on both lanes.
 int sync_lanes(Dev& d) {
   if (d.done_recorded) HIPCHK(hipEventSynchronize(d.done));
-  if (d.l1.done_recorded) HIPCHK(hipEventSynchronize(d.l1.done));
+  for (Lane1& x : d.xl)
+    if (x.done_recorded) HIPCHK(hipEventSynchronize(x.done));
   return BH_OK;
 }
 
@@ -369,12 +393,14 @@ int dev_init(Dev& d, int id) {
   for (auto& e : d.ev) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&d.reg_written, hipEventDisableTiming));
-  HIPCHK(hipStreamCreateWithFlags(&d.l1.stream, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&d.l1.aux, hipStreamNonBlocking));
-  HIPCHK(hipEventCreateWithFlags(&d.l1.fork, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&d.l1.join, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&d.l1.done, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&d.l1.build, hipEventDisableTiming));
+  for (Lane1& x : d.xl) {
+    HIPCHK(hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&x.aux, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&x.fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&x.join, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&x.build, hipEventDisableTiming));
+  }
   HIPCHK(hipEventCreateWithFlags(&d.build, hipEventDisableTiming));
   {
     const char* e = getenv("BH_LANE_STAGGER");
@@ -388,16 +414,20 @@ void dev_free(Dev& d) {
   (void)hipSetDevice(d.id);
   (void)sync_lanes(d);
   if (d.stream) (void)hipStreamSynchronize(d.stream);
-  if (d.l1.stream) {
-    (void)hipStreamSynchronize(d.l1.stream);
-    (void)hipStreamSynchronize(d.l1.aux);
+  for (Lane1& x : d.xl) {
+    if (x.stream) {
+      (void)hipStreamSynchronize(x.stream);
+      (void)hipStreamSynchronize(x.aux);
+    }
+    x.ws.release();
+    for (hipEvent_t e : {x.fork, x.join, x.done, x.build})
+      if (e) (void)hipEventDestroy(e);
+    if (x.aux) (void)hipStreamDestroy(x.aux);
+    if (x.stream) (void)hipStreamDestroy(x.stream);
+    x = Lane1{};
   }
-  d.l1.ws.release();
-  for (hipEvent_t e : {d.l1.fork, d.l1.join, d.l1.done, d.l1.build, d.build, d.reg_written})
+  for (hipEvent_t e : {d.build, d.reg_written})
     if (e) (void)hipEventDestroy(e);
-  if (d.l1.aux) (void)hipStreamDestroy(d.l1.aux);
-  if (d.l1.stream) (void)hipStreamDestroy(d.l1.stream);
-  d.l1 = Lane1{};
   if (d.copy) (void)hipStreamSynchronize(d.copy);
   for (auto& g : d.gtab)
     if (g) (void)hipFree(g);
@@ -521,36 +551,39 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
     int rc = reg_alloc(d, curve, kDefaultRegCap);
     if (rc) return rc;
   }
-  const bool l1 = lane == 1;
+  const LaneRef L = lane_ref(d, lane);  // lane < 0: lane 0's resources, after every lane
   g_dev_batches.fetch_add(1, std::memory_order_relaxed);
   g_dev_records.fetch_add(n, std::memory_order_relaxed);
   if (lane < 0) {
     HIPCHK(wait_lanes(d, s));
-  } else if (!l1) {
-    if (d.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.done, 0));
   } else {
-    if (d.l1.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.l1.done, 0));
-    if (d.reg_written_recorded) HIPCHK(hipStreamWaitEvent(s, d.reg_written, 0));
+    if (*L.done_recorded) HIPCHK(hipStreamWaitEvent(s, L.done, 0));
+    // lanes >= 1 also wait for the last registry write (lane 0 runs on the
+    // stream registry writers use, so it is ordered after them already)
+    if (lane > 0 && d.reg_written_recorded) HIPCHK(hipStreamWaitEvent(s, d.reg_written, 0));
   }
   const size_t chunk = max_chunk();
   for (size_t base = 0; base < n; base += chunk) {
     const size_t m = std::min(chunk, n - base);
     bh::Work w;
     bh::Plan pl;
-    int rc = carve_work(d, m, &w, &pl, false, l1 ? &d.l1.ws : nullptr);
+    int rc = carve_work(d, m, &w, &pl, false, lane > 0 ? L.ws : nullptr);
     if (rc) return rc;
     bh::LaunchOpts o = launch_opts(m, flags);
     {
       const char* e = getenv("BH_LL");
       o.ll_tables = !(e && atoi(e) == 0);
     }
-    o.aux = l1 ? d.l1.aux : d.aux;
-    o.ev_fork = l1 ? d.l1.fork : d.fork;
-    o.ev_join = l1 ? d.l1.join : d.join;
+    o.aux = L.aux;
+    o.ev_fork = L.fork;
+    o.ev_join = L.join;
     if (lane >= 0 && d.build_staggered && lanes() > 1) {
       // (an event never recorded is complete: the first builds do not wait)
-      o.ev_build_wait = l1 ? d.build : d.l1.build;
-      o.ev_build_done = l1 ? d.l1.build : d.build;
+      // builds take turns around the lanes: this lane's waits for the lane
+      // before it, so each build runs beside other lanes' key combs
+      const uint32_t nl = lanes();
+      o.ev_build_wait = lane_ref(d, (int)((lane + nl - 1) % nl)).build;
+      o.ev_build_done = L.build;
     }
     hipEvent_t* ev = t ? d.ev : nullptr;
     if (!t && d.defer) {
@@ -583,13 +616,8 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
       t->wide = (uint32_t)o.wide;
     }
   }
-  if (l1) {
-    HIPCHK(hipEventRecord(d.l1.done, s));
-    d.l1.done_recorded = true;
-  } else {
-    HIPCHK(hipEventRecord(d.done, s));
-    d.done_recorded = true;
-  }
+  HIPCHK(hipEventRecord(L.done, s));
+  *L.done_recorded = true;
   if (flags & BH_F_KEEP_KEYS) HIPCHK(note_reg_write(d, s));
   return BH_OK;
 }
@@ -879,7 +907,7 @@ int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, 
   // alternate the compute lanes (BH_LANES=1: lane 0 only); registry writers
   // (BH_F_KEEP_KEYS) serialise on lane 0
   const int lane = (flags & BH_F_KEEP_KEYS) ? -1 : (int)(d.next_lane++ % lanes());
-  hipStream_t s = lane == 1 ? d.l1.stream : d.stream;
+  hipStream_t s = lane > 0 ? lane_ref(d, lane).stream : d.stream;
   HIPCHK(hipStreamWaitEvent(s, sl.uploaded, 0));
   HIPCHK(expand_dev(db, m, s));
   uint64_t* dbm = (uint64_t*)sl.out.p;
@@ -963,19 +991,16 @@ int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, si
   // inverses are one serial lane each), so the coalescer's two batches in
   // flight run side by side instead of one after the other. Each lane has its
   // own workspace; both wait for the last registry write.
-  const bool l1 = lanes() > 1 && (d.next_lane++ % lanes()) == 1;
-  hipStream_t s = l1 ? d.l1.stream : d.stream;
-  if (l1) {
-    if (d.l1.done_recorded) HIPCHK(hipStreamWaitEvent(s, d.l1.done, 0));
-  } else if (d.done_recorded) {
-    HIPCHK(hipStreamWaitEvent(s, d.done, 0));
-  }
+  const int lane = lanes() > 1 ? (int)(d.next_lane++ % lanes()) : 0;
+  const LaneRef L = lane_ref(d, lane);
+  hipStream_t s = L.stream;
+  if (*L.done_recorded) HIPCHK(hipStreamWaitEvent(s, L.done, 0));
   if (d.reg_written_recorded) HIPCHK(hipStreamWaitEvent(s, d.reg_written, 0));
   char* dv = (char*)sl.stage.p;
   HIPCHK(hipMemcpyAsync(dv, h, total, hipMemcpyHostToDevice, s));
   bh::Work w;
   bh::Plan pl;
-  if ((rc = carve_work(d, m, &w, &pl, false, l1 ? &d.l1.ws : nullptr))) return rc;
+  if ((rc = carve_work(d, m, &w, &pl, false, L.ws))) return rc;
   const bh::BatchIn in{(const uint8_t*)(dv + o_pub), (const uint8_t*)(dv + o_sig),
                        (const uint64_t*)(dv + o_soff), (const uint32_t*)(dv + o_slen),
                        (const uint8_t*)(dv + o_msg), (const uint64_t*)(dv + o_moff),
@@ -987,13 +1012,8 @@ int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, si
                           (uint8_t*)sl.out.p, s, small_block));
   HIPCHK(hipMemcpyAsync(sl.host_out.p, sl.out.p, m, hipMemcpyDeviceToHost, s));
   HIPCHK(hipEventRecord(sl.done, s));
-  if (l1) {
-    HIPCHK(hipEventRecord(d.l1.done, s));
-    d.l1.done_recorded = true;
-  } else {
-    HIPCHK(hipEventRecord(d.done, s));
-    d.done_recorded = true;
-  }
+  HIPCHK(hipEventRecord(L.done, s));
+  *L.done_recorded = true;
   sl.owner = j;
   sl.owner_part = j->parts.size();
   Part part{&d, k, lo, m, false};
@@ -1448,12 +1468,12 @@ int bh_verify_dev(int device, int curve, const bh_batch* b, size_t n, uint32_t f
   if (!d) return fail(BH_E_NOT_INIT, "device not initialised (call bh_init)");
   std::lock_guard<std::mutex> g(d->mu);
   HIPCHK(hipSetDevice(d->id));
-  // BH_F_ANY_LANE: alternate the two compute lanes like host batches (run_dev
+  // BH_F_ANY_LANE: rotate over the compute lanes like host batches (run_dev
   // orders the pass after its lane's previous one only)
   int lane = -1;
   if ((flags & BH_F_ANY_LANE) && !stream && !timing && !(flags & BH_F_KEEP_KEYS) && lanes() > 1)
     lane = (int)(d->next_lane++ % lanes());
-  hipStream_t s = stream ? (hipStream_t)stream : (lane == 1 ? d->l1.stream : d->stream);
+  hipStream_t s = stream ? (hipStream_t)stream : lane_ref(*d, lane).stream;
   if (n == 0) return BH_OK;
   int rc = run_dev(*d, curve, b, n, flags, bitmap_words, reason, s, timing, lane);
   if (rc) return rc;
@@ -1653,7 +1673,7 @@ int bh_sync(int device) {
   HIPCHK(hipSetDevice(d->id));
   if (int rc = sync_lanes(*d)) return rc;
   HIPCHK(hipStreamSynchronize(d->stream));
-  HIPCHK(hipStreamSynchronize(d->l1.stream));
+  for (Lane1& x : d->xl) HIPCHK(hipStreamSynchronize(x.stream));
   return BH_OK;
 }
 

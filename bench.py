@@ -77,6 +77,16 @@ FP_KTAB = ((LL_T - 1) * LL_S * 8 + (_LL_CHAIN - 1) + 6 * _LL_CHAIN + (LL_T - 1) 
 FP_KEYCOMB = ((LL_S - 1) * (8 + 11) if LL_TABLES else 65 * 16) + 23
 MACS_PER_VERIFY = FP_LADDER * MAC_PER_FP
 KERNELS = {"build_ladder_ms": "k_ktab_ladder", "keycomb_ms": "k_keycomb"}
+MAX_LANES = 4  # bdls_hip.cpp kMaxLanes
+
+
+def lane_count() -> int:
+    """The library's compute lanes (bdls_hip.cpp lanes(): BH_LANES, default 3)."""
+    try:
+        v = int(os.environ.get("BH_LANES", "3"))
+    except ValueError:
+        v = 3
+    return min(MAX_LANES, max(1, v))
 CONFIG5_TOTAL = 1 << 26
 
 
@@ -115,7 +125,7 @@ def parse(argv=None):
                     help="host path input layout: bh_cbatch (distinct keys + u32 indices, "
                          "lengths only) or bh_batch (per-record keys, u64 offsets)")
     ap.add_argument("--resident-lanes", type=int, default=1,
-                    help="timed resident passes alternate the two compute lanes (BH_F_ANY_LANE)")
+                    help="timed resident passes rotate over the compute lanes (BH_F_ANY_LANE)")
     ap.add_argument("--hbm-resident", type=int, default=1,
                     help="also time the same passes on inputs already in HBM")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0")
@@ -637,7 +647,7 @@ def bench_throughput(a, rank, world, local):
         batch_bytes = sum(int(x.nbytes) for x in (w.pub, w.sig, w.sig_off, w.sig_len, w.msg,
                                                   w.msg_off, w.msg_len))
     dist.barrier(world)
-    # Timed region: K host-buffer batches. The library alternates them over two
+    # Timed region: K host-buffer batches. The library rotates them over its
     # compute lanes (bdls_hip.cpp Lane1), so batch k+1's kernels run beside
     # batch k's; per-kernel durations are therefore taken from the serialised
     # HBM-resident passes below (HIP events around every stage of every pass,
@@ -658,21 +668,21 @@ def bench_throughput(a, rank, world, local):
     parity_ok = bool((rs == w.reason).all() and (bits == w.expected_valid).all())
 
     # the same passes on inputs already resident in HBM (no PCIe in the loop).
-    # Timed: K passes alternating the two compute lanes (BH_F_ANY_LANE; two
-    # output sets), so pass k+1's early kernels fill pass k's tail as host
-    # batches do. Per-kernel durations (roofline) come from K more passes run
+    # Timed: K passes rotating over the compute lanes (BH_F_ANY_LANE; one
+    # output set per possible lane, so no in-flight pass shares its outputs),
+    # so pass k+1's early kernels fill pass k's tail as host batches do. Per-kernel durations (roofline) come from K more passes run
     # serialised, each kernel alone on the device.
     resident = None
     if a.hbm_resident:
         DA = _lib.DeviceArray
         d = [DA.from_numpy(local, x) for x in (w.pub, w.sig, w.sig_off, w.sig_len, w.msg,
                                                w.msg_off, w.msg_len)]
-        outs_dev = [(DA(local, ((n + 63) // 64) * 8), DA(local, n)) for _ in range(2)]
+        outs_dev = [(DA(local, ((n + 63) // 64) * 8), DA(local, n)) for _ in range(MAX_LANES)]
         db = _lib.BhBatch(*[x.ptr for x in d])
         lane_flag = _lib.BH_F_ANY_LANE if a.resident_lanes else 0
 
         def step(k, f=flags | lane_flag):
-            words, dreason = outs_dev[k % 2]
+            words, dreason = outs_dev[k % MAX_LANES]
             _lib.check(L.bh_verify_dev(local, 0, ctypes.byref(db), n, f, words.ptr,
                                        dreason.ptr, None, 0, None))
         for k in range(max(1, a.warmup)):
@@ -686,7 +696,7 @@ def bench_throughput(a, rank, world, local):
         r1 = time.perf_counter()
         r_el = dist.max_over_ranks(r1 - r0, world)
         r_ok = True
-        for words, dreason in outs_dev[:min(2, a.steps)]:
+        for words, dreason in outs_dev[:min(MAX_LANES, a.steps)]:
             rbits = np.unpackbits(words.to_numpy(np.uint64, (n + 63) // 64).view(np.uint8),
                                   bitorder="little")[:n].astype(bool)
             r_ok = r_ok and bool((dreason.to_numpy(np.uint8, n) == w.reason).all()
@@ -702,7 +712,7 @@ def bench_throughput(a, rank, world, local):
         parity_ok = parity_ok and r_ok
         resident = {"value": round(dist.sum_over_ranks(n, world) * a.steps / r_el, 1),
                     "ms_per_step": round(r_el * 1e3 / a.steps, 3), "parity": r_ok,
-                    "lanes": 2 if a.resident_lanes else 1,
+                    "lanes": lane_count() if a.resident_lanes else 1,
                     "serialised_ms_per_step": round(t_el * 1e3 / a.steps, 3)}
         for x in d + [y for pair in outs_dev for y in pair]:
             x.free()
@@ -749,7 +759,7 @@ def bench_throughput(a, rank, world, local):
             "msg_len": a.msg_len, "nkeys": nkeys, "corrupt_den": corrupt,
             "parallelism": f"shard{world} (no collective)",
             "value_is": ("HBM-resident: bh_verify_dev passes over inputs already in device "
-                         "memory (one pass = one step; consecutive passes alternate the two "
+                         "memory (one pass = one step; consecutive passes rotate over the "
                          "compute lanes, BH_F_ANY_LANE), barrier + device sync around the "
                          "timed steps" if resident else
                          "host C ABI BatchVerify (bh_verify_submit/wait) from page-locked host "
@@ -763,7 +773,7 @@ def bench_throughput(a, rank, world, local):
                                 "+ u32 indices, lengths only) " if compact else
                                 "host C ABI BatchVerify (bh_verify_submit/wait, bh_batch) ")
                                + "from page-locked host buffers: H2D + verify + D2H per step, "
-                               "three batches in flight over two compute lanes (SURVEY 8(d)'s "
+                               "batches in flight over the compute lanes (SURVEY 8(d)'s "
                                "config-2 timed quantity, PCIe-inclusive)"),
                       "layout": a.host_layout,
                       "single_batch_ms": round(single_ms, 3), "batch_bytes": batch_bytes,
@@ -776,7 +786,7 @@ def bench_throughput(a, rank, world, local):
         "kernel_ms_per_step": {k: round(v / a.steps, 3) for k, v in kern.items()},
         "kernel_ms_source": ("K serialised HBM-resident passes (bh_verify_dev, HIP events) run "
                              "after the timed ones" if a.hbm_resident
-                             else "the timed host-path passes (two compute lanes overlap)"),
+                             else "the timed host-path passes (compute lanes overlap)"),
         "routes": routes,
         "roofline": {
             "bound": "valu",

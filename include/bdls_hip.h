@@ -63,10 +63,12 @@ extern "C" {
                                  of an MSP with SignatureHashFamily SHA3 (msp/identities.go:
                                  219-227, bccsp/sw/new.go:72). Exclusive with BH_F_HASH_SHA256. */
 #define BH_F_ANY_LANE 16u   /* bh_verify_dev on the library's streams (stream NULL, no timing):
-                               the pass may run on the device's other compute lane, beside the
-                               previous call's pass, with its own workspace -- consecutive
-                               resident batches overlap as host batches do. Its outputs must
-                               not alias an in-flight call's; bh_sync waits for both lanes.
+                               consecutive calls rotate over the device's compute lanes
+                               (BH_LANES, default 3, at most 4), each with its own workspace,
+                               so a pass runs beside the previous calls' passes as host
+                               batches do. Its outputs must not alias an in-flight call's
+                               (4 rotating output sets are always safe); bh_sync waits for
+                               every lane.
                                Ignored elsewhere (host batches already alternate lanes). */
 
 #define BH_CURVE_P256 0

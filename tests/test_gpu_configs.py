@@ -328,8 +328,8 @@ def test_compact_layout_rejects_bad_input(L):
 
 
 def test_resident_passes_on_two_lanes(L):
-    """BH_F_ANY_LANE: consecutive bh_verify_dev calls alternate the device's
-    two compute lanes (each with its own workspace) and overlap; with
+    """BH_F_ANY_LANE: consecutive bh_verify_dev calls rotate over the device's
+    compute lanes (each with its own workspace) and overlap; with
     distinct outputs every pass's bitmap and reasons are exact after bh_sync,
     for batches of different shapes (key tables and ladder) in flight
     together."""

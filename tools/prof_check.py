@@ -5,9 +5,9 @@ command, split by bench phase, against the line's `roofline.launch_ms`.
 
 usage: python tools/prof_check.py <kernel_trace.csv> <bench.json> <out.json>
 
-The bench runs, in order: the host path (warmup + 1 single + K timed batches,
-two compute lanes, so a kernel may share the GPU with the other lane's), then
-the HBM-resident passes (warmup + K timed, alternating two lanes), K more
+The bench runs, in order: the host path (warmup + 1 single + K timed batches
+over the compute lanes, so a kernel may share the GPU with another lane's),
+then the HBM-resident passes (warmup + K timed, rotating over the lanes), K more
 resident passes serialised with HIP events on every stage (the per-kernel
 timing), then the side configs (config 5's rank shard launches the one-lane
 kernels with no key-comb records: short dispatches). bench.py takes launch_ms
@@ -48,8 +48,8 @@ def main():
         out["frac_from_rocprof"] = round(b["roofline"]["frac"] * out["bench_launch_ms"]
                                          / out["resident_timed_mean_ms"], 4)
     out["note"] = ("phases by dispatch order: host path = first warmup + 1 + steps dispatches "
-                   "(two lanes: durations include the other lane's kernels), then warmup + "
-                   "steps resident passes over two lanes (the timed `value`), then `steps` "
+                   "(lanes overlap: durations include other lanes' kernels), then warmup + "
+                   "steps resident passes over the lanes (the timed `value`), then `steps` "
                    "serialised resident passes (resident_timed_*); bench_launch_ms = HIP events "
                    "over those serialised passes")
     json.dump(out, open(dst, "w"), indent=1)
