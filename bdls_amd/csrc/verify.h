@@ -1154,6 +1154,26 @@ BH_HD void llaff_load(uint32_t x[9], uint32_t y[9], const uint32_t* tab, uint32_
   y[7] = f.x; y[8] = f.y;
 }
 
+// The same 18 words (x then y) through 8-byte loads at any 8-byte-aligned
+// slot: k_keycomb's LDS copies of a workgroup's tables pack entries at 72
+// bytes (kLLLds words), the per-batch tables at 80 (kLLAff); the pointer may
+// be either (a flat load).
+constexpr uint32_t kLLLds = 18;
+struct alignas(8) W2 {
+  uint32_t x, y;
+};
+BH_HD void llent_load(uint32_t x[9], uint32_t y[9], const uint32_t* p) {
+  const W2* s = reinterpret_cast<const W2*>(p);
+  W2 v[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) v[k] = s[k];
+  x[0] = v[0].x; x[1] = v[0].y; x[2] = v[1].x; x[3] = v[1].y;
+  x[4] = v[2].x; x[5] = v[2].y; x[6] = v[3].x; x[7] = v[3].y;
+  x[8] = v[4].x; y[0] = v[4].y; y[1] = v[5].x; y[2] = v[5].y;
+  y[3] = v[6].x; y[4] = v[6].y; y[5] = v[7].x; y[6] = v[7].y;
+  y[7] = v[8].x; y[8] = v[8].y;
+}
+
 // Field inverse by safegcd (fe.h mod_inv_sg, constant iteration so the lanes
 // of a wave stay together): a R -> a^-1 R for the radix-2^30 field (any beta
 // f_reduce accepts, a != 0 mod p). The divsteps run on the canonical value
@@ -1336,8 +1356,12 @@ BH_HD void ll_slices(uint64_t sl[kLLTeeth], const uint32_t u2[8]) {
 }
 
 // u2 Q from an affine signed comb table (Horner over the s columns, top first).
+// stride 0: the per-batch table in global memory (16-byte loads of its 80-byte
+// slots); else entries `stride` words apart read by llent_load (k_keycomb's
+// LDS copy, or the global table when the workgroup's copy is full).
 template <class P>
-BH_HD void q_llcomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab) {
+BH_HD void q_llcomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab,
+                    uint32_t stride = 0) {
   uint32_t u2[8], one[9];
   ld8(u2, w.r, i, w.ns);
   f_const(one, P::r1);
@@ -1346,7 +1370,8 @@ BH_HD void q_llcomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32
   uint32_t idx;
   bool neg;
   ll_column(sl, kLLSpace - 1, idx, neg);  // top column: top bit set, +E[idx]
-  llaff_load(A.X, A.Y, tab, idx);
+  if (stride) llent_load(A.X, A.Y, tab + idx * stride);
+  else llaff_load(A.X, A.Y, tab, idx);
   f_copy(A.Z, one);
   a_inf = false;
 #pragma unroll 1
@@ -1354,7 +1379,8 @@ BH_HD void q_llcomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32
     j_dbl<P>(A, A);  // (while a_inf, A is a placeholder the next point replaces)
     ll_column(sl, j, idx, neg);
     uint32_t tx[9], ty[9], nty[9];
-    llaff_load(tx, ty, tab, idx);
+    if (stride) llent_load(tx, ty, tab + idx * stride);
+    else llaff_load(tx, ty, tab, idx);
     f_neg<P, 64>(nty, ty);
     f_sel(ty, neg, nty, ty);
     bool same;
@@ -1411,10 +1437,10 @@ BH_HD void stage_gpart(const Work& w, const uint32_t* gtab, uint32_t i, uint32_t
 
 template <class P>
 BH_HD bool stage_keycomb_q(const Work& w, uint32_t i, uint32_t j, const uint32_t* tab,
-                           bool ll = false) {
+                           bool ll = false, uint32_t stride = 0) {
   J30 A, B;
   bool a_inf;
-  if (ll) q_llcomb<P>(A, a_inf, w, i, tab);  // a per-batch Lim-Lee comb table
+  if (ll) q_llcomb<P>(A, a_inf, w, i, tab, stride);  // a per-batch Lim-Lee comb table
   else q_keycomb<P>(A, a_inf, w, i, tab);
   const uint32_t* o = w.gpart + j;
 #pragma unroll

@@ -518,16 +518,79 @@ __global__ __launch_bounds__(256) void k_reg_publish(Work w, Plan pl, KeyReg g) 
 #else
 #define BH_KEYCOMB_ATTR
 #endif
+// BH_KEYCOMB_LDS (default 1): with comb tables, each 256-record workgroup
+// first copies the tables its records use -- the list is grouped by table, so
+// they are the runs of equal ids, ~17 at 16 records per key -- into LDS
+// (kLdsTabs slots of 64 x 72 B = 78 KB: two workgroups per CU, the occupancy
+// the registers allow anyway), then reads every Horner step's entry from
+// there. Each table is then fetched from L2 / HBM once per workgroup instead
+// of once per Horner step of every wave that uses it, whose working set
+// (~5 MB per XCD) overflowed the 4 MB L2. Runs beyond the slots read their
+// table in global memory.
+#ifndef BH_KEYCOMB_LDS
+#define BH_KEYCOMB_LDS 1
+#endif
+constexpr uint32_t kLdsTabs = 17;
+constexpr uint32_t kLdsTabWords = kLLEnt * kLLLds;
 template <class P>
 __global__ __launch_bounds__(256) BH_KEYCOMB_ATTR void k_keycomb(Work w, Plan pl, KeyReg g,
                                                  const uint32_t* __restrict__ gtab,
                                                  uint8_t* __restrict__ reason, uint32_t ll) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t cnt = pl.counters[0];
-  if (j >= cnt) return;
-  const uint32_t i = pl.comb_order[j];
-  const uint32_t id = pl.rec_tab[i];
-  const bool ok = stage_keycomb_q<P>(w, i, j, tab_ptr(pl, g, id), ll && (id & kLocal));
+  if (!BH_KEYCOMB_LDS || !ll) {  // uniform over the grid
+    if (j >= cnt) return;
+    const uint32_t i = pl.comb_order[j];
+    const uint32_t id = pl.rec_tab[i];
+    const bool ok = stage_keycomb_q<P>(w, i, j, tab_ptr(pl, g, id), ll && (id & kLocal));
+    reason[i] = ok ? R_OK : R_MATH;
+    return;
+  }
+  if (blockIdx.x * blockDim.x >= cnt) return;  // the whole workgroup: no barrier skipped
+  __shared__ uint32_t s_tab[kLdsTabs * kLdsTabWords];
+  __shared__ const uint32_t* s_src[kLdsTabs];
+  __shared__ uint32_t s_id[256];
+  __shared__ uint32_t s_wsum[4];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const bool have = j < cnt;
+  uint32_t i = 0, id = kNone;
+  if (have) {
+    i = pl.comb_order[j];
+    id = pl.rec_tab[i];
+  }
+  const bool lcl = have && (id & kLocal);  // a per-batch comb table
+  s_id[t] = lcl ? id : kNone;
+  __syncthreads();
+  // runs of equal ids -> slots: inclusive count of run starts up to this lane
+  const bool start = lcl && (t == 0u || s_id[t - 1u] != id);
+  const uint64_t m = __ballot(start);
+  uint32_t slot = (uint32_t)__popcll(m & (lane == 63u ? ~0ull : ((2ull << lane) - 1ull)));
+  if (lane == 0u) s_wsum[wv] = (uint32_t)__popcll(m);
+  __syncthreads();
+  uint32_t runs = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 4u; q++) {
+    const uint32_t c = s_wsum[q];
+    if (q < wv) slot += c;
+    runs += c;
+  }
+  slot -= 1u;  // meaningful for lcl lanes (>= 1 start at or before them)
+  if (start && slot < kLdsTabs) s_src[slot] = tab_ptr(pl, g, id);
+  __syncthreads();
+  const uint32_t nst = runs < kLdsTabs ? runs : kLdsTabs;
+  for (uint32_t e = t; e < nst * kLLEnt; e += 256u) {  // one entry per lane: 5 x 16 B in, 9 x 8 B out
+    const W4* s = reinterpret_cast<const W4*>(s_src[e / kLLEnt] + (e % kLLEnt) * kLLAff);
+    const W4 a = s[0], b = s[1], c = s[2], d = s[3], f = s[4];
+    W2* o = reinterpret_cast<W2*>(s_tab + e * kLLLds);
+    o[0] = W2{a.x, a.y}; o[1] = W2{a.z, a.w}; o[2] = W2{b.x, b.y};
+    o[3] = W2{b.z, b.w}; o[4] = W2{c.x, c.y}; o[5] = W2{c.z, c.w};
+    o[6] = W2{d.x, d.y}; o[7] = W2{d.z, d.w}; o[8] = W2{f.x, f.y};
+  }
+  __syncthreads();
+  if (!have) return;
+  const bool in_lds = lcl && slot < kLdsTabs;
+  const uint32_t* tab = in_lds ? s_tab + slot * kLdsTabWords : tab_ptr(pl, g, id);
+  const bool ok = stage_keycomb_q<P>(w, i, j, tab, lcl, lcl ? (in_lds ? kLLLds : kLLAff) : 0u);
   reason[i] = ok ? R_OK : R_MATH;
 }
 
