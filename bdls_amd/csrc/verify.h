@@ -613,6 +613,56 @@ BH_HD void recode_goff(uint32_t v[9], const uint32_t k[8]) {
 // adds). The common step is one in-place mixed addition; a zero digit (odd
 // 2^-kGW per window), B still at infinity, and the degenerate additions of
 // crafted scalars take a side branch that the lanes skip together.
+// Software-pipelined (BH_GCOMB_PREFETCH, default 1): window win + 1's entry is
+// loaded before window win's addition, so its L2 / MALL latency (the 5.9 MB
+// table does not fit one XCD's 4 MB L2) runs under a mixed addition instead
+// of stalling the wave -- there is no doubling here to hide it behind, unlike
+// the key comb's Horner step.
+#ifndef BH_GCOMB_PREFETCH
+#define BH_GCOMB_PREFETCH 1
+#endif
+// the digit of the window v now starts at (v shifted past it) and its entry
+BH_HD void g_window(uint32_t v[9], int win, const uint32_t* gtab, uint32_t tx[9], uint32_t ty[9],
+                    uint32_t& mag, bool& neg) {
+  const int d = (int)(v[0] & (2u * kCombEntries - 1u)) - kCombEntries;
+  shr_const<kGW>(v);
+  mag = (uint32_t)(d < 0 ? -d : d);
+  neg = d < 0;
+  const uint32_t* te = gtab + ((size_t)win * kCombEntries + (mag ? mag - 1 : 0)) * kGEntry;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    tx[k] = te[k];
+    ty[k] = te[9 + k];
+  }
+}
+
+// One window of g_comb: B += T (T = the signed entry, mag 0: B unchanged).
+template <class P>
+BH_HD void g_step(J30& B, bool& b_inf, const uint32_t tx[9], const uint32_t ty[9], uint32_t mag,
+                  const uint32_t one[9]) {
+  if (mag == 0u || b_inf) {  // zero digit: B unchanged; B at infinity: B = T
+    if (mag != 0u) {
+      f_copy(B.X, tx);
+      f_copy(B.Y, ty);
+      f_copy(B.Z, one);
+      b_inf = false;
+    }
+  } else {
+    bool same;
+    if (j_madd<P>(B, B, tx, ty, &same)) {  // rare: x(B) == x(T)
+      if (same) {
+        J30 Tj;
+        f_copy(Tj.X, tx);
+        f_copy(Tj.Y, ty);
+        f_copy(Tj.Z, one);
+        j_dbl<P>(B, Tj);
+      } else {
+        b_inf = true;
+      }
+    }
+  }
+}
+
 template <class P>
 BH_HD void g_comb(J30& B, bool& b_inf, const uint32_t* gtab, const uint32_t u1[8]) {
   uint32_t one[9];
@@ -623,40 +673,27 @@ BH_HD void g_comb(J30& B, bool& b_inf, const uint32_t* gtab, const uint32_t u1[8
   f_copy(B.Z, one);
   uint32_t v[9];
   recode_goff(v, u1);
+  uint32_t tx[9], ty[9], mag;
+  bool neg;
+  if (BH_GCOMB_PREFETCH) g_window(v, 0, gtab, tx, ty, mag, neg);
 #pragma unroll 1
   for (int win = 0; win < kCombWindows; win++) {
-    const int d = (int)(v[0] & (2u * kCombEntries - 1u)) - kCombEntries;
-    shr_const<kGW>(v);
-    const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-    const bool neg = d < 0;
-    const uint32_t* te = gtab + ((size_t)win * kCombEntries + (mag ? mag - 1 : 0)) * kGEntry;
-    uint32_t tx[9], ty[9];
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      tx[k] = te[k];
-      ty[k] = te[9 + k];
-    }
-    if (neg) f_neg<P, 64>(ty, ty);
-    if (mag == 0u || b_inf) {  // zero digit: B unchanged; B at infinity: B = T
-      if (mag != 0u) {
-        f_copy(B.X, tx);
-        f_copy(B.Y, ty);
-        f_copy(B.Z, one);
-        b_inf = false;
-      }
+    if (BH_GCOMB_PREFETCH) {
+      // next window's entry (past the last window: a valid entry, unused)
+      uint32_t nx[9], ny[9], nmag;
+      bool nneg;
+      const int nw = win + 1 < kCombWindows ? win + 1 : win;
+      g_window(v, nw, gtab, nx, ny, nmag, nneg);
+      if (neg) f_neg<P, 64>(ty, ty);
+      g_step<P>(B, b_inf, tx, ty, mag, one);
+      f_copy(tx, nx);
+      f_copy(ty, ny);
+      mag = nmag;
+      neg = nneg;
     } else {
-      bool same;
-      if (j_madd<P>(B, B, tx, ty, &same)) {  // rare: x(B) == x(T)
-        if (same) {
-          J30 Tj;
-          f_copy(Tj.X, tx);
-          f_copy(Tj.Y, ty);
-          f_copy(Tj.Z, one);
-          j_dbl<P>(B, Tj);
-        } else {
-          b_inf = true;
-        }
-      }
+      g_window(v, win, gtab, tx, ty, mag, neg);
+      if (neg) f_neg<P, 64>(ty, ty);
+      g_step<P>(B, b_inf, tx, ty, mag, one);
     }
   }
 }
