@@ -30,7 +30,8 @@ for s in $STEPS; do
     pmc)    export TMPDIR=/tmp
             for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE" "SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "FETCH_SIZE" "WRITE_SIZE"; do
               tag=$(echo $grp | tr ' ' '_' | cut -c1-40)
-              timeout -k 10 600 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d gpurun_out/pmc_$tag -o pmc -- python3 bench.py --steps 1 --warmup 0 --cpu-baseline 0 --hbm-resident 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/pmc_$tag.log 2>&1; rc=$?; ok_or_stop $rc "pmc $grp"
+              # one compute lane: each kernel alone on the device, so GRBM_GUI_ACTIVE is its own
+              BH_LANES=1 timeout -k 10 600 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d gpurun_out/pmc_$tag -o pmc -- python3 bench.py --steps 1 --warmup 0 --cpu-baseline 0 --hbm-resident 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/pmc_$tag.log 2>&1; rc=$?; ok_or_stop $rc "pmc $grp"
             done ;;
   esac
 done
