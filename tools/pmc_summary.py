@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Per-kernel summary of rocprofv3 --pmc passes (tools/gpu_check.sh step pmc).
 
-usage: python tools/pmc_summary.py <dir with pmc_*/ subdirs or csvs> <out.json> [--traffic]
+usage: python tools/pmc_summary.py <dir with pmc_*/ subdirs or csvs> <out.json> [--traffic
+       --workload=config<N>:n<records per rank> --source=<profiles dir>]
+
+bench.py prints the counters only when --workload names its own workload
+(config2:n1048576 for the default line) and the kernel build matches.
 
 For each kernel (short name) and counter: mean value per dispatch. With
 --traffic, also writes profiles/traffic.json: HBM bytes per launch from
