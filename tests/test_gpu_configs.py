@@ -260,6 +260,19 @@ def test_comb_and_window_tables_agree(L):
         assert (r == w.reason).all() and (bits == w.expected_valid).all()
 
 
+def test_comb_tables_beyond_the_lds_slots(L):
+    """k_keycomb copies the comb tables of each 256-record workgroup's runs of
+    equal table ids into 17 LDS slots; runs past the slots read their table in
+    global memory. At ~6 records per key a workgroup spans ~40 tables, so most
+    workgroups (and waves) mix LDS-staged and global runs, and keys used < 4
+    times take the ladder in between: bitmap and reasons still exact."""
+    w = workload.generate(120_000, 20_000, 64, 16, seed=47)
+    bits, r, tm = dev_verify(L, w)
+    assert tm.n_keytables > 10_000 and tm.n_keycomb > 0.8 * w.n and tm.n_ladder > 1_000
+    assert (r == w.reason).all() and (bits == w.expected_valid).all()
+    orc_sample(w, 100, seed=47)
+
+
 # ---------------------------------------------------------------- compact host layout
 def _compact_verify(L, cb, n, flags=_lib.BH_F_HASH_SHA256, submit=False):
     bm = np.zeros((n + 7) // 8 or 1, np.uint8)
