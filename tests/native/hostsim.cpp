@@ -72,7 +72,21 @@ static bool keycomb_any(const Work& w, const uint32_t* gtab, uint32_t i, const u
     case 0: return stage_keycomb<P>(w, gtab, i, tab);
     default:  // the device's split: u1 G stored by list position, then the table half
       stage_gpart<P>(w, gtab, i, i);
-      return stage_keycomb_q<P>(w, i, i, tab, g_ll != 0);
+      if (!g_ll) return stage_keycomb_q<P>(w, i, i, tab, false);
+      // k_keycomb's three ways to read a comb table, taken in turn: 16-byte
+      // loads of the per-batch table (stride 0), the workgroup's packed LDS
+      // copy (kLLLds words per entry), and the per-batch table through the same
+      // 8-byte loads (a run past the LDS slots)
+      switch (i % 3) {
+        case 0: return stage_keycomb_q<P>(w, i, i, tab, true, 0);
+        case 1: {
+          std::vector<uint32_t> lds((size_t)kLLEnt * kLLLds);
+          for (uint32_t e = 0; e < kLLEnt; e++)
+            for (uint32_t k = 0; k < kLLLds; k++) lds[e * kLLLds + k] = tab[e * kLLAff + k];
+          return stage_keycomb_q<P>(w, i, i, lds.data(), true, kLLLds);
+        }
+        default: return stage_keycomb_q<P>(w, i, i, tab, true, kLLAff);
+      }
   }
 }
 
