@@ -181,6 +181,39 @@ def test_submit_wait_pipeline(L):
     _lib.check(L.bh_verify_wait(job))
 
 
+def test_concurrent_host_callers(L):
+    """Goroutine-style callers: six threads (ctypes drops the GIL in the call)
+    run whole batches through bh_verify at once -- the one-launch small path,
+    windowed and comb key tables, the ladder, and a BH_F_KEEP_KEYS caller whose
+    registry writes are serialised behind every lane -- so passes of different
+    callers share the compute lanes and pipeline slots. Every result is exact."""
+    import threading
+    shapes = [(200, 20, 0), (9_000, 300, 0), (50_000, 2_000, 0), (40_000, 40_000, 0),
+              (60_000, 3_000, _lib.BH_F_KEEP_KEYS), (700, 700, 0)]
+    ws = [workload.generate(n, k, 96, 8, seed=90 + j) for j, (n, k, _) in enumerate(shapes)]
+    errors = []
+
+    def caller(j):
+        try:
+            w, flags = ws[j], _lib.BH_F_HASH_SHA256 | shapes[j][2]
+            for rep in range(3):
+                valid, reason = host_verify(L, w, flags)
+                if not ((reason == w.reason).all() and (valid == w.expected_valid).all()):
+                    errors.append((j, rep))
+        except Exception as e:  # noqa: BLE001 -- reported below with its caller
+            errors.append((j, repr(e)))
+
+    _lib.check(L.bh_keys_clear(0, 0))
+    threads = [threading.Thread(target=caller, args=(j,)) for j in range(len(ws))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in threads)
+    assert not errors, errors
+    _lib.check(L.bh_keys_clear(0, 0))
+
+
 def test_unique_keys_forced_passes(L, small_chunks):
     """Config 5's shape (every key used once: the variable-base ladder, no key
     tables) through the pass loop: 300,000 unique keys in 131,072-record passes
