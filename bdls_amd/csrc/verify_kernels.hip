@@ -377,11 +377,10 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(Work w, Plan pl, uint32_t
 // while the builds run: one build wave per SIMD leaves issue slots free.
 constexpr uint32_t kBuildPerBlock = 256;
 template <class P>
-__global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
-                                                     const uint32_t* __restrict__ gtab,
-                                                     uint8_t* __restrict__ reason,
-                                                     uint32_t tab_blocks,
-                                                     uint32_t lad_blocks, uint32_t ll) {
+__device__ __forceinline__ void ktab_ladder_body(const Work& w, const Plan& pl, const KeyReg& g,
+                                                 const uint32_t* __restrict__ gtab,
+                                                 uint8_t* __restrict__ reason, uint32_t tab_blocks,
+                                                 uint32_t lad_blocks, uint32_t ll) {
   if (blockIdx.x >= tab_blocks + lad_blocks) {
     const uint32_t j = (blockIdx.x - tab_blocks - lad_blocks) * blockDim.x + threadIdx.x;
     if (j < pl.counters[0]) stage_gpart<P>(w, gtab, pl.comb_order[j], j);
@@ -410,6 +409,48 @@ __global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
   const bool ok = stage_ladder<P>(w, gtab, i, j0 >> 6, threadIdx.x & 63u);
   if (active) reason[i] = ok ? R_OK : R_MATH;
 }
+
+// BH_WAVE_TIMES (experiment builds only, tools/build_exp.sh): every wave of
+// k_ktab_ladder records its role (0 table build, 1 ladder, 2 u1 G), CU and
+// start / end on the constant-rate wall clock, read back by bh_wave_times.
+#ifdef BH_WAVE_TIMES
+constexpr uint32_t kWaveTimes = 65536;
+__device__ unsigned long long g_wave_t[kWaveTimes * 4];
+#endif
+
+template <class P>
+__global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
+                                                     const uint32_t* __restrict__ gtab,
+                                                     uint8_t* __restrict__ reason,
+                                                     uint32_t tab_blocks,
+                                                     uint32_t lad_blocks, uint32_t ll) {
+#ifdef BH_WAVE_TIMES
+  const unsigned long long t0 = wall_clock64();
+#endif
+  ktab_ladder_body<P>(w, pl, g, gtab, reason, tab_blocks, lad_blocks, ll);
+#ifdef BH_WAVE_TIMES
+  const unsigned long long t1 = wall_clock64();
+  const uint32_t wid = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u;
+  if ((threadIdx.x & 63u) == 0u && wid < kWaveTimes) {
+    const uint32_t role = blockIdx.x < tab_blocks ? 0u : blockIdx.x < tab_blocks + lad_blocks ? 1u : 2u;
+    g_wave_t[4 * wid] = t0;
+    g_wave_t[4 * wid + 1] = t1;
+    g_wave_t[4 * wid + 2] = role;
+    g_wave_t[4 * wid + 3] = (unsigned long long)__smid();
+  }
+#endif
+}
+
+#ifdef BH_WAVE_TIMES
+extern "C" int bh_wave_times(unsigned long long* out, int clear) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (clear) {
+    static unsigned long long zero[kWaveTimes * 4];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_wave_t), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), sizeof(g_wave_t)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // Butterfly over groups of L adjacent lanes: every lane ends with the group's
 // sum (L partial sums of one record).
@@ -1058,6 +1099,8 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   REC(3);
   const uint32_t tab_blocks = (pl.max_tables + kBuildPerBlock - 1) / kBuildPerBlock;
   // u1 G of the key-comb list runs inside k_ktab_ladder for the 1-lane comb
+  // (a separate kernel on the aux stream, 146 VGPRs, did not run faster:
+  // profiles/r04/v14)
   const uint32_t gp_blocks = o.wide <= 1 ? grd.x : 0u;
   // from here on only plc (rec_slot consumed by the sort)
   if (split) {
