@@ -214,7 +214,7 @@ struct Dev {
   hipEvent_t build = nullptr; // end of lane 0's last table-build kernel
   bool build_staggered = false;  // lane builds alternate (BH_LANE_STAGGER, default on)
   uint32_t next_lane = 0;
-  hipEvent_t reg_written = nullptr;  // the last registry write (lane 1 passes wait for it)
+  hipEvent_t reg_written = nullptr;  // the last registry write (passes on lanes >= 1 wait for it)
   bool reg_written_recorded = false;
   // deferred timing (bh_timing_begin/_end): one event set per pass, read at end
   bool defer = false;
@@ -311,7 +311,7 @@ int carve_work(Dev& d, size_t n, bh::Work* w, bh::Plan* pl, bool reg = false,
   return BH_OK;
 }
 
-// Order stream s after every pass on both lanes (serialised operations).
+// Order stream s after every pass on every lane (serialised operations).
 hipError_t wait_lanes(Dev& d, hipStream_t s) {
   hipError_t e = hipSuccess;
   if (d.done_recorded && (e = hipStreamWaitEvent(s, d.done, 0)) != hipSuccess) return e;
@@ -321,7 +321,7 @@ hipError_t wait_lanes(Dev& d, hipStream_t s) {
   return e;
 }
 
-// Host wait for every pass on both lanes.
+// Host wait for every pass on every lane.
 int sync_lanes(Dev& d) {
   if (d.done_recorded) HIPCHK(hipEventSynchronize(d.done));
   for (Lane1& x : d.xl)
@@ -329,7 +329,7 @@ int sync_lanes(Dev& d) {
   return BH_OK;
 }
 
-// A registry write was enqueued on s: lane-1 passes enqueued later wait for it.
+// A registry write was enqueued on s: passes on lanes >= 1 enqueued later wait for it.
 hipError_t note_reg_write(Dev& d, hipStream_t s) {
   hipError_t e = hipEventRecord(d.reg_written, s);
   if (e == hipSuccess) d.reg_written_recorded = true;
@@ -538,10 +538,10 @@ hipError_t launch(int curve, const bh::BdlsIn& in, const bh::Work& w, const bh::
 
 // Core device-resident pass (caller holds d.mu and has set the device).
 // With t != nullptr, events bracket every stage and the call synchronises.
-// lane -1: serialised (after every pass on both lanes; lane 0's workspace);
-// lane 0 / 1: a host-API batch on that lane (after the lane's previous pass;
-// lane 1 also after the last registry write). BH_F_KEEP_KEYS passes write the
-// registry and are always serialised.
+// lane -1: serialised (after every pass on every lane; lane 0's workspace);
+// lane 0 .. lanes() - 1: a host-API batch on that lane (after the lane's
+// previous pass; lanes >= 1 also after the last registry write).
+// BH_F_KEEP_KEYS passes write the registry and are always serialised.
 template <class B>
 int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* bitmap,
             uint8_t* reason, hipStream_t s, bh_timing* t, int lane = -1) {
@@ -986,11 +986,11 @@ int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, si
     if (ml) std::memcpy(h + o_msg + mp, b->msg + b->msg_off[lo + i], ml);
     mp += ml;
   }
-  // Small batches alternate between the two compute lanes like host batches:
+  // Small batches rotate over the compute lanes like host batches:
   // a latency batch occupies a few CUs for ~50-90 us (its records' prep and
   // inverses are one serial lane each), so the coalescer's two batches in
   // flight run side by side instead of one after the other. Each lane has its
-  // own workspace; both wait for the last registry write.
+  // own workspace; every one waits for the last registry write.
   const int lane = lanes() > 1 ? (int)(d.next_lane++ % lanes()) : 0;
   const LaneRef L = lane_ref(d, lane);
   hipStream_t s = L.stream;
