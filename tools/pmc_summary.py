@@ -2,7 +2,8 @@
 """Per-kernel summary of rocprofv3 --pmc passes (tools/gpu_check.sh step pmc).
 
 usage: python tools/pmc_summary.py <dir with pmc_*/ subdirs or csvs> <out.json> [--traffic
-       --workload=config<N>:n<records per rank> --source=<profiles dir>]
+       --workload=config<N>:n<records per rank> --source=<profiles dir>
+       --traffic-out=<path, default profiles/traffic.json>]
 
 bench.py prints the counters only when --workload names its own workload
 (config2:n1048576 for the default line) and the kernel build matches.
@@ -95,8 +96,9 @@ def main():
                 e["grbm_gui_active"] = c["GRBM_GUI_ACTIVE"]
                 e["valu_util_2cyc"] = c["SQ_INSTS_VALU"] * 2 / (cyc * 1024) if cyc else None
                 e["valu_util_4cyc"] = c["SQ_INSTS_VALU"] * 4 / (cyc * 1024) if cyc else None
-        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                            "profiles", "traffic.json")
+        path = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--traffic-out=")),
+                    os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                 "profiles", "traffic.json"))
         with open(path, "w") as f:
             json.dump(tr, f, indent=1, sort_keys=True)
     for k, v in sorted(s.items()):
