@@ -85,3 +85,36 @@ def test_pmc_summary_traffic(tmp_path):
     sys.path.insert(0, ROOT)
     from bdls_amd.provenance import kernel_src_sha
     assert tr["kernel_src_sha"] == kernel_src_sha()
+
+
+def test_bench_refuses_foreign_counters(tmp_path, monkeypatch):
+    """bench.py prints traffic / VALU counters only when profiles/traffic.json
+    was taken on its own workload AND on the kernel build the loaded library
+    came from (BUILD_INFO.json's kernel_src_sha, checked by the library's
+    sha256); otherwise it says why."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from bdls_amd import _lib
+    from bdls_amd.provenance import lib_kernel_sha
+    if not os.path.exists(_lib.LIB_PATH):
+        import pytest
+        pytest.skip("library not built")
+    cur = lib_kernel_sha(_lib.LIB_PATH)
+    (tmp_path / "profiles").mkdir()
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    src, kernels, why = bench.load_counters(2, 1048576)
+    assert src is None and "no profiles/traffic.json" in why
+    good = {"workload": "config2:n1048576", "kernel_src_sha": cur, "git_rev": "x",
+            "source": "s", "kernels": {"k_keycomb<bh::F30_p256>": {"bytes_per_launch": 1.0}}}
+    tf = tmp_path / "profiles" / "traffic.json"
+    tf.write_text(json.dumps(dict(good, workload="config2:n65536")))
+    assert "not config2:n1048576" in bench.load_counters(2, 1048576)[2]
+    if cur is None:  # a library build() did not record: nothing is trusted
+        tf.write_text(json.dumps(good))
+        assert "no build record" in bench.load_counters(2, 1048576)[2]
+        return
+    tf.write_text(json.dumps(dict(good, kernel_src_sha="0" * 16)))
+    assert bench.load_counters(2, 1048576)[2].startswith("stale")
+    tf.write_text(json.dumps(good))
+    src, kernels, why = bench.load_counters(2, 1048576)
+    assert why is None and cur in src and kernels == good["kernels"]
