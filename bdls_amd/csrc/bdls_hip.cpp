@@ -214,6 +214,13 @@ struct Dev {
   hipEvent_t build = nullptr; // end of lane 0's last table-build kernel
   bool build_staggered = false;  // lane builds alternate (BH_LANE_STAGGER, default on)
   uint32_t next_lane = 0;
+  // BH_F_ANY_LANE passes: the k-th waits for the (k - kAnyRing)-th (the
+  // header's rotation contract; the lane rotation alone does not give it: at
+  // 3 lanes pass k + 4 shares a lane with pass k + 1, not k, and next_lane is
+  // shared with host and small batches)
+  static constexpr int kAnyRing = 4;
+  hipEvent_t any_ring[kAnyRing] = {nullptr, nullptr, nullptr, nullptr};
+  uint64_t any_count = 0;
   hipEvent_t reg_written = nullptr;  // the last registry write (passes on lanes >= 1 wait for it)
   bool reg_written_recorded = false;
   // deferred timing (bh_timing_begin/_end): one event set per pass, read at end
@@ -393,6 +400,7 @@ int dev_init(Dev& d, int id) {
   for (auto& e : d.ev) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&d.reg_written, hipEventDisableTiming));
+  for (hipEvent_t& e : d.any_ring) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (Lane1& x : d.xl) {
     HIPCHK(hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&x.aux, hipStreamNonBlocking));
@@ -427,6 +435,8 @@ void dev_free(Dev& d) {
     x = Lane1{};
   }
   for (hipEvent_t e : {d.build, d.reg_written})
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : d.any_ring)
     if (e) (void)hipEventDestroy(e);
   if (d.copy) (void)hipStreamSynchronize(d.copy);
   for (auto& g : d.gtab)
@@ -1037,8 +1047,14 @@ int wait_job(bh_job* j) {
       if (!j->parts[k].done) ev = d.slot[j->parts[k].slot].done;
     }
     if (ev) {
-      HIPCHK(hipSetDevice(d.id));
-      (void)hipEventSynchronize(ev);  // errors are reported by finish_part
+      // no early return: every part is still collected (finish_part releases
+      // its slot) and the job freed, whatever fails here
+      const hipError_t e = hipSetDevice(d.id);
+      if (e != hipSuccess && rc == BH_OK) {
+        rc = BH_E_DEVICE;
+        err = std::string("hipSetDevice: ") + hipGetErrorString(e);
+      }
+      if (e == hipSuccess) (void)hipEventSynchronize(ev);  // errors: finish_part reports them
     }
     std::lock_guard<std::mutex> g(d.mu);
     int r = finish_part(j, k);
@@ -1475,8 +1491,15 @@ int bh_verify_dev(int device, int curve, const bh_batch* b, size_t n, uint32_t f
     lane = (int)(d->next_lane++ % lanes());
   hipStream_t s = stream ? (hipStream_t)stream : lane_ref(*d, lane).stream;
   if (n == 0) return BH_OK;
+  const int ring = (int)(d->any_count % Dev::kAnyRing);
+  if (lane >= 0 && d->any_count >= (uint64_t)Dev::kAnyRing)
+    HIPCHK(hipStreamWaitEvent(s, d->any_ring[ring], 0));  // pass k - 4 has finished
   int rc = run_dev(*d, curve, b, n, flags, bitmap_words, reason, s, timing, lane);
   if (rc) return rc;
+  if (lane >= 0) {
+    HIPCHK(hipEventRecord(d->any_ring[ring], s));
+    d->any_count++;
+  }
   if (sync && !timing) HIPCHK(hipStreamSynchronize(s));
   return BH_OK;
 }

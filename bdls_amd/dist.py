@@ -35,6 +35,42 @@ def env_rank():
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
+_VISIBLE_VARS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+                 "GPU_DEVICE_ORDINAL")
+
+
+def visible_device_count(environ=None):
+    """Devices a rank process may see when a launcher or scheduler narrowed
+    them with a visibility variable (the smallest list among those set), or
+    None when none is set (every device of the node is visible). Read from
+    the environment only: counting through HIP would initialise the runtime
+    before the rank has chosen its device."""
+    env = os.environ if environ is None else environ
+    counts = []
+    for k in _VISIBLE_VARS:
+        v = env.get(k)
+        if v is None:
+            continue
+        items = [x for x in v.split(",") if x.strip() != ""]
+        counts.append(len(items))
+    return min(counts) if counts else None
+
+
+def device_for_rank(local: int, environ=None):
+    """(device index, why) for local rank `local`: the rank's own index when
+    more than `local` devices are visible (the launcher left every GPU of the
+    node visible: rank r drives GPU r), else device 0 (the launcher gave each
+    rank exactly its own GPU, e.g. HIP_VISIBLE_DEVICES=<r>)."""
+    vis = visible_device_count(environ)
+    if vis is None:
+        return local, "all devices visible: device = LOCAL_RANK"
+    if vis > local:
+        return local, f"{vis} devices visible: device = LOCAL_RANK"
+    if vis <= 0:
+        return 0, "visibility variable lists no device: device 0 (bh_init will fail loudly)"
+    return 0, f"{vis} device(s) visible to this rank (LOCAL_RANK {local}): device 0"
+
+
 def shard_range(n_total: int, rank: int, world: int, align: int = 64):
     """Contiguous [lo, hi) of rank in a batch of n_total records; boundaries are
     multiples of `align` so per-rank bitmap words concatenate without shifts."""

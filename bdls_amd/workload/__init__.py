@@ -83,6 +83,118 @@ def generate_shard(n_total: int, lo: int, count: int, nkeys: int, msg_len: int =
     return w
 
 
+_FIELDS = (("pub", np.uint8, 64), ("msg", np.uint8, None), ("msg_off", np.uint64, 1),
+           ("msg_len", np.uint32, 1), ("sig", np.uint8, SIG_STRIDE), ("sig_off", np.uint64, 1),
+           ("sig_len", np.uint32, 1), ("reason", np.uint8, 1), ("cls", np.uint8, 1))
+
+
+def _alloc_workload(n: int, msg_len: int, alloc) -> Workload:
+    return Workload(
+        pub=_empty(alloc, n * 64, np.uint8), msg=_empty(alloc, n * msg_len, np.uint8),
+        msg_off=_empty(alloc, n, np.uint64), msg_len=_empty(alloc, n, np.uint32),
+        sig=_empty(alloc, n * SIG_STRIDE, np.uint8), sig_off=_empty(alloc, n, np.uint64),
+        sig_len=_empty(alloc, n, np.uint32), reason=np.empty(n, np.uint8),
+        cls=np.empty(n, np.uint8))
+
+
+def cache_key(n_total, lo, count, nkeys, msg_len, corrupt_den, seed, family="SHA2") -> str:
+    return (f"p256_{family}_t{n_total}_lo{lo}_c{count}_k{nkeys}_m{msg_len}_d{corrupt_den}"
+            f"_s{seed}_v1")
+
+
+def generate_shard_cached(n_total: int, lo: int, count: int, nkeys: int, msg_len: int = 256,
+                          corrupt_den: int = 16, seed: int = 2, nthreads: int | None = None,
+                          alloc=None, cache_dir: str | None = None, save: bool = True,
+                          chunk: int = 1 << 20, log=None) -> tuple[Workload, dict]:
+    """generate_shard for big unique-key shards (config 5: SURVEY 8(d) row 5,
+    "generated once ... and cached on local disk"):
+      * the arrays are allocated ONCE (e.g. page-locked through `alloc`) and
+        filled in place -- from the cache directory when a complete copy of
+        this exact shard is there, else by the generator in chunks of `chunk`
+        records (record i is a function of (seed, i), so chunks concatenate to
+        the same shard), calling log(msg) after each chunk so a long run
+        reports progress;
+      * a freshly generated shard is written to cache_dir/<key>/ (one raw file
+        per array + meta.json last, so a partial write is never taken for a
+        copy) when `save` and the file system has room for it.
+    Returns (workload, info) -- info says where the records came from."""
+    log = log or (lambda m: None)
+    w = _alloc_workload(count, msg_len, alloc)
+    info = {"source": "generator", "cache_dir": cache_dir}
+    key = cache_key(n_total, lo, count, nkeys, msg_len, corrupt_den, seed)
+    path = os.path.join(cache_dir, key) if cache_dir else None
+    meta_path = os.path.join(path, "meta.json") if path else None
+    t0 = __import__("time").time()
+    if meta_path and os.path.exists(meta_path):
+        import json
+        with open(meta_path) as f:
+            meta = json.load(f)
+        if meta.get("key") == key:
+            for name, _, _ in _FIELDS:
+                a = getattr(w, name)
+                mv = memoryview(a.view(np.uint8).reshape(-1))
+                with open(os.path.join(path, name + ".bin"), "rb", buffering=0) as f:
+                    got, step = 0, 1 << 28
+                    while got < len(mv):
+                        k = f.readinto(mv[got:got + step])
+                        if not k:
+                            raise RuntimeError(f"cache file {name}.bin is short")
+                        got += k
+                log(f"cache: loaded {name} ({len(mv) / 1e9:.2f} GB)")
+            info.update(source="cache", path=path, load_s=round(__import__("time").time() - t0, 2))
+            return w, info
+    if not os.path.exists(_LIB):
+        raise RuntimeError(f"{_LIB} not built (run `make`)")
+    L = ctypes.CDLL(_LIB)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.gen_p256_shard.argtypes = [sz, sz, sz, sz, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                 ctypes.c_int, ctypes.c_int] + [vp] * 9
+    L.gen_p256_shard.restype = ctypes.c_int
+    if nthreads is None:
+        nthreads = min(16, os.cpu_count() or 1)
+    # shared keys are derived once per call: chunk only unique-key shards
+    step = chunk if nkeys >= n_total else count
+    w.sig[:] = 0
+    for b in range(0, count, step):
+        m = min(step, count - b)
+        rc = L.gen_p256_shard(n_total, lo + b, m, nkeys, msg_len, corrupt_den, seed, nthreads, 0,
+                              w.pub[64 * b:].ctypes.data, w.msg[msg_len * b:].ctypes.data,
+                              w.msg_off[b:].ctypes.data, w.msg_len[b:].ctypes.data,
+                              w.sig[SIG_STRIDE * b:].ctypes.data, w.sig_off[b:].ctypes.data,
+                              w.sig_len[b:].ctypes.data, w.reason[b:].ctypes.data,
+                              w.cls[b:].ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"gen_p256_shard failed: {rc}")
+        if b:  # the generator's offsets are local to its call
+            w.msg_off[b:b + m] += np.uint64(msg_len * b)
+            w.sig_off[b:b + m] += np.uint64(SIG_STRIDE * b)
+        if step < count:
+            log(f"generated {b + m}/{count} records ({nthreads} threads)")
+    info["gen_s"] = round(__import__("time").time() - t0, 2)
+    if path and save:
+        import json
+        import shutil
+        need = sum(getattr(w, name).nbytes for name, _, _ in _FIELDS)
+        os.makedirs(cache_dir, exist_ok=True)
+        free = shutil.disk_usage(cache_dir).free
+        if free < need * 1.1 + (1 << 30):
+            info["cache_skipped"] = f"{free / 1e9:.1f} GB free < {need / 1e9:.1f} GB needed"
+            log(f"cache: not written ({info['cache_skipped']})")
+            return w, info
+        t1 = __import__("time").time()
+        os.makedirs(path, exist_ok=True)
+        if os.path.exists(meta_path):
+            os.unlink(meta_path)
+        for name, _, _ in _FIELDS:
+            getattr(w, name).tofile(os.path.join(path, name + ".bin"))
+            log(f"cache: wrote {name}")
+        with open(meta_path + ".tmp", "w") as f:
+            json.dump({"key": key, "bytes": need}, f)
+        os.replace(meta_path + ".tmp", meta_path)
+        info.update(saved=path, save_s=round(__import__("time").time() - t1, 2))
+    return w, info
+
+
 def generate(n: int, nkeys: int, msg_len: int = 256, corrupt_den: int = 16, seed: int = 2,
              nthreads: int | None = None, family: str = "SHA2", alloc=None) -> Workload:
     """A whole batch of n records (see generate_shard)."""

@@ -43,6 +43,18 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+_T0 = time.time()
+
+
+def phase(msg: str) -> None:
+    """A flushed, timestamped progress line on stderr (stdout carries only the
+    JSON line): every long phase of a run -- generation, page-locked
+    allocations, uploads, each pass of a multi-pass batch -- says when it
+    starts and ends, so a run that stalls shows where (the
+    config-5 run was killed after 180 s of silence)."""
+    sys.stderr.write(f"[bench +{time.time() - _T0:8.1f}s rank {os.environ.get('RANK', '0')}] "
+                     f"{msg}\n")
+    sys.stderr.flush()
 
 # Algorithmic work per verify in SURVEY.md 8(d) units: F_p mul/sqr x 128 u32
 # MACs (64 product + 64 reduction). The variable-base ladder is schedule S0
@@ -138,6 +150,11 @@ def parse(argv=None):
     ap.add_argument("--side-steps", type=int, default=20)
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the launcher and the rank plumbing only")
+    ap.add_argument("--c5-cache", default=os.environ.get("BDLS_C5_CACHE", ""),
+                    help="config 5: directory of the on-disk copy of the seeded shard "
+                         "(default: <tmp>/bdls_c5_cache; 'off' disables)")
+    ap.add_argument("--c5-cache-save", type=int, default=1,
+                    help="config 5: write a freshly generated shard to the cache")
     return ap.parse_args(argv)
 
 
@@ -213,6 +230,7 @@ def bench_latency(a, rank, world, local):
     --steps calls. N GPUs run N independent replicas (the path does not shard
     at this size)."""
     from bdls_amd import _lib, dist, workload
+    local, _ = dist.device_for_rank(local)
     L = _lib.lib()
     _lib.check(L.bh_init(1 << local, 0))
     assert "torch" not in sys.modules, "torch must not share a process with libbdlship.so"
@@ -567,43 +585,74 @@ def bench_throughput(a, rank, world, local):
         desc = (f"BASELINE config 2: {a.n} records/GPU, {a.msg_len}B messages, {nkeys} distinct "
                 f"keys, 1/{corrupt} corrupted, fused SHA-256")
     n = hi - lo
+    dev, dev_why = dist.device_for_rank(local)
+    phase(f"config {a.config}: {n} records [{lo}, {hi}) of {n_total}; device {dev} ({dev_why})")
+    local = dev  # the device index every call below addresses
 
     # Page-locked host memory comes from libbdlship.so (bh_host_alloc); torch
     # ships its own HIP runtime and is never imported into a rank process.
     L = _lib.lib()
     _lib.check(L.bh_init(1 << local, 0))
     assert "torch" not in sys.modules, "torch must not share a process with libbdlship.so"
+    phase("bh_init done")
 
     pinned = []
 
     def alloc(nbytes):
+        t = time.time()
         h = _lib.HostArray(nbytes)
         pinned.append(h)
+        if nbytes >= (256 << 20):
+            phase(f"page-locked {nbytes / 1e9:.2f} GB in {time.time() - t:.2f} s")
         return h.u8
 
     t_gen = time.time()
     # generator threads: the CPUs this node's ranks may actually use (affinity
-    # and cgroup quota, not os.cpu_count()) shared by the local ranks, at least
-    # 4 each (config 5 at 8 ranks generates 8.4M unique keys per rank)
+    # and cgroup quota, not os.cpu_count()) shared by the local ranks -- 8
+    # ranks on a 16-CPU quota get 2 each, not 4
     cpus = host_cpus()
     usable = int(min(cpus.get("affinity", cpus["nproc"]),
                      cpus.get("cgroup_quota_cpus", cpus["nproc"]))) or 1
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", min(world, 8)))
-    gen_threads = max(4, min(32, usable // max(1, local_world)))
-    w = workload.generate_shard(n_total if a.config == 5 else a.n, lo, n, nkeys, a.msg_len,
-                                corrupt, seed=seed, nthreads=gen_threads, alloc=alloc)
+    gen_threads = max(1, min(32, usable // max(1, local_world)))
+    gen_info = {"threads": gen_threads}
+    if a.config == 5:
+        # one seeded unique-key batch: generated in 1M-record chunks with a
+        # progress line each, into page-locked arrays allocated once, and
+        # kept on local disk for the next run
+        import tempfile
+        cache = a.c5_cache or os.path.join(tempfile.gettempdir(), "bdls_c5_cache")
+        phase(f"shard: cache {cache if cache != 'off' else 'off'}, {gen_threads} generator "
+              f"threads")
+        w, info = workload.generate_shard_cached(
+            n_total, lo, n, nkeys, a.msg_len, corrupt, seed=seed, nthreads=gen_threads,
+            alloc=alloc, cache_dir=None if cache == "off" else cache, save=bool(a.c5_cache_save),
+            log=phase)
+        gen_info.update(info)
+    else:
+        w = workload.generate_shard(a.n, lo, n, nkeys, a.msg_len, corrupt, seed=seed,
+                                    nthreads=gen_threads, alloc=alloc)
     t_gen = time.time() - t_gen
+    phase(f"workload ready in {t_gen:.1f} s ({gen_info.get('source', 'generator')})")
     flags = _lib.BH_F_HASH_SHA256
     hb = _lib.BhBatch(*[x.ctypes.data for x in (w.pub, w.sig, w.sig_off, w.sig_len, w.msg,
                                                 w.msg_off, w.msg_len)])
-    compact = a.host_layout == "compact"
+    # config 5's keys are all distinct: the compact layout would hold the whole
+    # batch a second time in page-locked memory (and its key dedup / signature
+    # repack are minutes of numpy at 64M records) to save nothing -- plain
+    layout = "plain" if a.config == 5 else a.host_layout
+    compact = layout == "compact"
     if compact:
         # what a Go BatchVerify hands over: each distinct key once + a u32
         # index per record, lengths only (fixed 256-byte messages: none)
+        t = time.time()
         carrs, cb = _lib.compact_layout(w.pub, w.sig, w.sig_off, w.sig_len, w.msg, w.msg_off,
                                         w.msg_len, alloc=alloc)
+        layout_s = time.time() - t
+        phase(f"compact layout built in {layout_s:.2f} s")
     depth = 3  # batches in flight (the library keeps 3 pipeline slots per device)
     outs = [(np.zeros((n + 7) // 8, np.uint8), np.zeros(n, np.uint8)) for _ in range(depth)]
+    multipass = n > (1 << 22)
 
     def submit(k):
         job = ctypes.c_void_p()
@@ -625,14 +674,20 @@ def bench_throughput(a, rank, world, local):
         for k in range(steps):
             if len(q) == depth:
                 _lib.check(L.bh_verify_wait(q.popleft()))
+                if multipass:
+                    phase(f"host path: batch {k - depth} done")
             q.append(submit(k))
         while q:
             _lib.check(L.bh_verify_wait(q.popleft()))
+            if multipass:
+                phase("host path: batch done")
 
+    phase(f"host path: {a.warmup} warmup batches")
     run_host(a.warmup)
     _lib.check(L.bh_sync(local))
     # one batch alone (nothing in flight): H2D + verify + D2H latency, and the
     # page-locked H2D bandwidth of the batch's largest array
+    phase("host path: one batch alone")
     t = time.perf_counter()
     run_host(1)
     single_ms = (time.perf_counter() - t) * 1e3
@@ -656,9 +711,11 @@ def bench_throughput(a, rank, world, local):
     tm = _lib.BhTiming()
     if not a.hbm_resident:
         _lib.check(L.bh_timing_begin(local))
+    phase(f"host path: {a.steps} timed batches")
     t0 = time.perf_counter()
     run_host(a.steps)
     t1 = time.perf_counter()
+    phase(f"host path: {(t1 - t0) * 1e3 / a.steps:.2f} ms per batch")
     if not a.hbm_resident:
         _lib.check(L.bh_timing_end(local, ctypes.byref(tm)))
     dist.barrier(world)
@@ -675,8 +732,11 @@ def bench_throughput(a, rank, world, local):
     resident = None
     if a.hbm_resident:
         DA = _lib.DeviceArray
+        phase("resident: uploading the batch to HBM")
         d = [DA.from_numpy(local, x) for x in (w.pub, w.sig, w.sig_off, w.sig_len, w.msg,
                                                w.msg_off, w.msg_len)]
+        # one output set per in-flight pass: BH_F_ANY_LANE orders pass k + 4
+        # after pass k (bdls_hip.cpp any_lane ring), so 4 rotating sets are safe
         outs_dev = [(DA(local, ((n + 63) // 64) * 8), DA(local, n)) for _ in range(MAX_LANES)]
         db = _lib.BhBatch(*[x.ptr for x in d])
         lane_flag = _lib.BH_F_ANY_LANE if a.resident_lanes else 0
@@ -685,15 +745,18 @@ def bench_throughput(a, rank, world, local):
             words, dreason = outs_dev[k % MAX_LANES]
             _lib.check(L.bh_verify_dev(local, 0, ctypes.byref(db), n, f, words.ptr,
                                        dreason.ptr, None, 0, None))
+        phase("resident: warmup passes")
         for k in range(max(1, a.warmup)):
             step(k)
         _lib.check(L.bh_sync(local))
         dist.barrier(world)
+        phase(f"resident: {a.steps} timed passes")
         r0 = time.perf_counter()
         for k in range(a.steps):
             step(k)
         _lib.check(L.bh_sync(local))
         r1 = time.perf_counter()
+        phase(f"resident: {(r1 - r0) * 1e3 / a.steps:.2f} ms per pass")
         r_el = dist.max_over_ranks(r1 - r0, world)
         r_ok = True
         for words, dreason in outs_dev[:min(MAX_LANES, a.steps)]:
@@ -702,6 +765,7 @@ def bench_throughput(a, rank, world, local):
             r_ok = r_ok and bool((dreason.to_numpy(np.uint8, n) == w.reason).all()
                                  and (rbits == w.expected_valid).all())
         # the per-kernel timing passes (serialised, not part of `value`)
+        phase(f"resident: {a.steps} serialised passes (per-kernel HIP-event times)")
         _lib.check(L.bh_timing_begin(local))
         t_t0 = time.perf_counter()
         for k in range(a.steps):
@@ -709,6 +773,7 @@ def bench_throughput(a, rank, world, local):
         _lib.check(L.bh_sync(local))
         t_el = time.perf_counter() - t_t0
         _lib.check(L.bh_timing_end(local, ctypes.byref(tm)))
+        phase("resident: done")
         parity_ok = parity_ok and r_ok
         resident = {"value": round(dist.sum_over_ranks(n, world) * a.steps / r_el, 1),
                     "ms_per_step": round(r_el * 1e3 / a.steps, 3), "parity": r_ok,
@@ -775,7 +840,12 @@ def bench_throughput(a, rank, world, local):
                                + "from page-locked host buffers: H2D + verify + D2H per step, "
                                "batches in flight over the compute lanes (SURVEY 8(d)'s "
                                "config-2 timed quantity, PCIe-inclusive)"),
-                      "layout": a.host_layout,
+                      "layout": layout,
+                      "layout_build_s": round(layout_s, 3) if compact else None,
+                      "layout_note": ("the bh_cbatch arrays (np.unique key dedup + signature "
+                                      "repack) are built once before the timed region; a Go "
+                                      "caller pays that per BatchVerify (layout_build_s)"
+                                      if compact else "the generator's arrays as they are"),
                       "single_batch_ms": round(single_ms, 3), "batch_bytes": batch_bytes,
                       "h2d_gbps_pinned": round(h2d_gbps, 2),
                       # the host path's own roofline: every batch crosses PCIe once
@@ -808,6 +878,8 @@ def bench_throughput(a, rank, world, local):
             "alg_bytes_per_record": alg_bytes_per_record(a.msg_len),
         },
         "gen_s": round(t_gen, 2),
+        "workload_source": gen_info,
+        "device": {"index": local, "why": dev_why},
     }
     # the whole step priced two ways: the F_p ops this engine actually runs
     # (key tables skip the S0 doublings), and SURVEY 8(d)'s fixed schedule S0

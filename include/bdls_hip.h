@@ -66,9 +66,11 @@ extern "C" {
                                consecutive calls rotate over the device's compute lanes
                                (BH_LANES, default 3, at most 4), each with its own workspace,
                                so a pass runs beside the previous calls' passes as host
-                               batches do. Its outputs must not alias an in-flight call's
-                               (4 rotating output sets are always safe); bh_sync waits for
-                               every lane.
+                               batches do. The k-th BH_F_ANY_LANE pass of a device is
+                               ordered after the (k-4)-th (whatever lane each took and
+                               whatever other work ran between them), so a caller that
+                               rotates 4 output sets never has two in-flight passes
+                               writing one set; bh_sync waits for every lane.
                                Ignored elsewhere (host batches already alternate lanes). */
 
 #define BH_CURVE_P256 0

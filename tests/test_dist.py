@@ -20,6 +20,25 @@ def test_shard_ranges_cover_and_align():
                 assert lo % 64 == 0 or lo == n
 
 
+@pytest.mark.parametrize("env,local,want", [
+    ({}, 0, 0), ({}, 5, 5),                                        # nothing narrowed
+    ({"HIP_VISIBLE_DEVICES": "3"}, 3, 0),                          # one GPU per rank
+    ({"HIP_VISIBLE_DEVICES": "3"}, 0, 0),
+    ({"HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7"}, 7, 7),            # all eight listed
+    ({"ROCR_VISIBLE_DEVICES": "GPU-ab12"}, 6, 0),                  # UUID form, one device
+    ({"HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7", "ROCR_VISIBLE_DEVICES": "4"}, 4, 0),
+    ({"CUDA_VISIBLE_DEVICES": "0,1"}, 1, 1), ({"CUDA_VISIBLE_DEVICES": "0,1"}, 2, 0),
+])
+def test_device_for_rank(env, local, want):
+    """a rank drives device LOCAL_RANK only when more than
+    LOCAL_RANK devices are visible; a launcher that gives each rank its own GPU
+    (a visibility list of length 1) maps every rank to device 0."""
+    dev, why = dist.device_for_rank(local, env)
+    assert dev == want, why
+    assert dist.visible_device_count(env) == (None if not env else min(
+        len(v.split(",")) for v in env.values()))
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

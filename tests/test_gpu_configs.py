@@ -401,3 +401,68 @@ def test_resident_passes_on_two_lanes(L):
     for w, d, words, reason, b in bufs:
         for x in d + [words, reason]:
             x.free()
+
+
+def test_any_lane_four_rotating_output_sets(L):
+    """the BH_F_ANY_LANE contract -- 4 rotating output
+    sets are safe -- now holds by construction (pass k + 4 waits for pass k,
+    bdls_hip.cpp any_ring), at every lane count and with host batches taking
+    lanes in between. 12 passes over 3 DIFFERENT batches into 4 output sets:
+    after bh_sync set s holds exactly pass 8 + s's result (batch (8 + s) % 3)."""
+    DA = _lib.DeviceArray
+    n = 60_000
+    ws = [workload.generate(n, [3000, 60_000, 700][k], 96, 8, seed=90 + k) for k in range(3)]
+    ins = []
+    for w in ws:
+        d = [DA.from_numpy(0, x) for x in w.arrays()]
+        ins.append((d, _lib.BhBatch(*[x.ptr for x in d])))
+    outs = [(DA(0, ((n + 63) // 64) * 8), DA(0, n)) for _ in range(4)]
+    small = workload.generate(3000, 40, 64, 8, seed=99)
+    for k in range(12):
+        words, reason = outs[k % 4]
+        _lib.check(L.bh_verify_dev(0, 0, ctypes.byref(ins[k % 3][1]), n,
+                                   _lib.BH_F_HASH_SHA256 | _lib.BH_F_ANY_LANE, words.ptr,
+                                   reason.ptr, None, 0, None))
+        if k % 5 == 2:  # a host batch takes a lane in between
+            _, rs = host_verify(L, small)
+            assert (rs == small.reason).all()
+    _lib.check(L.bh_sync(0))
+    for s, (words, reason) in enumerate(outs):
+        w = ws[(8 + s) % 3]
+        bits = np.unpackbits(words.to_numpy(np.uint64, (n + 63) // 64).view(np.uint8),
+                             bitorder="little")[:n].astype(bool)
+        assert (reason.to_numpy(np.uint8, n) == w.reason).all(), s
+        assert (bits == w.expected_valid).all(), s
+    for d, _ in ins:
+        for x in d:
+            x.free()
+    for pair in outs:
+        for x in pair:
+            x.free()
+
+
+def test_config2_exact_shape(L):
+    """BASELINE config 2's exact batch -- 1,048,576 records,
+    65,536 keys, 256-B messages, 1/16 corrupted, seed 2 (bench.py's default
+    line) -- through the compact host ABI (the bench's host path) and the
+    device-resident ABI (its `value`): bitmap and reasons against construction,
+    the routes the roofline prices (every key-table record on the comb, every
+    key used >= 4 times gets a table), and a 300-record orc.csp_verify sample."""
+    n, nkeys = 1 << 20, 1 << 16
+    w = workload.generate(n, nkeys, 256, 16, seed=2)
+    orc_sample(w, 300, seed=2)
+    carrs, cb = _lib.compact_layout(*w.arrays())
+    # the off-curve / >= p corruptions each add a distinct (invalid) key row
+    bad_keys = int(np.isin(w.cls, [6, 7]).sum())
+    assert nkeys <= len(carrs["keys"]) // 64 <= nkeys + bad_keys
+    bm = np.zeros(n // 8, np.uint8)
+    rs = np.zeros(n, np.uint8)
+    _lib.check(L.bh_verify_compact(0, ctypes.byref(cb), n, _lib.BH_F_HASH_SHA256,
+                                   bm.ctypes.data, rs.ctypes.data))
+    assert (rs == w.reason).all()
+    assert (np.unpackbits(bm, bitorder="little").astype(bool) == w.expected_valid).all()
+    bits, dreason, tm = dev_verify(L, w)
+    assert (dreason == w.reason).all() and (bits == w.expected_valid).all()
+    ok_prep = int((w.reason == 0).sum() + (w.reason == 9).sum())  # math-checked records
+    assert tm.n_keycomb + tm.n_ladder == ok_prep
+    assert tm.n_keytables >= 65_000 and tm.n_keycomb >= 0.99 * ok_prep

