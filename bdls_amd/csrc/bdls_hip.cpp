@@ -78,7 +78,7 @@ namespace {
   } while (0)
 
 constexpr size_t kMaxChunk = size_t(1) << 22;  // records per kernel pass (workspace bound)
-constexpr size_t kGtabWords = size_t(bh::kCombWindows) * bh::kCombEntries * bh::kGEntry;
+constexpr size_t kGtabWords = bh::kGTabAllWords;  // 13-bit G comb + folded tables
 constexpr size_t kDefaultRegCap = size_t(1) << 16;
 
 size_t round64(size_t n) { return (n + 63) & ~size_t(63); }

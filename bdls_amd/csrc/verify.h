@@ -1438,6 +1438,207 @@ BH_HD void q_llcomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32
   }
 }
 
+// ---- u1 G folded into the key comb's Horner (round 5) ---------------------------
+// The G half shares the key comb's s - 1 = 36 doublings. u1 is recoded like u2
+// (ll_slices: k = u1 or u1 + n, t = 7 teeth x s = 37 columns, digits +-1), so
+// u1 G = sum_j 2^j W_j G with W_j = sum_i d_(i,j) 2^(s i). The Horner adds, at
+// every odd column j = 35, 33, ..., 1, the column pair (j + 1, j) as ONE point
+//   (2 W_(j+1) + W_j) G
+// (adding W_(j+1) one column late, doubled once, is the same sum), and at
+// column 0 the single column W_0 G. The pair table holds the 2^13 sign
+// patterns whose top digit (tooth t - 1 of column j + 1) is +1 -- every entry
+// a multiple of G in (2^223 - 2^222, 3 * 2^222), never infinity; the other
+// 2^13 patterns are their negatives -- and the single-column table the 2^6
+// patterns of one column with its top digit +1: 8,256 affine points, 660 KB
+// per curve (L2-resident), built at bh_init. 18 + 1 = 19 mixed additions per
+// record instead of the separate 13-bit G comb's 20, and no u1 G partial sum
+// stored by the build kernel and reloaded, no final Jacobian addition A + B.
+constexpr uint32_t kG2Ent = 1u << (2 * kLLTeeth - 1);  // two-column entries
+constexpr uint32_t kG1Ent = kLLEnt;                     // single-column entries
+constexpr size_t kG2Words = (size_t)(kG2Ent + kG1Ent) * kLLAff;
+// Per curve, one device buffer holds the 13-bit G comb (ladder records,
+// registry-table records, small batches) and, after it, the folded tables.
+constexpr size_t kGCombWords = (size_t)kCombWindows * kCombEntries * kGEntry;
+constexpr size_t kGTabAllWords = kGCombWords + kG2Words;
+static_assert(kGCombWords % 4 == 0, "folded tables 16-byte aligned");
+BH_HD const uint32_t* g2_of(const uint32_t* gtab) { return gtab + kGCombWords; }
+static_assert(kLLSpace % 2 == 1, "pairs (j + 1, j) at odd j cover columns 1 .. s - 1");
+
+// Entry t of the folded G tables: t < kG2Ent the pair pattern (hi, lo) =
+// ((1 << (t_teeth - 1)) | t >> t_teeth, t & (2^t - 1)) -> (2 W(hi) + W(lo)) G;
+// else the single column (1 << (t - 1)) | (t - kG2Ent) -> W G. Affine,
+// canonical Montgomery radix 2^30, in the 80-byte llaff layout. One lane per
+// entry at bh_init (and in the host harness).
+template <class P>
+BH_HD void gtab2_entry(uint32_t t, uint32_t* out) {
+  constexpr uint32_t top = 1u << (kLLTeeth - 1), all = (1u << kLLTeeth) - 1u;
+  int c[kLLTeeth];
+  if (t < kG2Ent) {
+    const uint32_t hi = top | (t >> kLLTeeth), lo = t & all;
+    for (int i = 0; i < kLLTeeth; i++)
+      c[i] = 2 * (2 * (int)((hi >> i) & 1u) - 1) + (2 * (int)((lo >> i) & 1u) - 1);
+  } else {
+    const uint32_t b = top | (t - kG2Ent);
+    for (int i = 0; i < kLLTeeth; i++) c[i] = 2 * (int)((b >> i) & 1u) - 1;
+  }
+  // v = sum c_i 2^(s i) > 0 (the top term dominates), as 9 x 32-bit words
+  uint32_t pos[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, neg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < kLLTeeth; i++) {
+    uint32_t* dst = c[i] > 0 ? pos : neg;
+    const uint64_t mag = (uint64_t)(c[i] > 0 ? c[i] : -c[i]) << ((kLLSpace * i) & 31);
+    const int wd = (kLLSpace * i) >> 5;
+    uint64_t cy = mag;
+    for (int q = wd; q < 9 && cy; q++) {
+      cy += dst[q];
+      dst[q] = (uint32_t)cy;
+      cy >>= 32;
+    }
+  }
+  uint32_t v[9];
+  int64_t br = 0;
+  for (int q = 0; q < 9; q++) {
+    br += (int64_t)pos[q] - (int64_t)neg[q];
+    v[q] = (uint32_t)br;
+    br >>= 32;  // arithmetic: 0 or -1
+  }
+  // v G by left-to-right double-and-add from the affine G: A = m G with
+  // 2 <= m < 2^227 before every addition, never +-G
+  uint32_t gx[9], gy[9];
+  f_const(gx, P::gx_m);
+  f_const(gy, P::gy_m);
+  int topbit = 287;
+  while (topbit > 0 && !((v[topbit >> 5] >> (topbit & 31)) & 1u)) topbit--;
+  J30 A;
+  f_copy(A.X, gx);
+  f_copy(A.Y, gy);
+  f_const(A.Z, P::r1);
+  for (int b = topbit - 1; b >= 0; b--) {
+    j_dbl<P>(A, A);
+    if ((v[b >> 5] >> (b & 31)) & 1u) {
+      bool same;
+      (void)j_madd<P>(A, A, gx, gy, &same);
+    }
+  }
+  uint32_t z[9], zi[9], zi2[9], x[9], y[9];
+  f_reduce<P>(z, A.Z);
+  f_inv<P>(zi, z);
+  f_sqr<P>(zi2, zi);
+  f_mul<P>(x, A.X, zi2);
+  f_mul<P>(zi2, zi2, zi);
+  f_mul<P>(y, A.Y, zi2);
+  f_reduce<P>(x, x);
+  f_reduce<P>(y, y);
+  llaff_store(out, 0, x, y);
+}
+
+// The folded G entry added at column j of u1's slices: the pair (j + 1, j) for
+// odd j, the single column for j = 0 (index past the pair table). neg: the
+// entry's negative (all digits flipped).
+BH_HD void g2_column(const uint64_t gl[kLLTeeth], int j, uint32_t& idx, bool& neg) {
+  if (j == 0) {
+    ll_column(gl, 0, idx, neg);
+    idx += kG2Ent;
+    return;
+  }
+  uint32_t hi = 0, lo = 0;
+#pragma unroll
+  for (int t = 0; t < kLLTeeth; t++) {
+    hi |= (uint32_t)((gl[t] >> (j + 1)) & 1ull) << t;
+    lo |= (uint32_t)((gl[t] >> j) & 1ull) << t;
+  }
+  neg = ((hi >> (kLLTeeth - 1)) & 1u) == 0u;
+  constexpr uint32_t all = (1u << kLLTeeth) - 1u;
+  if (neg) {
+    hi = ~hi & all;
+    lo = ~lo & all;
+  }
+  idx = ((hi & (all >> 1)) << kLLTeeth) | lo;
+}
+
+// A += +-(tx, ty) with the explicit degenerate cases (A at infinity: A = T;
+// A == T: 2 T; A == -T: infinity), as a branch the lanes skip together.
+template <class P>
+BH_HD void ll_madd(J30& A, bool& a_inf, const uint32_t tx[9], uint32_t ty[9], bool neg,
+                   const uint32_t one[9]) {
+  uint32_t nty[9];
+  f_neg<P, 64>(nty, ty);
+  f_sel(ty, neg, nty, ty);
+  bool same;
+  const bool deg = j_madd<P>(A, A, tx, ty, &same);
+  if (a_inf || deg) {  // rare (crafted scalars)
+    if (a_inf || same) {
+      J30 T;
+      f_copy(T.X, tx);
+      f_copy(T.Y, ty);
+      f_copy(T.Z, one);
+      if (a_inf) j_copy(A, T);
+      else j_dbl<P>(A, T);
+      a_inf = false;
+    } else {
+      a_inf = true;
+    }
+  }
+}
+
+// u1 G + u2 Q from the key's signed comb table (stride as q_llcomb) and the
+// folded G tables g2: Horner from the top column; at column j a doubling, the
+// key table's column, and at odd j and j = 0 the folded G entry (loaded one
+// step ahead, under the doubling).
+template <class P>
+BH_HD void q_llcomb_g(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab,
+                      uint32_t stride, const uint32_t* g2) {
+  uint32_t u2[8], u1[8], one[9];
+  ld8(u2, w.r, i, w.ns);
+  ld8(u1, w.e, i, w.ns);
+  f_const(one, P::r1);
+  uint64_t sl[kLLTeeth], gl[kLLTeeth];
+  ll_slices<P>(sl, u2);
+  ll_slices<P>(gl, u1);
+  uint32_t idx;
+  bool neg;
+  ll_column(sl, kLLSpace - 1, idx, neg);  // top column: top bit set, +E[idx]
+  if (stride) llent_load(A.X, A.Y, tab + idx * stride);
+  else llaff_load(A.X, A.Y, tab, idx);
+  f_copy(A.Z, one);
+  a_inf = false;
+  uint32_t gx[9], gy[9], gidx;
+  bool gneg;
+  g2_column(gl, kLLSpace - 2, gidx, gneg);
+  llaff_load(gx, gy, g2, gidx);
+#pragma unroll 1
+  for (int j = kLLSpace - 2; j >= 0; j--) {
+    j_dbl<P>(A, A);  // (while a_inf, A is a placeholder the next point replaces)
+    const int nadd = ((j & 1) || j == 0) ? 2 : 1;
+#pragma unroll 1
+    for (int a = 0; a < nadd; a++) {
+      uint32_t tx[9], ty[9];
+      if (a == 0) {
+        ll_column(sl, j, idx, neg);
+        if (stride) llent_load(tx, ty, tab + idx * stride);
+        else llaff_load(tx, ty, tab, idx);
+      } else {
+        f_copy(tx, gx);
+        f_copy(ty, gy);
+        neg = gneg;
+      }
+      ll_madd<P>(A, a_inf, tx, ty, neg, one);
+    }
+    if (nadd == 2 && j > 0) {  // the next folded G entry: column j - 2, or column 0
+      g2_column(gl, j >= 3 ? j - 2 : 0, gidx, gneg);
+      llaff_load(gx, gy, g2, gidx);
+    }
+  }
+}
+
+template <class P>
+BH_HD bool stage_keycomb_fold(const Work& w, uint32_t i, const uint32_t* tab, uint32_t stride,
+                              const uint32_t* g2) {
+  J30 A;
+  bool a_inf;
+  q_llcomb_g<P>(A, a_inf, w, i, tab, stride, g2);
+  return finish_check<P>(w, i, A, a_inf, A, true);
+}
+
 template <class P>
 BH_HD bool stage_keycomb(const Work& w, const uint32_t* gtab, uint32_t i, const uint32_t* tab) {
   J30 A, B;

@@ -631,7 +631,10 @@ __global__ __launch_bounds__(256) BH_KEYCOMB_ATTR void k_keycomb(Work w, Plan pl
   if (!have) return;
   const bool in_lds = lcl && slot < kLdsTabs;
   const uint32_t* tab = in_lds ? s_tab + slot * kLdsTabWords : tab_ptr(pl, g, id);
-  const bool ok = stage_keycomb_q<P>(w, i, j, tab, lcl, lcl ? (in_lds ? kLLLds : kLLAff) : 0u);
+  // per-batch comb tables: u1 G folded into the Horner (round 5, verify.h
+  // q_llcomb_g); registry (windowed) tables: their windows + the 13-bit G comb
+  const bool ok = lcl ? stage_keycomb_fold<P>(w, i, tab, in_lds ? kLLLds : kLLAff, g2_of(gtab))
+                      : stage_keycomb<P>(w, gtab, i, tab);
   reason[i] = ok ? R_OK : R_MATH;
 }
 
@@ -763,12 +766,17 @@ __global__ __launch_bounds__(256) void k_small_lad(Work w, const uint32_t* __res
   if (l == 0) reason[j] = finish_check<P>(w, j, C, c_inf, C, true) ? R_OK : R_MATH;
 }
 
-// G comb table (see verify.h gtab_entry): one lane per entry.
+// G tables (verify.h gtab_entry, gtab2_entry): one lane per entry -- the
+// 13-bit comb, then the folded two-column / single-column tables after it.
 template <class P>
 __global__ __launch_bounds__(64) void k_gtab_build(uint32_t* gtab) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (uint32_t)(kCombWindows * kCombEntries)) return;
-  gtab_entry<P>(t, gtab + (size_t)t * kGEntry);
+  constexpr uint32_t nc = (uint32_t)(kCombWindows * kCombEntries);
+  if (t < nc) {
+    gtab_entry<P>(t, gtab + (size_t)t * kGEntry);
+  } else if (t < nc + kG2Ent + kG1Ent) {
+    gtab2_entry<P>(t - nc, gtab + kGCombWords + (size_t)(t - nc) * kLLAff);
+  }
 }
 
 // bh_keys_register: keys only (X || Y per record) -> Work.qx / qy / st.
@@ -870,7 +878,7 @@ hipError_t launch_expand(const uint8_t* keys, const uint32_t* key_idx, uint8_t* 
 }
 
 hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s) {
-  const int nt = kCombWindows * kCombEntries;
+  const int nt = kCombWindows * kCombEntries + (int)(kG2Ent + kG1Ent);
   if (curve == 0)
     hipLaunchKernelGGL((k_gtab_build<F30_p256>), dim3((nt + 63) / 64), dim3(64), 0, s,
                        gtab);
@@ -1098,10 +1106,13 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   }
   REC(3);
   const uint32_t tab_blocks = (pl.max_tables + kBuildPerBlock - 1) / kBuildPerBlock;
-  // u1 G of the key-comb list runs inside k_ktab_ladder for the 1-lane comb
-  // (a separate kernel on the aux stream, 146 VGPRs, did not run faster:
-  // profiles/r04/v14)
-  const uint32_t gp_blocks = o.wide <= 1 ? grd.x : 0u;
+  // Lim-Lee comb tables for the one-lane key comb (o.wide == 1)
+  const uint32_t ll = (o.ll_tables && o.wide <= 1) ? 1u : 0u;
+  // u1 G of the key-comb list: folded into k_keycomb's Horner with comb tables
+  // (round 5); with windowed tables (BH_LL=0) inside k_ktab_ladder beside the
+  // builds, stored by list position (a separate kernel on the aux stream, 146
+  // VGPRs, did not run faster: profiles/r04/v14)
+  const uint32_t gp_blocks = (o.wide <= 1 && !ll) ? grd.x : 0u;
   // from here on only plc (rec_slot consumed by the sort)
   if (split) {
     // key tables (no u1), then the u2 Q halves; u1 G after the join
@@ -1138,8 +1149,6 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   }
   // (small secp256k1 batches are BDLS, hence split: the 2-lane GLV ladder)
   if (o.ev_build_wait && (e = hipStreamWaitEvent(s, (hipEvent_t)o.ev_build_wait, 0))) return e;
-  // Lim-Lee comb tables for the one-lane key comb (o.wide == 1)
-  const uint32_t ll = (o.ll_tables && o.wide <= 1) ? 1u : 0u;
   hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x + gp_blocks), blk, 0, s, w, plc,
                      g, gtab, reason, tab_blocks, grd.x, ll);
   if (o.ev_build_done && (e = hipEventRecord((hipEvent_t)o.ev_build_done, s))) return e;

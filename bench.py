@@ -86,7 +86,11 @@ _LL_ENT = 2**(LL_T - 1)
 _LL_CHAIN = 2 * (LL_T - 1)
 FP_KTAB = ((LL_T - 1) * LL_S * 8 + (_LL_CHAIN - 1) + 6 * _LL_CHAIN + (LL_T - 1) * 11
            + (_LL_ENT - 1) * 12 + _LL_ENT * 6 + 2 * FP_INV_SG) if LL_TABLES else 65 * 58
-FP_KEYCOMB = ((LL_S - 1) * (8 + 11) if LL_TABLES else 65 * 16) + 23
+# round 5: with comb tables u1 G is folded into k_keycomb's Horner (verify.h
+# q_llcomb_g): 19 mixed additions from the two-column G table (18 column pairs
+# + column 0) and the x check (~7 ops), no stored u1 G half and no final A + B
+FOLD_G_ADDS = (LL_S - 1) // 2 + 1
+FP_KEYCOMB = ((LL_S - 1) * (8 + 11) + FOLD_G_ADDS * 11 + 7) if LL_TABLES else 65 * 16 + 23
 MACS_PER_VERIFY = FP_LADDER * MAC_PER_FP
 KERNELS = {"build_ladder_ms": "k_ktab_ladder", "keycomb_ms": "k_keycomb"}
 MAX_LANES = 4  # bdls_hip.cpp kMaxLanes
@@ -106,7 +110,7 @@ def kernel_fp_ops(stage: str, routes: dict) -> float:
     """Algorithmic F_p ops of one launch of the stage's kernel."""
     if stage == "build_ladder_ms":
         return (routes["ladder"] * FP_LADDER + routes["key_tables"] * FP_KTAB
-                + routes["keycomb"] * FP_GPART)
+                + (0 if LL_TABLES else routes["keycomb"] * FP_GPART))
     return routes["keycomb"] * FP_KEYCOMB
 
 
@@ -866,10 +870,12 @@ def bench_throughput(a, rank, world, local):
             "unit": "TMAC/s (u32 x u32 -> u64)",
             "frac": achieved / peak if peak else None,
             "work_per_launch": (f"{routes['ladder']} ladder verifies x {FP_LADDER} + "
-                                f"{routes['key_tables']} key tables x {FP_KTAB} + "
-                                f"{routes['keycomb']} u1 G halves x {FP_GPART}"
+                                f"{routes['key_tables']} key tables x {FP_KTAB}"
+                                + ("" if LL_TABLES else
+                                   f" + {routes['keycomb']} u1 G halves x {FP_GPART}")
                                 if dom == "build_ladder_ms" else
-                                f"{routes['keycomb']} key-table verifies x {FP_KEYCOMB}")
+                                f"{routes['keycomb']} key-table verifies x {FP_KEYCOMB}"
+                                + (" (u2 Q comb + folded u1 G)" if LL_TABLES else ""))
                                + f" F_p mul/sqr x {MAC_PER_FP} u32 MACs (SURVEY 8(d) units)",
             "fp_ops_per_launch": fp_ops,
             "launch_ms": round(dom_avg_s * 1e3, 4),

@@ -142,3 +142,137 @@ def records_for_u2(curve, u2s, seed: int = 77, d: int | None = None, low_s: bool
         for dg in (e.to_bytes(32, "big"), (e ^ 1).to_bytes(32, "big")):
             recs.append((qx, qy, O.marshal_ecdsa_signature(r, s), dg))
     return recs
+
+
+# ---- u1 G folded into the key comb's Horner (round 5, verify.h q_llcomb_g) ----
+def comb_columns(u: int, n: int, t: int, s: int) -> list[int]:
+    """The signed comb's column values V_j (u = sum 2^j V_j mod n)."""
+    k = u if u & 1 else u + n
+    c = (k >> 1) | (1 << (t * s - 1))
+    return [sum((2 * ((c >> (s * i + j)) & 1) - 1) << (s * i) for i in range(t)) for j in range(s)]
+
+
+def fold_events(u1: int, u2: int, d: int, n: int, t: int, s: int):
+    """The folded Horner (q_llcomb_g) on u1 G + u2 Q with Q = d G, as integers
+    mod n (multiples of G), in the kernel's order: load the top column of u2;
+    per column j = s-2 .. 0 a doubling, the u2 column (kind "Q"), then at odd
+    j the u1 pair (j+1, j) and at j = 0 the u1 column 0 (kind "G").
+    Returns ([(event, column, kind)], total is infinity)."""
+    V, W = comb_columns(u2, n, t, s), comb_columns(u1, n, t, s)
+    ev, a, inf = [], V[s - 1] * d % n, False
+    for j in range(s - 2, -1, -1):
+        if not inf:
+            a = 2 * a % n
+        adds = [("Q", V[j] * d % n)]
+        if j & 1:
+            adds.append(("G", (2 * W[j + 1] + W[j]) % n))
+        if j == 0:
+            adds.append(("G", W[0] % n))
+        for kind, T in adds:
+            if inf:
+                a, inf = T, False
+                ev.append(("from_inf", j, kind))
+            elif (a - T) % n == 0:
+                ev.append(("dbl", j, kind))
+                a = 2 * T % n
+            elif (a + T) % n == 0:
+                ev.append(("inf", j, kind))
+                a, inf = 0, True
+            else:
+                a = (a + T) % n
+    assert (inf and (u1 + u2 * d) % n == 0) or (not inf and a == (u1 + u2 * d) % n)
+    return ev, inf
+
+
+def fold_crafted(curve, t: int, s: int, seed: int = 17, tries: int = 20000,
+                 low_s: bool = False):
+    """(u1, u2, d) triples whose folded Horner takes each degenerate branch
+    reachable by construction -- the last columns, where the remaining sum can
+    be solved for: u1's column-0 entry doubling / cancelling the sum (the
+    single-column table), u2's column-0 entry doubling / cancelling it, the
+    column-1 pair entry doubling / cancelling it, and u2's column-1 entry
+    cancelling it (the pair then taken from infinity). u1 is drawn, u2 is
+    solved from the wanted total u1 + u2 d, and kept when its own column
+    pattern matches the one the total assumed (~1/2^t). low_s: a finite
+    R = u1 G + u2 Q must give s = x(R) / u2 <= n / 2 (Fabric's rule), else the
+    draw is discarded."""
+    import random
+    n = curve.n
+    rng = random.Random(seed)
+    want = {("dbl", 0, "G"), ("inf", 0, "G"), ("dbl", 0, "Q"), ("inf", 0, "Q"),
+            ("dbl", 1, "G"), ("inf", 1, "G"), ("inf", 1, "Q")}
+    found, out = set(), []
+    for _ in range(tries):
+        if found == want:
+            break
+        d = rng.randrange(1, n)
+        u1 = rng.randrange(1, n)
+        W = comb_columns(u1, n, t, s)
+        p = [rng.choice((-1, 1)) for _ in range(t)]
+        v0 = sum(x << (s * i) for i, x in enumerate(p))
+        pair1 = 2 * W[2] + W[1]
+        targets = {  # event -> the total u1 + u2 d it needs (v0 = u2's assumed column 0)
+            ("dbl", 0, "G"): 2 * W[0],
+            ("inf", 0, "G"): 0,
+            ("dbl", 0, "Q"): 2 * v0 * d + W[0],
+            ("inf", 0, "Q"): W[0],
+            ("dbl", 1, "G"): 4 * pair1 + v0 * d + W[0],
+            ("inf", 1, "G"): v0 * d + W[0],
+            ("inf", 1, "Q"): 2 * pair1 + v0 * d + W[0],
+        }
+        for key, total in targets.items():
+            if key in found:
+                continue
+            u2 = (total - u1) * pow(d, -1, n) % n
+            if not u2:
+                continue
+            ev, inf = fold_events(u1, u2, d, n, t, s)
+            if key not in [e for e in ev if e[0] != "from_inf"][:1]:
+                continue
+            if low_s and not inf:
+                q = O.scalar_mult(curve, d, (curve.gx, curve.gy))
+                r = O.double_scalar(curve, u1, u2, q)[0] % n
+                if r == 0 or r * pow(u2, -1, n) % n > n // 2:
+                    continue
+            found.add(key)
+            out.append((u1, u2, d, key, inf))
+    return out
+
+
+def records_for_fold(curve, triples, seed: int = 23, low_s: bool = True):
+    """Per (u1, u2, d): records whose verify computes exactly these u1, u2
+    with Q = d G -- [(qx, qy, der_sig, digest, expected reason)]. A finite
+    R = u1 G + u2 Q gives the valid signature (r = x(R) mod n, s = r / u2,
+    e = u1 s) and its flipped-digest twin (R_MATH); R at infinity gives one
+    record with any r (it must fail, R_MATH). With low_s, a high s is
+    answered by scaling: (u1, u2) -> (c u1, c u2) changes the events, so such
+    triples are dropped instead."""
+    import random
+    n = curve.n
+    rng = random.Random(seed)
+    out = []
+    for u1, u2, d, _key, inf in triples:
+        qx, qy = O.scalar_mult(curve, d, (curve.gx, curve.gy))
+        if inf:
+            for _ in range(64):
+                r = rng.randrange(1, n)
+                s_ = r * pow(u2, -1, n) % n
+                if not low_s or s_ <= n // 2:
+                    break
+            else:
+                continue
+            e = u1 * s_ % n
+            out.append((qx, qy, O.marshal_ecdsa_signature(r, s_), e.to_bytes(32, "big"), 9))
+            continue
+        R = O.double_scalar(curve, u1, u2, (qx, qy))
+        r = R[0] % n
+        if r == 0:
+            continue
+        s_ = r * pow(u2, -1, n) % n
+        if low_s and s_ > n // 2:
+            continue
+        e = u1 * s_ % n
+        sig = O.marshal_ecdsa_signature(r, s_)
+        out.append((qx, qy, sig, e.to_bytes(32, "big"), 0))
+        out.append((qx, qy, sig, (e ^ 1).to_bytes(32, "big"), 9))
+    return out

@@ -18,10 +18,12 @@ static std::vector<uint32_t> g_gtab, g_gtab_k1;
 template <class P>
 static const uint32_t* gtab_for() {
   std::vector<uint32_t>& g = P::sparse_p256 ? g_gtab : g_gtab_k1;
-  if (g.empty()) {
-    g.assign((size_t)kCombWindows * kCombEntries * kGEntry, 0);
+  if (g.empty()) {  // the device buffer's layout: 13-bit comb, then the folded tables
+    g.assign(kGTabAllWords, 0);
     for (uint32_t t = 0; t < (uint32_t)(kCombWindows * kCombEntries); t++)
       gtab_entry<P>(t, g.data() + (size_t)t * kGEntry);
+    for (uint32_t t = 0; t < kG2Ent + kG1Ent; t++)
+      gtab2_entry<P>(t, g.data() + kGCombWords + (size_t)t * kLLAff);
   }
   return g.data();
 }
@@ -70,22 +72,25 @@ static bool keycomb_any(const Work& w, const uint32_t* gtab, uint32_t i, const u
     case 16: return wide_keycomb<P, 16>(w, gtab, i, tab);
     case 32: return wide_keycomb<P, 32>(w, gtab, i, tab);  // k_small's group
     case 0: return stage_keycomb<P>(w, gtab, i, tab);
-    default:  // the device's split: u1 G stored by list position, then the table half
-      stage_gpart<P>(w, gtab, i, i);
-      if (!g_ll) return stage_keycomb_q<P>(w, i, i, tab, false);
-      // k_keycomb's three ways to read a comb table, taken in turn: 16-byte
-      // loads of the per-batch table (stride 0), the workgroup's packed LDS
-      // copy (kLLLds words per entry), and the per-batch table through the same
-      // 8-byte loads (a run past the LDS slots)
+    default:
+      if (!g_ll) {  // windowed tables: u1 G stored by list position, then the table half
+        stage_gpart<P>(w, gtab, i, i);
+        return stage_keycomb_q<P>(w, i, i, tab, false);
+      }
+      // comb tables: u1 G folded into the Horner (k_keycomb). Its three ways
+      // to read a comb table, taken in turn: 16-byte loads of the per-batch
+      // table (stride 0), the workgroup's packed LDS copy (kLLLds words per
+      // entry), and the per-batch table through the same 8-byte loads (a run
+      // past the LDS slots)
       switch (i % 3) {
-        case 0: return stage_keycomb_q<P>(w, i, i, tab, true, 0);
+        case 0: return stage_keycomb_fold<P>(w, i, tab, 0, g2_of(gtab));
         case 1: {
           std::vector<uint32_t> lds((size_t)kLLEnt * kLLLds);
           for (uint32_t e = 0; e < kLLEnt; e++)
             for (uint32_t k = 0; k < kLLLds; k++) lds[e * kLLLds + k] = tab[e * kLLAff + k];
-          return stage_keycomb_q<P>(w, i, i, lds.data(), true, kLLLds);
+          return stage_keycomb_fold<P>(w, i, lds.data(), kLLLds, g2_of(gtab));
         }
-        default: return stage_keycomb_q<P>(w, i, i, tab, true, kLLAff);
+        default: return stage_keycomb_fold<P>(w, i, tab, kLLAff, g2_of(gtab));
       }
   }
 }

@@ -29,7 +29,8 @@ import pytest
 from bdls_amd import _lib, workload
 from oracle import ecdsa_ref as O
 from oracle import orc
-from tests.comb_cases import g_comb_u1, records_for_u2, signed_comb_u2, unsigned_comb_u2
+from tests.comb_cases import (fold_crafted, g_comb_u1, records_for_fold, records_for_u2,
+                              signed_comb_u2, unsigned_comb_u2)
 
 pytestmark = pytest.mark.gpu
 
@@ -103,6 +104,14 @@ def p256_edge_batch(golden):
             recs.append((qx.to_bytes(32, "big") + qy.to_bytes(32, "big"), sig, dg))
     for k in range(len(crafted)):  # valid signature, then its flipped-digest twin
         want += [0 if k % 2 == 0 else 9] * 4
+    # round 5: the folded u1 G (k_keycomb's q_llcomb_g) on records whose joint
+    # Horner takes each degenerate branch (tests/comb_cases.py fold_crafted)
+    fold = records_for_fold(c, fold_crafted(c, 7, 37, seed=33, low_s=True), low_s=True)
+    assert len(fold) >= 13
+    for qx, qy, sig, dg, exp in fold:
+        for _ in range(4):
+            recs.append((qx.to_bytes(32, "big") + qy.to_bytes(32, "big"), sig, dg))
+            want.append(exp)
     fill = 40_960 - len(recs)
     w = workload.generate(fill, fill // 64, 64, 16, seed=47)  # ~64 uses per key
     for i in range(w.n):

@@ -311,3 +311,54 @@ def test_hostsim_g_comb_crafted_u1(hs, ll):
     assert ncomb.value > 0
     assert [int(o) for o in out[0::2]] == [0] * (len(recs) // 2)
     assert all(int(o) == 9 for o in out[1::2])
+
+
+@pytest.mark.parametrize("curve", ["P256", "SECP256K1"])
+def test_hostsim_folded_g_crafted_events(hs, curve):
+    """Round 5: u1 G folded into the key comb's Horner (verify.h q_llcomb_g).
+    Records crafted (tests/comb_cases.py fold_crafted) so that the joint
+    Horner takes every degenerate branch reachable by construction: the u1
+    single-column entry and the column-1 pair entry doubling / cancelling the
+    running sum, u2's column-0 entry doubling / cancelling it, u2's column-1
+    entry cancelling it (the pair entry then taken from infinity), and a total
+    at infinity. Through the one-lane comb route with every record on a key
+    table: the verdicts equal the construction (valid 0, twins / infinity 9)."""
+    from oracle import ecdsa_ref as O
+    from tests.comb_cases import fold_crafted, fold_events, records_for_fold
+    c = getattr(O, curve)
+    sh = hs.hs_ll_shape()
+    t, s = sh >> 8, sh & 0xFF
+    triples = fold_crafted(c, t, s, seed=31)
+    kinds = {x[3] for x in triples}
+    assert {("dbl", 0, "G"), ("inf", 0, "G"), ("dbl", 1, "G"), ("inf", 1, "G"),
+            ("dbl", 0, "Q"), ("inf", 0, "Q"), ("inf", 1, "Q")} <= kinds
+    for u1, u2, d, key, _ in triples:
+        assert key in fold_events(u1, u2, d, c.n, t, s)[0]
+    recs = records_for_fold(c, triples, low_s=False)
+    pub = np.frombuffer(b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big")
+                                 for x, y, _, _, _ in recs), np.uint8)
+    sigs, dgs = [r[2] for r in recs], [r[3] for r in recs]
+    sl = np.array([len(x) for x in sigs], np.uint32)
+    dl = np.array([len(x) for x in dgs], np.uint32)
+    so = np.concatenate([[0], np.cumsum(sl[:-1])]).astype(np.uint64)
+    do = np.concatenate([[0], np.cumsum(dl[:-1])]).astype(np.uint64)
+    sig = np.frombuffer(b"".join(sigs), np.uint8)
+    dg = np.frombuffer(b"".join(dgs), np.uint8)
+    out = np.zeros(len(recs), np.uint8)
+    ncomb = ctypes.c_uint32()
+    hs.hs_set_ll(1)
+    try:
+        if curve == "P256":
+            hs.hs_verify2(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
+                          dg.ctypes.data, do.ctypes.data, dl.ctypes.data, len(recs), 2, 4, 1,
+                          out.ctypes.data, ctypes.byref(ncomb))
+            assert ncomb.value == len(recs)
+        else:
+            hs.hs_verify_k1_digest.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_uint32] * 2 + [
+                ctypes.c_void_p]
+            hs.hs_verify_k1_digest(pub.ctypes.data, sig.ctypes.data, so.ctypes.data,
+                                   sl.ctypes.data, dg.ctypes.data, do.ctypes.data,
+                                   dl.ctypes.data, len(recs), 1, out.ctypes.data)
+    finally:
+        hs.hs_set_ll(0)
+    assert [int(o) for o in out] == [r[4] for r in recs]
