@@ -1125,19 +1125,25 @@ BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint3
 // and no empty columns -- at t = 7 (s = 37) 36 + 36 instead of the unsigned
 // 6 x 43 comb's 42 + 43 with a zero-column select, for a table of the same 64
 // entries.
-// Build, one lane per table (one build wave per SIMD beside the u1 G waves):
-// (t - 1) s doublings give D_i = 2 B_i and B_(i+1) = 2^(s-1) D_i; those
-// 2 (t - 1) points are made affine with one inversion (Montgomery's trick);
-// E[0] = B_(t-1) - sum_(i < t-1) B_i (t - 1 mixed additions); a Gray-code walk
-// reaches every other E[g] by one mixed addition of +-D_i (flipping digit i
-// from -1 to +1 adds 2 B_i), storing raw Jacobian entries and the running
-// product of their Z; one more inversion and a backward pass make them affine.
-// No build step can degenerate: every scalar involved lies in (0, n / 2) and
-// the walk's partial sums e_m = 2^(s(t-1)) +- ... exceed every d_i = 2^(s i+1)
-// with e_m + d_i < n. The Horner additions keep explicit degenerate handling
-// (A = +-V_j only for crafted scalars), as a branch the lanes skip together.
-// Registry tables and small batches keep the windowed tables (their lanes
-// split the windows; a comb's doubling chain cannot be split).
+// Build, one lane per table (round 5): (t - 1) s doublings give D_i = 2 B_i and
+// B_(i+1) = 2^(s-1) D_i; those 2 (t - 1) chain points are made affine with one
+// inversion (Montgomery's trick). The 2^(t-1) entries are then SUMS of two
+// small affine tables over a split of the lower t - 1 digits into a low group
+// (a digits) and a high group (the other t - 1 - a, plus the top tooth):
+//   E[m] = H[m >> a] + L[m & (2^a - 1)],
+//   L[x] = sum_(i < a) (2 x_i - 1) B_i,
+//   H[y] = B_(t-1) + sum_(a <= i < t-1) (2 y_(i-a) - 1) B_i.
+// L and H (2^a + 2^(t-1-a) points) come from two Gray-code walks of mixed
+// additions of +-D_i (flipping digit i from -1 to +1 adds 2 B_i), made affine
+// with a second inversion; each entry is one affine addition H + L whose
+// denominators x_H - x_L are inverted together (a third inversion): 6 F_p ops
+// per entry instead of the full Gray walk over all entries (11 + 1) and its
+// backward affine pass (6), and no raw Jacobian entry written and read back.
+// No build step can degenerate: every scalar involved lies in (0, n / 2), the
+// walks' partial sums exceed every d_i they add with e + d < n, and H's scalar
+// (~2^(s (t-1))) never equals +-L's (< 2^(s a + 1)). The Horner additions keep
+// explicit degenerate handling (A = +-V_j only for crafted scalars), as a
+// branch the lanes skip together.
 #ifndef BH_LL_T
 #define BH_LL_T 7  // teeth: 7 x 37 bits, 64 entries (signed)
 #endif
@@ -1145,12 +1151,23 @@ constexpr int kLLTeeth = BH_LL_T, kLLSpace = (257 + kLLTeeth - 1) / kLLTeeth;
 constexpr int kLLTS = kLLTeeth * kLLSpace;        // >= 257: c < 2^(t s)
 constexpr uint32_t kLLEnt = 1u << (kLLTeeth - 1);  // entries E[0 .. 2^(t-1))
 constexpr uint32_t kLLAff = 20;                    // words per affine point
-constexpr uint32_t kLLAux = kLLEnt;                // affine B_0..B_(t-1), D_0..D_(t-2)
-constexpr uint32_t kLLChain = 2u * (kLLTeeth - 1); // Jacobian D_i / B_(i+1) of the chain
-constexpr uint32_t kLLRaw = ((kLLAux + 2u * kLLTeeth - 1u) * kLLAff + 3u) & ~3u;
-constexpr uint32_t kLLPre = kLLRaw + 28u * (kLLEnt + kLLChain);  // running Z products
-static_assert(kLLTS >= 257 && kLLTS <= 288 && kLLSpace < 64 && kLLTeeth >= 2 &&
-                  kLLPre + 12u * kLLEnt <= kKTabWords && kLLChain <= kLLEnt,
+// the build's split: L over the a low digits, H over the others + the top tooth
+constexpr int kLLA = (kLLTeeth - 1) / 2;
+constexpr uint32_t kLLNL = 1u << kLLA, kLLNH = 1u << (kLLTeeth - 1 - kLLA);
+constexpr uint32_t kLLWalk = kLLNL + kLLNH;         // L and H points (two walks)
+constexpr uint32_t kLLChain = 2u * (kLLTeeth - 1);  // Jacobian D_i / B_(i+1) of the chain
+// Table region (words): entries [0, kLLEnt) x kLLAff (all the comb reads), then
+// build scratch: affine B_0..B_(t-1), D_0..D_(t-2) (aux), affine L and H, raw
+// Jacobian points (the chain's, then the walks'), running Z / denominator
+// products (12 words each).
+constexpr uint32_t kLLAux = kLLEnt;
+constexpr uint32_t kLLLH = kLLAux + 2u * kLLTeeth - 1u;
+constexpr uint32_t kLLRaw = ((kLLLH + kLLWalk) * kLLAff + 3u) & ~3u;
+constexpr uint32_t kLLRawN = kLLChain > kLLWalk ? kLLChain : kLLWalk;
+constexpr uint32_t kLLPre = kLLRaw + 28u * kLLRawN;
+static_assert(kLLTS >= 257 && kLLTS <= 288 && kLLSpace < 64 && kLLTeeth >= 3 &&
+                  kLLPre + 12u * kLLEnt <= kKTabWords && kLLChain <= kLLEnt &&
+                  kLLWalk <= kLLEnt,
               "comb table layout");
 
 BH_HD void llraw_store(uint32_t* tab, uint32_t b, const J30& P) { ktab_store(tab + kLLRaw, 0, b, P); }
@@ -1240,6 +1257,80 @@ BH_HD void ll_to_affine(uint32_t x[9], uint32_t y[9], const J30& E, const uint32
 // Walk position m (0..2^(t-1) - 1) -> entry gray(m); step m flips digit ctz(m).
 BH_HD uint32_t ll_gray(uint32_t m) { return m ^ (m >> 1); }
 
+// One Gray-code walk of the build (L or H): the 2^nd points
+//   P[g] = top + sum_(k < nd) (2 g_k - 1) B_(i0 + k)   (top = B_(t-1) for H, none for L),
+// as raw Jacobian points at raw slots [r0, r0 + 2^nd) in walk order with the
+// running product z of their Z (the whole build's walks share one product
+// chain: pre slot r0 + m holds z after point m). Start: top - sum B_(i0 + k)
+// (mixed additions of -B, never degenerate); step m flips digit ctz(m) of
+// gray(m), adding +-D_(i0 + ctz(m)).
+template <class P>
+BH_HD void ll_walk(uint32_t* tab, uint32_t i0, int nd, bool top, uint32_t r0, uint32_t z[9],
+                   const uint32_t one[9]) {
+  J30 A;
+  bool same;
+  int k = nd - 1;
+  if (top) {
+    llaff_load(A.X, A.Y, tab, kLLAux + kLLTeeth - 1u);  // B_(t-1)
+  } else {  // -B_(i0 + nd - 1)
+    llaff_load(A.X, A.Y, tab, kLLAux + i0 + (uint32_t)k);
+    f_neg<P, 64>(A.Y, A.Y);
+    k--;
+  }
+  f_copy(A.Z, one);
+#pragma unroll 1
+  for (; k >= 0; k--) {
+    uint32_t bx[9], by[9];
+    llaff_load(bx, by, tab, kLLAux + i0 + (uint32_t)k);
+    f_neg<P, 64>(by, by);
+    (void)j_madd<P>(A, A, bx, by, &same);  // never degenerate (see above)
+  }
+  llraw_store(tab, r0, A);
+  if (r0 == 0) f_copy(z, A.Z);
+  else f_mul<P>(z, z, A.Z);
+  llpre_store(tab, r0, z);
+  const uint32_t npts = 1u << nd;
+  uint32_t nx[9], ny[9];
+  llaff_load(nx, ny, tab, kLLAux + kLLTeeth + i0);  // D_i0 for m = 1
+#pragma unroll 1
+  for (uint32_t m = 1; m < npts; m++) {
+    uint32_t dx[9], dy[9];
+    f_copy(dx, nx);
+    f_copy(dy, ny);
+    if (m + 1u < npts)
+      llaff_load(nx, ny, tab, kLLAux + kLLTeeth + i0 + (uint32_t)__builtin_ctz(m + 1u));
+    const uint32_t g = ll_gray(m);
+    if (!((g >> __builtin_ctz(m)) & 1u)) f_neg<P, 64>(dy, dy);  // digit back to -1
+    (void)j_madd<P>(A, A, dx, dy, &same);                        // never degenerate
+    llraw_store(tab, r0 + m, A);
+    f_mul<P>(z, z, A.Z);
+    llpre_store(tab, r0 + m, z);
+  }
+}
+
+// Montgomery's trick backwards over raw slots [0, cnt) with pre[k] = prod of
+// the Z of slots 0..k: each raw point made affine into the affine slot
+// dst(k). inv = (pre[cnt - 1])^-1 on entry.
+template <class P, class Dst>
+BH_HD void ll_affine_back(uint32_t* tab, uint32_t cnt, uint32_t inv[9], Dst dst) {
+#pragma unroll 1
+  for (uint32_t c = cnt; c-- > 0;) {
+    J30 E;
+    llraw_load(E, tab, c);
+    uint32_t zi[9], x[9], y[9];
+    if (c > 0) {
+      uint32_t pre[9];
+      llpre_load(pre, tab, c - 1u);
+      f_mul<P>(zi, inv, pre);
+      f_mul<P>(inv, inv, E.Z);
+    } else {
+      f_copy(zi, inv);
+    }
+    ll_to_affine<P>(x, y, E, zi);
+    llaff_store(tab, dst(c), x, y);
+  }
+}
+
 template <class P>
 BH_HD void lltab_build(uint32_t* tab, const Work& w, uint32_t rec) {
   uint32_t one[9];
@@ -1256,98 +1347,71 @@ BH_HD void lltab_build(uint32_t* tab, const Work& w, uint32_t rec) {
 #pragma unroll 1
   for (uint32_t i = 0; i + 1 < (uint32_t)kLLTeeth; i++) {
     j_dbl<P>(B, B);
-    llraw_store(tab, kLLEnt + 2u * i, B);
+    llraw_store(tab, 2u * i, B);
     if (i == 0) f_copy(z, B.Z);
     else f_mul<P>(z, z, B.Z);
     llpre_store(tab, 2u * i, z);
 #pragma unroll 1
     for (int d = 1; d < kLLSpace; d++) j_dbl<P>(B, B);
-    llraw_store(tab, kLLEnt + 2u * i + 1u, B);
+    llraw_store(tab, 2u * i + 1u, B);
     f_mul<P>(z, z, B.Z);
     llpre_store(tab, 2u * i + 1u, z);
   }
   uint32_t inv[9];
   f_inv_sg<P>(inv, z);
-#pragma unroll 1
-  for (uint32_t c = kLLChain; c-- > 0;) {
-    J30 E;
-    llraw_load(E, tab, kLLEnt + c);
-    uint32_t zi[9], x[9], y[9];
-    if (c > 0) {
-      uint32_t pre[9];
-      llpre_load(pre, tab, c - 1u);
-      f_mul<P>(zi, inv, pre);
-      f_mul<P>(inv, inv, E.Z);
-    } else {
-      f_copy(zi, inv);
-    }
-    ll_to_affine<P>(x, y, E, zi);
-    // D_i -> aux slot t + i; B_(i+1) -> aux slot i + 1
-    llaff_store(tab, (c & 1u) ? kLLAux + (c >> 1) + 1u : kLLAux + kLLTeeth + (c >> 1), x, y);
-  }
-  // 2. E[0] = B_(t-1) - B_0 - ... - B_(t-2), then the Gray walk: step m adds
-  //    +-D_i (i = ctz(m); + when digit i of gray(m) is set). Raw entries at
-  //    their final index; pre[m] = prod of the Z of entries 0..m. The next
-  //    step's point is loaded one step ahead, off the dependency chain.
-  J30 A;
-  llaff_load(A.X, A.Y, tab, kLLAux + kLLTeeth - 1u);
-  f_copy(A.Z, one);
-  bool same;
-#pragma unroll 1
-  for (uint32_t i = 0; i + 1 < (uint32_t)kLLTeeth; i++) {
-    uint32_t bx[9], by[9];
-    llaff_load(bx, by, tab, kLLAux + i);
-    f_neg<P, 64>(by, by);
-    (void)j_madd<P>(A, A, bx, by, &same);  // never degenerate (see above)
-  }
-  llraw_store(tab, 0, A);
-  f_copy(z, A.Z);
-  llpre_store(tab, 0, z);
-  uint32_t nx[9], ny[9];
-  llaff_load(nx, ny, tab, kLLAux + kLLTeeth);  // D_0 for m = 1
-#pragma unroll 1
-  for (uint32_t m = 1; m < kLLEnt; m++) {
-    uint32_t dx[9], dy[9];
-    f_copy(dx, nx);
-    f_copy(dy, ny);
-    if (m + 1u < kLLEnt) llaff_load(nx, ny, tab, kLLAux + kLLTeeth + __builtin_ctz(m + 1u));
-    const uint32_t g = ll_gray(m);
-    if (!((g >> __builtin_ctz(m)) & 1u)) f_neg<P, 64>(dy, dy);  // digit back to -1
-    (void)j_madd<P>(A, A, dx, dy, &same);                        // never degenerate
-    llraw_store(tab, g, A);
-    f_mul<P>(z, z, A.Z);
-    llpre_store(tab, m, z);
-  }
-  // 3. Montgomery's trick backwards over m = 2^(t-1) - 1 .. 0: inv = (prod Z)^-1;
-  //    Z_m^-1 = inv pre[m - 1], inv *= Z_m. The next entry and prefix are
-  //    loaded one step ahead.
+  // D_i -> aux slot t + i; B_(i+1) -> aux slot i + 1
+  ll_affine_back<P>(tab, kLLChain, inv, [](uint32_t c) {
+    return (c & 1u) ? kLLAux + (c >> 1) + 1u : kLLAux + kLLTeeth + (c >> 1);
+  });
+  // 2. L (digits 0 .. a-1) and H (digits a .. t-2 + the top tooth) by two
+  //    Gray walks into raw slots [0, NL) and [NL, NL + NH), one product chain,
+  //    made affine with one inversion into L / H slots (by Gray index).
+  ll_walk<P>(tab, 0u, kLLA, false, 0u, z, one);
+  ll_walk<P>(tab, (uint32_t)kLLA, kLLTeeth - 1 - kLLA, true, kLLNL, z, one);
   f_inv_sg<P>(inv, z);
-  J30 E;
-  uint32_t pre[9];
-  llraw_load(E, tab, ll_gray(kLLEnt - 1u));
-  llpre_load(pre, tab, kLLEnt - 2u);
+  ll_affine_back<P>(tab, kLLWalk, inv, [](uint32_t c) {
+    return kLLLH + (c < kLLNL ? ll_gray(c) : kLLNL + ll_gray(c - kLLNL));
+  });
+  // 3. E[m] = H[m >> a] + L[m & (NL - 1)]: affine additions, the denominators
+  //    x_H - x_L inverted together. Forward: their running products (pre);
+  //    backward: lambda = (y_H - y_L) / (x_H - x_L), x = lambda^2 - x_H - x_L,
+  //    y = lambda (x_L - x) - y_L (beta 34 each: the comb's mixed additions
+  //    take beta <= 64).
+  uint32_t hx[9], hy[9], lx[9], ly[9], d[9];
 #pragma unroll 1
-  for (uint32_t m = kLLEnt - 1u;; m--) {
-    J30 En;
-    uint32_t pn[9];
-    if (m >= 2u) {
-      llraw_load(En, tab, ll_gray(m - 1u));
-      llpre_load(pn, tab, m - 2u);
-    } else if (m == 1u) {
-      llraw_load(En, tab, 0);
-    }
-    uint32_t zi[9], x[9], y[9];
+  for (uint32_t m = 0; m < kLLEnt; m++) {
+    if ((m & (kLLNL - 1u)) == 0u) llaff_load(hx, hy, tab, kLLLH + kLLNL + (m >> kLLA));
+    llaff_load(lx, ly, tab, kLLLH + (m & (kLLNL - 1u)));
+    f_sub<P, 32>(d, hx, lx);                 // [b34], nonzero (H != +-L)
+    if (m == 0) f_copy(z, d);
+    else f_mul<P>(z, z, d);
+    if (m + 1u < kLLEnt) llpre_store(tab, m, z);
+  }
+  f_inv_sg<P>(inv, z);
+#pragma unroll 1
+  for (uint32_t m = kLLEnt; m-- > 0;) {
+    if (m == kLLEnt - 1u || (m & (kLLNL - 1u)) == kLLNL - 1u)
+      llaff_load(hx, hy, tab, kLLLH + kLLNL + (m >> kLLA));
+    llaff_load(lx, ly, tab, kLLLH + (m & (kLLNL - 1u)));
+    f_sub<P, 32>(d, hx, lx);
+    uint32_t di[9], lam[9], t[9], x[9], y[9];
     if (m > 0u) {
-      f_mul<P>(zi, inv, pre);   // Z_m^-1
-      f_mul<P>(inv, inv, E.Z);  // (prod_(< m))^-1
+      uint32_t pre[9];
+      llpre_load(pre, tab, m - 1u);
+      f_mul<P>(di, inv, pre);                // (x_H - x_L)^-1
+      f_mul<P>(inv, inv, d);
     } else {
-      f_copy(zi, inv);
+      f_copy(di, inv);
     }
-    ll_to_affine<P>(x, y, E, zi);
-    llaff_store(tab, ll_gray(m), x, y);
-    if (m == 0u) break;
-    j_copy(E, En);
-    if (m >= 2u) f_copy(pre, pn);
+    f_sub<P, 32>(t, hy, ly);                 // [b34]
+    f_mul<P>(lam, t, di);                    // [b2]
+    f_sqr<P>(x, lam);                        // [b2]
+    f_add(t, hx, lx);                        // [b4]
+    f_sub<P, 32>(x, x, t);                   // [b34]
+    f_sub<P, 64>(t, lx, x);                  // [b66]
+    f_mul<P>(y, lam, t);                     // [b2]
+    f_sub<P, 32>(y, y, ly);                  // [b34]
+    llaff_store(tab, m, x, y);
   }
 }
 

@@ -65,11 +65,14 @@ def phase(msg: str) -> None:
 # stored u1 G and checks x (~23 ops). Per-batch tables of large batches are
 # signed Lim-Lee combs (round 4, verify.h lltab_build; BH_LL=0: 4-bit windows)
 # with LL_T teeth spaced LL_S bits (BH_LL_T, 7 x 37), 2^(LL_T-1) entries:
-#   build: (LL_T-1) LL_S doublings (8 ops); the 2 (LL_T-1) chain points made
-#     affine (2 (LL_T-1) - 1 prefix products + 6 per point); E[0] by LL_T-1
-#     mixed additions (11); the Gray walk's 2^(LL_T-1) - 1 mixed additions plus
-#     one running Z product (12); the backward pass (6 per entry); two safegcd
-#     inversions (~14k VALU instructions each, ~85 F_p-op equivalents)
+#   build (round 5, verify.h lltab_build): (LL_T-1) LL_S doublings (8 ops);
+#     the 2 (LL_T-1) chain points made affine (prefix products + 6 per point +
+#     an inversion); L over a = (LL_T-1)//2 low digits and H over the rest by
+#     two Gray walks (start: a - 1 and LL_T-1-a mixed additions; 2^a - 1 and
+#     2^(LL_T-1-a) - 1 steps of a mixed addition (11) + a Z product (1)), made
+#     affine (6 per point + an inversion); each entry E = H + L one affine
+#     addition whose denominators share an inversion (6 per entry); three
+#     safegcd inversions (~14k VALU instructions each, ~85 F_p-op equivalents)
 #   comb: LL_S - 1 doublings + LL_S - 1 mixed additions per record (the top
 #     column is loaded, every column is nonzero)
 # windows: build 65 x 58 = 3,770 per table (co-Z chain), comb 65 additions
@@ -79,13 +82,19 @@ G_COMB_BITS = 13
 G_WINDOWS = (257 + G_COMB_BITS - 1) // G_COMB_BITS
 LL_TABLES = os.environ.get("BH_LL", "1") != "0"
 FP_LADDER, FP_GPART = 3200, G_WINDOWS * 11
-LL_T = 7
+LL_T = int(os.environ.get("BH_LL_T", 7))  # the comb shape the library was built with (verify.h)
 LL_S = -(-257 // LL_T)
 FP_INV_SG = 85
 _LL_ENT = 2**(LL_T - 1)
 _LL_CHAIN = 2 * (LL_T - 1)
-FP_KTAB = ((LL_T - 1) * LL_S * 8 + (_LL_CHAIN - 1) + 6 * _LL_CHAIN + (LL_T - 1) * 11
-           + (_LL_ENT - 1) * 12 + _LL_ENT * 6 + 2 * FP_INV_SG) if LL_TABLES else 65 * 58
+_LL_A = (LL_T - 1) // 2
+_LL_NL, _LL_NH = 2**_LL_A, 2**(LL_T - 1 - _LL_A)
+FP_KTAB = ((LL_T - 1) * LL_S * 8                                     # the doubling chain
+           + (_LL_CHAIN - 1) + 6 * _LL_CHAIN + FP_INV_SG             # chain points affine
+           + ((_LL_A - 1) + (LL_T - 1 - _LL_A)) * 11                 # walk starts
+           + (_LL_NL - 1 + _LL_NH - 1) * 12                          # walk steps + Z products
+           + 6 * (_LL_NL + _LL_NH) + FP_INV_SG                       # L, H affine
+           + 6 * _LL_ENT - 1 + FP_INV_SG) if LL_TABLES else 65 * 58  # entries H + L
 # round 5: with comb tables u1 G is folded into k_keycomb's Horner (verify.h
 # q_llcomb_g): 19 mixed additions from the two-column G table (18 column pairs
 # + column 0) and the x check (~7 ops), no stored u1 G half and no final A + B
