@@ -257,6 +257,47 @@ BH_HD bool j_madd(J30& r, const J30& p, const uint32_t x2[9], const uint32_t y2[
   return degenerate;
 }
 
+// j_madd that also returns pz = p rescaled to r's Z: (X1 H^2, Y1 H^3, Z3) --
+// both are intermediates of the addition, so pz is free; it is the co-Z
+// partner j_zaddu needs for the composite 2 p + q = (p + q) + p. Requirements
+// and degenerate contract as j_madd (r may alias p). pz beta (2, 2, 2).
+template <class F>
+BH_HD bool j_madd_co(J30& r, J30& pz, const J30& p, const uint32_t x2[9], const uint32_t y2[9],
+                     bool* same_y) {
+  uint32_t z1z1[9], u2[9], s2[9], h[9], rr[9], t[9], hh[9], hhh[9];
+  f_sqr<F>(z1z1, p.Z);                    // [b2]
+  f_mul<F>(u2, x2, z1z1);                 // [b2]
+  f_mul<F>(t, p.Z, z1z1);                 // [b2]
+  f_mul<F>(s2, y2, t);                    // [b2]
+  f_sub<F, 64>(h, u2, p.X);               // [b66]
+  f_sub<F, 64>(rr, s2, p.Y);              // [b66]
+  f_sqr<F>(hh, h);                        // [b2]
+  f_mul<F>(hhh, hh, h);                   // [b2]
+  f_mul<F>(pz.X, p.X, hh);                // [b2]   V = X1 H^2
+  f_sqr<F>(t, rr);                        // [b2]
+  f_mulc<2>(s2, pz.X);                    // [b4]
+  f_add(s2, s2, hhh);                     // [b6]
+  f_sub<F, 32>(r.X, t, s2);               // [b34]  X3 = r^2 - H^3 - 2V
+  f_mulc<3>(s2, pz.X);                    // [b6]
+  f_add(s2, s2, hhh);                     // [b8]
+  f_sub<F, 32>(s2, s2, t);                // [b40]  V - X3
+  f_mul<F>(s2, rr, s2);                   // [b2]   66*40
+  f_mul<F>(pz.Y, p.Y, hhh);               // [b2]   Y1 H^3
+  f_sub<F, 32>(r.Y, s2, pz.Y);            // [b34]
+  f_mul<F>(r.Z, p.Z, h);                  // [b2]   34*66
+  f_copy(pz.Z, r.Z);
+  const bool degenerate = f_is_zero2<F>(r.Z);
+  if (degenerate) {
+    f_reduce<F>(t, rr);
+    uint32_t z = 0;
+    for (int i = 0; i < 9; i++) z |= t[i];
+    *same_y = (z == 0);
+  } else {
+    *same_y = false;
+  }
+  return degenerate;
+}
+
 // y^2 == x^3 + a x + b for Montgomery-domain x, y with beta <= 2.
 template <class F>
 BH_HD bool j_on_curve(const uint32_t x[9], const uint32_t y[9]) {

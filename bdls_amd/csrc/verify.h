@@ -1644,10 +1644,46 @@ BH_HD void ll_madd(J30& A, bool& a_inf, const uint32_t tx[9], uint32_t ty[9], bo
   }
 }
 
+// A = 2 A + T (T = +-(tx, ty)) as (A + T) + A: a mixed addition that also
+// rescales A onto the sum's Z (j_madd_co), then a co-Z addition (j_zaddu):
+// 8M + 3S + 5M + 2S = 18 F_p ops against a doubling + a mixed addition's 19
+// (round 5). Degenerate cases, as branches the lanes skip together: A at
+// infinity -> T; A == T -> 3 T = 2 T + T; A == -T -> A; A + T == -A (the
+// co-Z sum's x difference is 0; A + T == A would need T = 0) -> infinity.
+template <class P>
+BH_HD void ll_dbladd(J30& A, bool& a_inf, const uint32_t tx[9], uint32_t ty[9], bool neg,
+                     const uint32_t one[9]) {
+  uint32_t nty[9];
+  f_neg<P, 64>(nty, ty);
+  f_sel(ty, neg, nty, ty);
+  if (a_inf) {  // rare: 2 inf + T
+    f_copy(A.X, tx);
+    f_copy(A.Y, ty);
+    f_copy(A.Z, one);
+    a_inf = false;
+    return;
+  }
+  J30 R, Az;
+  bool same;
+  if (j_madd_co<P>(R, Az, A, tx, ty, &same)) {  // rare: A == +-T
+    J30 T;
+    f_copy(T.X, tx);
+    f_copy(T.Y, ty);
+    f_copy(T.Z, one);
+    if (same) {
+      j_dbl<P>(A, T);
+      (void)j_madd<P>(A, A, tx, ty, &same);  // 2 T + T: 2 T != +-T (prime order)
+    }  // else A == -T: 2 A + T = A, unchanged
+    return;
+  }
+  j_zaddu<P>(A, R, Az);
+  if (f_is_zero2<P>(A.Z)) a_inf = true;  // rare: A + T == -A
+}
+
 // u1 G + u2 Q from the key's signed comb table (stride as q_llcomb) and the
-// folded G tables g2: Horner from the top column; at column j a doubling, the
-// key table's column, and at odd j and j = 0 the folded G entry (loaded one
-// step ahead, under the doubling).
+// folded G tables g2: Horner from the top column; at column j A = 2 A + V_j Q
+// (ll_dbladd), and at odd j and j = 0 the folded G entry (loaded one step
+// ahead).
 template <class P>
 BH_HD void q_llcomb_g(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab,
                       uint32_t stride, const uint32_t* g2) {
@@ -1671,25 +1707,19 @@ BH_HD void q_llcomb_g(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint
   llaff_load(gx, gy, g2, gidx);
 #pragma unroll 1
   for (int j = kLLSpace - 2; j >= 0; j--) {
-    j_dbl<P>(A, A);  // (while a_inf, A is a placeholder the next point replaces)
-    const int nadd = ((j & 1) || j == 0) ? 2 : 1;
-#pragma unroll 1
-    for (int a = 0; a < nadd; a++) {
+    {
       uint32_t tx[9], ty[9];
-      if (a == 0) {
-        ll_column(sl, j, idx, neg);
-        if (stride) llent_load(tx, ty, tab + idx * stride);
-        else llaff_load(tx, ty, tab, idx);
-      } else {
-        f_copy(tx, gx);
-        f_copy(ty, gy);
-        neg = gneg;
-      }
-      ll_madd<P>(A, a_inf, tx, ty, neg, one);
+      ll_column(sl, j, idx, neg);
+      if (stride) llent_load(tx, ty, tab + idx * stride);
+      else llaff_load(tx, ty, tab, idx);
+      ll_dbladd<P>(A, a_inf, tx, ty, neg, one);  // A = 2 A + V_j Q
     }
-    if (nadd == 2 && j > 0) {  // the next folded G entry: column j - 2, or column 0
-      g2_column(gl, j >= 3 ? j - 2 : 0, gidx, gneg);
-      llaff_load(gx, gy, g2, gidx);
+    if ((j & 1) || j == 0) {
+      ll_madd<P>(A, a_inf, gx, gy, gneg, one);
+      if (j > 0) {  // the next folded G entry: column j - 2, or column 0
+        g2_column(gl, j >= 3 ? j - 2 : 0, gidx, gneg);
+        llaff_load(gx, gy, g2, gidx);
+      }
     }
   }
 }

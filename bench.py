@@ -99,7 +99,9 @@ FP_KTAB = ((LL_T - 1) * LL_S * 8                                     # the doubl
 # q_llcomb_g): 19 mixed additions from the two-column G table (18 column pairs
 # + column 0) and the x check (~7 ops), no stored u1 G half and no final A + B
 FOLD_G_ADDS = (LL_S - 1) // 2 + 1
-FP_KEYCOMB = ((LL_S - 1) * (8 + 11) + FOLD_G_ADDS * 11 + 7) if LL_TABLES else 65 * 16 + 23
+# Each Horner step A = 2 A + V_j Q is (A + T) + A: a mixed addition that also
+# rescales A (8M + 3S) + a co-Z addition (5M + 2S) = 18 ops (verify.h ll_dbladd)
+FP_KEYCOMB = ((LL_S - 1) * 18 + FOLD_G_ADDS * 11 + 7) if LL_TABLES else 65 * 16 + 23
 MACS_PER_VERIFY = FP_LADDER * MAC_PER_FP
 KERNELS = {"build_ladder_ms": "k_ktab_ladder", "keycomb_ms": "k_keycomb"}
 MAX_LANES = 4  # bdls_hip.cpp kMaxLanes

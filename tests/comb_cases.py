@@ -155,15 +155,30 @@ def comb_columns(u: int, n: int, t: int, s: int) -> list[int]:
 def fold_events(u1: int, u2: int, d: int, n: int, t: int, s: int):
     """The folded Horner (q_llcomb_g) on u1 G + u2 Q with Q = d G, as integers
     mod n (multiples of G), in the kernel's order: load the top column of u2;
-    per column j = s-2 .. 0 a doubling, the u2 column (kind "Q"), then at odd
-    j the u1 pair (j+1, j) and at j = 0 the u1 column 0 (kind "G").
-    Returns ([(event, column, kind)], total is infinity)."""
+    per column j = s-2 .. 0 the composite A = 2 A + V_j Q computed as
+    (A + T) + A (ll_dbladd, kind "Q": A == T -> "dbl", A == -T -> "neg",
+    2 A + T == 0 -> "inf"), then at odd j the u1 pair (j+1, j) and at j = 0
+    the u1 column 0 (a mixed addition, kind "G": A == T -> "dbl", A == -T ->
+    "inf"). Returns ([(event, column, kind)], total is infinity)."""
     V, W = comb_columns(u2, n, t, s), comb_columns(u1, n, t, s)
     ev, a, inf = [], V[s - 1] * d % n, False
     for j in range(s - 2, -1, -1):
-        if not inf:
-            a = 2 * a % n
-        adds = [("Q", V[j] * d % n)]
+        T = V[j] * d % n
+        if inf:
+            a, inf = T, False
+            ev.append(("from_inf", j, "Q"))
+        elif (a - T) % n == 0:
+            ev.append(("dbl", j, "Q"))
+            a = 3 * T % n
+        elif (a + T) % n == 0:
+            ev.append(("neg", j, "Q"))
+            a = -T % n
+        elif (2 * a + T) % n == 0:
+            ev.append(("inf", j, "Q"))
+            a, inf = 0, True
+        else:
+            a = (2 * a + T) % n
+        adds = []
         if j & 1:
             adds.append(("G", (2 * W[j + 1] + W[j]) % n))
         if j == 0:
@@ -189,9 +204,10 @@ def fold_crafted(curve, t: int, s: int, seed: int = 17, tries: int = 20000,
     """(u1, u2, d) triples whose folded Horner takes each degenerate branch
     reachable by construction -- the last columns, where the remaining sum can
     be solved for: u1's column-0 entry doubling / cancelling the sum (the
-    single-column table), u2's column-0 entry doubling / cancelling it, the
-    column-1 pair entry doubling / cancelling it, and u2's column-1 entry
-    cancelling it (the pair then taken from infinity). u1 is drawn, u2 is
+    single-column table), u2's column-0 composite 2 A + T meeting A == T,
+    A == -T and 2 A + T == 0, the column-1 pair entry doubling / cancelling
+    the sum, and u2's column-1 composite cancelling it (the pair then taken
+    from infinity). u1 is drawn, u2 is
     solved from the wanted total u1 + u2 d, and kept when its own column
     pattern matches the one the total assumed (~1/2^t). low_s: a finite
     R = u1 G + u2 Q must give s = x(R) / u2 <= n / 2 (Fabric's rule), else the
@@ -199,8 +215,8 @@ def fold_crafted(curve, t: int, s: int, seed: int = 17, tries: int = 20000,
     import random
     n = curve.n
     rng = random.Random(seed)
-    want = {("dbl", 0, "G"), ("inf", 0, "G"), ("dbl", 0, "Q"), ("inf", 0, "Q"),
-            ("dbl", 1, "G"), ("inf", 1, "G"), ("inf", 1, "Q")}
+    want = {("dbl", 0, "G"), ("inf", 0, "G"), ("dbl", 0, "Q"), ("neg", 0, "Q"),
+            ("inf", 0, "Q"), ("dbl", 1, "G"), ("inf", 1, "G"), ("inf", 1, "Q")}
     found, out = set(), []
     for _ in range(tries):
         if found == want:
@@ -214,7 +230,8 @@ def fold_crafted(curve, t: int, s: int, seed: int = 17, tries: int = 20000,
         targets = {  # event -> the total u1 + u2 d it needs (v0 = u2's assumed column 0)
             ("dbl", 0, "G"): 2 * W[0],
             ("inf", 0, "G"): 0,
-            ("dbl", 0, "Q"): 2 * v0 * d + W[0],
+            ("dbl", 0, "Q"): 3 * v0 * d + W[0],
+            ("neg", 0, "Q"): -v0 * d + W[0],
             ("inf", 0, "Q"): W[0],
             ("dbl", 1, "G"): 4 * pair1 + v0 * d + W[0],
             ("inf", 1, "G"): v0 * d + W[0],

@@ -319,9 +319,9 @@ def test_hostsim_folded_g_crafted_events(hs, curve):
     Records crafted (tests/comb_cases.py fold_crafted) so that the joint
     Horner takes every degenerate branch reachable by construction: the u1
     single-column entry and the column-1 pair entry doubling / cancelling the
-    running sum, u2's column-0 entry doubling / cancelling it, u2's column-1
-    entry cancelling it (the pair entry then taken from infinity), and a total
-    at infinity. Through the one-lane comb route with every record on a key
+    running sum, u2's column-0 composite 2 A + T (ll_dbladd) meeting A == T,
+    A == -T and 2 A + T == 0, u2's column-1 composite cancelling the sum (the
+    pair entry then taken from infinity), and a total at infinity. Through the one-lane comb route with every record on a key
     table: the verdicts equal the construction (valid 0, twins / infinity 9)."""
     from oracle import ecdsa_ref as O
     from tests.comb_cases import fold_crafted, fold_events, records_for_fold
@@ -331,7 +331,7 @@ def test_hostsim_folded_g_crafted_events(hs, curve):
     triples = fold_crafted(c, t, s, seed=31)
     kinds = {x[3] for x in triples}
     assert {("dbl", 0, "G"), ("inf", 0, "G"), ("dbl", 1, "G"), ("inf", 1, "G"),
-            ("dbl", 0, "Q"), ("inf", 0, "Q"), ("inf", 1, "Q")} <= kinds
+            ("dbl", 0, "Q"), ("neg", 0, "Q"), ("inf", 0, "Q"), ("inf", 1, "Q")} <= kinds
     for u1, u2, d, key, _ in triples:
         assert key in fold_events(u1, u2, d, c.n, t, s)[0]
     recs = records_for_fold(c, triples, low_s=False)
