@@ -1505,68 +1505,47 @@ BH_HD void q_llcomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32
 // ---- u1 G folded into the key comb's Horner (round 5) ---------------------------
 // The G half shares the key comb's s - 1 = 36 doublings. u1 is recoded like u2
 // (ll_slices: k = u1 or u1 + n, t = 7 teeth x s = 37 columns, digits +-1), so
-// u1 G = sum_j 2^j W_j G with W_j = sum_i d_(i,j) 2^(s i). The Horner adds, at
-// every odd column j = 35, 33, ..., 1, the column pair (j + 1, j) as ONE point
-//   (2 W_(j+1) + W_j) G
-// (adding W_(j+1) one column late, doubled once, is the same sum), and at
-// column 0 the single column W_0 G. The pair table holds the 2^13 sign
-// patterns whose top digit (tooth t - 1 of column j + 1) is +1 -- every entry
-// a multiple of G in (2^223 - 2^222, 3 * 2^222), never infinity; the other
-// 2^13 patterns are their negatives -- and the single-column table the 2^6
-// patterns of one column with its top digit +1: 8,256 affine points, 660 KB
-// per curve (L2-resident), built at bh_init. 18 + 1 = 19 mixed additions per
-// record instead of the separate 13-bit G comb's 20, and no u1 G partial sum
-// stored by the build kernel and reloaded, no final Jacobian addition A + B.
-constexpr uint32_t kG2Ent = 1u << (2 * kLLTeeth - 1);  // two-column entries
-constexpr uint32_t kG1Ent = kLLEnt;                     // single-column entries
-constexpr size_t kG2Words = (size_t)(kG2Ent + kG1Ent) * kLLAff;
+// u1 G = sum_j 2^j W_j G with W_j = sum_i d_(i,j) 2^(s i). The Horner adds the
+// columns in groups of kGF (BH_GFOLD, default 3): the group of columns
+// j, .., j + kGF - 1 (j = 1, 1 + kGF, ..., s - kGF) as ONE point
+//   (sum_c 2^c W_(j+c)) G
+// at column j (adding W_(j+c) c columns late, doubled c times, is the same
+// sum), and column 0 alone. The group table holds the sign patterns whose top
+// digit (tooth t - 1 of column j + kGF - 1) is +1 -- every entry a positive
+// multiple of G below 2^(225 + kGF), never infinity; the other half are their
+// negatives -- and the single-column table the 2^(t-1) patterns of one column
+// with its top digit +1. kGF = 2: 8,192 + 64 affine points, 660 KB per curve
+// (L2-resident), 18 + 1 = 19 mixed additions per record; kGF = 3: 2^20 + 64
+// points, 84 MB (MALL), 12 + 1 = 13. Built at bh_init. Against the separate
+// 13-bit G comb (20 mixed additions) the fold also drops the u1 G partial sum
+// the build kernel stored and k_keycomb reloaded, and the final addition A + B.
+#ifndef BH_GFOLD
+#define BH_GFOLD 3  // same box (profiles/r05/v6): 2 columns 179.8 / 180.6, 3 columns 188.5 / 189.2 M/s
+#endif
+constexpr int kGF = BH_GFOLD;
+static_assert(kGF >= 1 && kGF <= 4 && (kLLSpace - 1) % kGF == 0,
+              "column groups of the folded G tables tile columns 1 .. s - 1");
+constexpr int kGFBits = (kLLTeeth - 1) + (kGF - 1) * kLLTeeth;  // group entry index bits
+constexpr uint32_t kG2Ent = 1u << kGFBits;                        // group entries
+constexpr uint32_t kG1Ent = kLLEnt;                               // single-column entries
+constexpr int kGAdds = (kLLSpace - 1) / kGF + 1;                  // G additions per record
+// base points of the tables' construction: (2 m + 1) 2^(s i) G, i < t, m < 2^(kGF-1)
+constexpr uint32_t kGOdd = 1u << (kGF - 1);
+constexpr uint32_t kGBase = (uint32_t)kLLTeeth * kGOdd;
+constexpr size_t kG2Words = (size_t)(kG2Ent + kG1Ent + kGBase) * kLLAff;
 // Per curve, one device buffer holds the 13-bit G comb (ladder records,
-// registry-table records, small batches) and, after it, the folded tables.
+// registry-table records, small batches) and, after it, the folded tables
+// (group entries, single-column entries, base points).
 constexpr size_t kGCombWords = (size_t)kCombWindows * kCombEntries * kGEntry;
 constexpr size_t kGTabAllWords = kGCombWords + kG2Words;
 static_assert(kGCombWords % 4 == 0, "folded tables 16-byte aligned");
 BH_HD const uint32_t* g2_of(const uint32_t* gtab) { return gtab + kGCombWords; }
-static_assert(kLLSpace % 2 == 1, "pairs (j + 1, j) at odd j cover columns 1 .. s - 1");
 
-// Entry t of the folded G tables: t < kG2Ent the pair pattern (hi, lo) =
-// ((1 << (t_teeth - 1)) | t >> t_teeth, t & (2^t - 1)) -> (2 W(hi) + W(lo)) G;
-// else the single column (1 << (t - 1)) | (t - kG2Ent) -> W G. Affine,
-// canonical Montgomery radix 2^30, in the 80-byte llaff layout. One lane per
-// entry at bh_init (and in the host harness).
+// v G for v < 2^288 (v != 0) by left-to-right double-and-add from the affine
+// G, made affine (Fermat inverse). A = m G with 2 <= m < v before every
+// addition, never +-G, for v < n. Init-time only.
 template <class P>
-BH_HD void gtab2_entry(uint32_t t, uint32_t* out) {
-  constexpr uint32_t top = 1u << (kLLTeeth - 1), all = (1u << kLLTeeth) - 1u;
-  int c[kLLTeeth];
-  if (t < kG2Ent) {
-    const uint32_t hi = top | (t >> kLLTeeth), lo = t & all;
-    for (int i = 0; i < kLLTeeth; i++)
-      c[i] = 2 * (2 * (int)((hi >> i) & 1u) - 1) + (2 * (int)((lo >> i) & 1u) - 1);
-  } else {
-    const uint32_t b = top | (t - kG2Ent);
-    for (int i = 0; i < kLLTeeth; i++) c[i] = 2 * (int)((b >> i) & 1u) - 1;
-  }
-  // v = sum c_i 2^(s i) > 0 (the top term dominates), as 9 x 32-bit words
-  uint32_t pos[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, neg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (int i = 0; i < kLLTeeth; i++) {
-    uint32_t* dst = c[i] > 0 ? pos : neg;
-    const uint64_t mag = (uint64_t)(c[i] > 0 ? c[i] : -c[i]) << ((kLLSpace * i) & 31);
-    const int wd = (kLLSpace * i) >> 5;
-    uint64_t cy = mag;
-    for (int q = wd; q < 9 && cy; q++) {
-      cy += dst[q];
-      dst[q] = (uint32_t)cy;
-      cy >>= 32;
-    }
-  }
-  uint32_t v[9];
-  int64_t br = 0;
-  for (int q = 0; q < 9; q++) {
-    br += (int64_t)pos[q] - (int64_t)neg[q];
-    v[q] = (uint32_t)br;
-    br >>= 32;  // arithmetic: 0 or -1
-  }
-  // v G by left-to-right double-and-add from the affine G: A = m G with
-  // 2 <= m < 2^227 before every addition, never +-G
+BH_HD void scalar_g_affine(const uint32_t v[9], uint32_t x[9], uint32_t y[9]) {
   uint32_t gx[9], gy[9];
   f_const(gx, P::gx_m);
   f_const(gy, P::gy_m);
@@ -1583,7 +1562,7 @@ BH_HD void gtab2_entry(uint32_t t, uint32_t* out) {
       (void)j_madd<P>(A, A, gx, gy, &same);
     }
   }
-  uint32_t z[9], zi[9], zi2[9], x[9], y[9];
+  uint32_t z[9], zi[9], zi2[9];
   f_reduce<P>(z, A.Z);
   f_inv<P>(zi, z);
   f_sqr<P>(zi2, zi);
@@ -1592,31 +1571,89 @@ BH_HD void gtab2_entry(uint32_t t, uint32_t* out) {
   f_mul<P>(y, A.Y, zi2);
   f_reduce<P>(x, x);
   f_reduce<P>(y, y);
-  llaff_store(out, 0, x, y);
 }
 
-// The folded G entry added at column j of u1's slices: the pair (j + 1, j) for
-// odd j, the single column for j = 0 (index past the pair table). neg: the
-// entry's negative (all digits flipped).
+// Base point k = i * kGOdd + m of the folded tables: (2 m + 1) 2^(s i) G,
+// affine, at slot kG2Ent + kG1Ent + k. One lane per point (init kernel 1).
+template <class P>
+BH_HD void gtab2_base(uint32_t k, uint32_t* g2) {
+  const uint32_t i = k / kGOdd, m = k % kGOdd;
+  uint32_t v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const int b = kLLSpace * (int)i;
+  const uint64_t mag = (uint64_t)(2u * m + 1u) << (b & 31);
+  v[b >> 5] = (uint32_t)mag;
+  if ((b >> 5) + 1 < 9) v[(b >> 5) + 1] = (uint32_t)(mag >> 32);
+  uint32_t x[9], y[9];
+  scalar_g_affine<P>(v, x, y);
+  llaff_store(g2, kG2Ent + kG1Ent + k, x, y);
+}
+
+// Entry t of the folded tables (init kernel 2, after the base points): t <
+// kG2Ent a group pattern -- index bits, most significant first: the top
+// column's lower t - 1 teeth (its top tooth is +1), then the other kGF - 1
+// columns' t teeth each, highest column first; else the single column
+// (1 << (t - 1)) | (t - kG2Ent). The point sum_i c_i 2^(s i) G with odd c_i,
+// |c_i| < 2^kGF, c_(t-1) > 0, from the top term down by mixed additions of
+// +-base points (a partial sum above 2^(s (i+1)) - ... never meets +-|c_i|
+// 2^(s i) G), made affine by safegcd. Affine radix-2^30 Montgomery in the
+// 80-byte llaff layout.
+template <class P>
+BH_HD void gtab2_entry(uint32_t t, uint32_t* g2) {
+  constexpr uint32_t top = 1u << (kLLTeeth - 1), all = (1u << kLLTeeth) - 1u;
+  int c[kLLTeeth];
+  for (int i = 0; i < kLLTeeth; i++) c[i] = 0;
+  if (t < kG2Ent) {
+    for (int cc = 0; cc < kGF; cc++) {  // column cc of the group (0 = lowest)
+      const uint32_t bits = cc == kGF - 1 ? (top | (t >> ((kGF - 1) * kLLTeeth)))
+                                          : (t >> (cc * kLLTeeth)) & all;
+      for (int i = 0; i < kLLTeeth; i++) c[i] += (2 * (int)((bits >> i) & 1u) - 1) << cc;
+    }
+  } else {
+    const uint32_t b = top | (t - kG2Ent);
+    for (int i = 0; i < kLLTeeth; i++) c[i] = 2 * (int)((b >> i) & 1u) - 1;
+  }
+  J30 A;
+  llaff_load(A.X, A.Y, g2, kG2Ent + kG1Ent + (uint32_t)(kLLTeeth - 1) * kGOdd +
+                               (uint32_t)((c[kLLTeeth - 1] - 1) / 2));
+  f_const(A.Z, P::r1);
+  for (int i = kLLTeeth - 2; i >= 0; i--) {
+    const int a = c[i] < 0 ? -c[i] : c[i];
+    uint32_t bx[9], by[9];
+    llaff_load(bx, by, g2, kG2Ent + kG1Ent + (uint32_t)i * kGOdd + (uint32_t)((a - 1) / 2));
+    if (c[i] < 0) f_neg<P, 64>(by, by);
+    bool same;
+    (void)j_madd<P>(A, A, bx, by, &same);  // never degenerate (see above)
+  }
+  uint32_t zi[9], x[9], y[9];
+  f_inv_sg<P>(zi, A.Z);
+  ll_to_affine<P>(x, y, A, zi);
+  llaff_store(g2, t, x, y);
+}
+
+// The folded G entry added at column j of u1's slices: the group of columns
+// j .. j + kGF - 1 (j >= 1), the single column for j = 0 (index past the
+// group table). neg: the entry's negative (all digits flipped).
 BH_HD void g2_column(const uint64_t gl[kLLTeeth], int j, uint32_t& idx, bool& neg) {
   if (j == 0) {
     ll_column(gl, 0, idx, neg);
     idx += kG2Ent;
     return;
   }
-  uint32_t hi = 0, lo = 0;
-#pragma unroll
-  for (int t = 0; t < kLLTeeth; t++) {
-    hi |= (uint32_t)((gl[t] >> (j + 1)) & 1ull) << t;
-    lo |= (uint32_t)((gl[t] >> j) & 1ull) << t;
-  }
-  neg = ((hi >> (kLLTeeth - 1)) & 1u) == 0u;
   constexpr uint32_t all = (1u << kLLTeeth) - 1u;
-  if (neg) {
-    hi = ~hi & all;
-    lo = ~lo & all;
+  uint32_t col[kGF];
+#pragma unroll
+  for (int cc = 0; cc < kGF; cc++) {
+    uint32_t b = 0;
+#pragma unroll
+    for (int t = 0; t < kLLTeeth; t++) b |= (uint32_t)((gl[t] >> (j + cc)) & 1ull) << t;
+    col[cc] = b;
   }
-  idx = ((hi & (all >> 1)) << kLLTeeth) | lo;
+  neg = ((col[kGF - 1] >> (kLLTeeth - 1)) & 1u) == 0u;
+  uint32_t x = col[kGF - 1] & (all >> 1);
+  if (neg) x = ~col[kGF - 1] & (all >> 1);
+#pragma unroll
+  for (int cc = kGF - 2; cc >= 0; cc--) x = (x << kLLTeeth) | ((neg ? ~col[cc] : col[cc]) & all);
+  idx = x;
 }
 
 // A += +-(tx, ty) with the explicit degenerate cases (A at infinity: A = T;
@@ -1682,8 +1719,8 @@ BH_HD void ll_dbladd(J30& A, bool& a_inf, const uint32_t tx[9], uint32_t ty[9], 
 
 // u1 G + u2 Q from the key's signed comb table (stride as q_llcomb) and the
 // folded G tables g2: Horner from the top column; at column j A = 2 A + V_j Q
-// (ll_dbladd), and at odd j and j = 0 the folded G entry (loaded one step
-// ahead).
+// (ll_dbladd), and at the lowest column of each G group and at j = 0 the
+// folded G entry (loaded one group ahead).
 template <class P>
 BH_HD void q_llcomb_g(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab,
                       uint32_t stride, const uint32_t* g2) {
@@ -1703,7 +1740,7 @@ BH_HD void q_llcomb_g(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint
   a_inf = false;
   uint32_t gx[9], gy[9], gidx;
   bool gneg;
-  g2_column(gl, kLLSpace - 2, gidx, gneg);
+  g2_column(gl, kLLSpace - kGF, gidx, gneg);
   llaff_load(gx, gy, g2, gidx);
 #pragma unroll 1
   for (int j = kLLSpace - 2; j >= 0; j--) {
@@ -1714,10 +1751,10 @@ BH_HD void q_llcomb_g(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint
       else llaff_load(tx, ty, tab, idx);
       ll_dbladd<P>(A, a_inf, tx, ty, neg, one);  // A = 2 A + V_j Q
     }
-    if ((j & 1) || j == 0) {
+    if (j == 0 || (j - 1) % kGF == 0) {
       ll_madd<P>(A, a_inf, gx, gy, gneg, one);
-      if (j > 0) {  // the next folded G entry: column j - 2, or column 0
-        g2_column(gl, j >= 3 ? j - 2 : 0, gidx, gneg);
+      if (j > 0) {  // the next folded G entry: the group at j - kGF, or column 0
+        g2_column(gl, j > kGF ? j - kGF : 0, gidx, gneg);
         llaff_load(gx, gy, g2, gidx);
       }
     }

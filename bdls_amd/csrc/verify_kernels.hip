@@ -766,17 +766,20 @@ __global__ __launch_bounds__(256) void k_small_lad(Work w, const uint32_t* __res
   if (l == 0) reason[j] = finish_check<P>(w, j, C, c_inf, C, true) ? R_OK : R_MATH;
 }
 
-// G tables (verify.h gtab_entry, gtab2_entry): one lane per entry -- the
-// 13-bit comb, then the folded two-column / single-column tables after it.
+// G tables (verify.h gtab_entry, gtab2_base, gtab2_entry): one lane per
+// entry -- the 13-bit comb and the folded tables' base points, then (a second
+// launch) the folded group / single-column entries from those base points.
 template <class P>
 __global__ __launch_bounds__(64) void k_gtab_build(uint32_t* gtab) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   constexpr uint32_t nc = (uint32_t)(kCombWindows * kCombEntries);
-  if (t < nc) {
-    gtab_entry<P>(t, gtab + (size_t)t * kGEntry);
-  } else if (t < nc + kG2Ent + kG1Ent) {
-    gtab2_entry<P>(t - nc, gtab + kGCombWords + (size_t)(t - nc) * kLLAff);
-  }
+  if (t < nc) gtab_entry<P>(t, gtab + (size_t)t * kGEntry);
+  else if (t < nc + kGBase) gtab2_base<P>(t - nc, gtab + kGCombWords);
+}
+template <class P>
+__global__ __launch_bounds__(64) void k_gtab2_build(uint32_t* gtab) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < kG2Ent + kG1Ent) gtab2_entry<P>(t, gtab + kGCombWords);
 }
 
 // bh_keys_register: keys only (X || Y per record) -> Work.qx / qy / st.
@@ -878,12 +881,14 @@ hipError_t launch_expand(const uint8_t* keys, const uint32_t* key_idx, uint8_t* 
 }
 
 hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s) {
-  const int nt = kCombWindows * kCombEntries + (int)(kG2Ent + kG1Ent);
-  if (curve == 0)
-    hipLaunchKernelGGL((k_gtab_build<F30_p256>), dim3((nt + 63) / 64), dim3(64), 0, s,
-                       gtab);
-  else
+  const int nt = kCombWindows * kCombEntries + (int)kGBase, nt2 = (int)(kG2Ent + kG1Ent);
+  if (curve == 0) {
+    hipLaunchKernelGGL((k_gtab_build<F30_p256>), dim3((nt + 63) / 64), dim3(64), 0, s, gtab);
+    hipLaunchKernelGGL((k_gtab2_build<F30_p256>), dim3((nt2 + 63) / 64), dim3(64), 0, s, gtab);
+  } else {
     hipLaunchKernelGGL((k_gtab_build<F30_k1>), dim3((nt + 63) / 64), dim3(64), 0, s, gtab);
+    hipLaunchKernelGGL((k_gtab2_build<F30_k1>), dim3((nt2 + 63) / 64), dim3(64), 0, s, gtab);
+  }
   return hipGetLastError();
 }
 

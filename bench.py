@@ -96,9 +96,11 @@ FP_KTAB = ((LL_T - 1) * LL_S * 8                                     # the doubl
            + 6 * (_LL_NL + _LL_NH) + FP_INV_SG                       # L, H affine
            + 6 * _LL_ENT - 1 + FP_INV_SG) if LL_TABLES else 65 * 58  # entries H + L
 # round 5: with comb tables u1 G is folded into k_keycomb's Horner (verify.h
-# q_llcomb_g): 19 mixed additions from the two-column G table (18 column pairs
-# + column 0) and the x check (~7 ops), no stored u1 G half and no final A + B
-FOLD_G_ADDS = (LL_S - 1) // 2 + 1
+# q_llcomb_g): (LL_S - 1) / G_FOLD + 1 mixed additions (13 at 3 columns per
+# entry: 12 column groups + column 0) and the x check (~7 ops), no stored u1 G
+# half and no final A + B
+G_FOLD = int(os.environ.get("BH_GFOLD", 3))  # u1 columns per folded G entry (verify.h kGF)
+FOLD_G_ADDS = (LL_S - 1) // G_FOLD + 1
 # Each Horner step A = 2 A + V_j Q is (A + T) + A: a mixed addition that also
 # rescales A (8M + 3S) + a co-Z addition (5M + 2S) = 18 ops (verify.h ll_dbladd)
 FP_KEYCOMB = ((LL_S - 1) * 18 + FOLD_G_ADDS * 11 + 7) if LL_TABLES else 65 * 16 + 23

@@ -152,14 +152,15 @@ def comb_columns(u: int, n: int, t: int, s: int) -> list[int]:
     return [sum((2 * ((c >> (s * i + j)) & 1) - 1) << (s * i) for i in range(t)) for j in range(s)]
 
 
-def fold_events(u1: int, u2: int, d: int, n: int, t: int, s: int):
+def fold_events(u1: int, u2: int, d: int, n: int, t: int, s: int, kgf: int = 2):
     """The folded Horner (q_llcomb_g) on u1 G + u2 Q with Q = d G, as integers
     mod n (multiples of G), in the kernel's order: load the top column of u2;
     per column j = s-2 .. 0 the composite A = 2 A + V_j Q computed as
     (A + T) + A (ll_dbladd, kind "Q": A == T -> "dbl", A == -T -> "neg",
-    2 A + T == 0 -> "inf"), then at odd j the u1 pair (j+1, j) and at j = 0
-    the u1 column 0 (a mixed addition, kind "G": A == T -> "dbl", A == -T ->
-    "inf"). Returns ([(event, column, kind)], total is infinity)."""
+    2 A + T == 0 -> "inf"), then at the lowest column j of each group of kgf
+    u1 columns (j = 1, 1 + kgf, ...) the group's point sum_c 2^c W_(j+c), and
+    at j = 0 the u1 column 0 (a mixed addition, kind "G": A == T -> "dbl",
+    A == -T -> "inf"). Returns ([(event, column, kind)], total is infinity)."""
     V, W = comb_columns(u2, n, t, s), comb_columns(u1, n, t, s)
     ev, a, inf = [], V[s - 1] * d % n, False
     for j in range(s - 2, -1, -1):
@@ -179,8 +180,8 @@ def fold_events(u1: int, u2: int, d: int, n: int, t: int, s: int):
         else:
             a = (2 * a + T) % n
         adds = []
-        if j & 1:
-            adds.append(("G", (2 * W[j + 1] + W[j]) % n))
+        if j >= 1 and (j - 1) % kgf == 0:
+            adds.append(("G", sum(W[j + c] << c for c in range(kgf)) % n))
         if j == 0:
             adds.append(("G", W[0] % n))
         for kind, T in adds:
@@ -200,7 +201,7 @@ def fold_events(u1: int, u2: int, d: int, n: int, t: int, s: int):
 
 
 def fold_crafted(curve, t: int, s: int, seed: int = 17, tries: int = 20000,
-                 low_s: bool = False):
+                 low_s: bool = False, kgf: int = 2):
     """(u1, u2, d) triples whose folded Horner takes each degenerate branch
     reachable by construction -- the last columns, where the remaining sum can
     be solved for: u1's column-0 entry doubling / cancelling the sum (the
@@ -226,7 +227,7 @@ def fold_crafted(curve, t: int, s: int, seed: int = 17, tries: int = 20000,
         W = comb_columns(u1, n, t, s)
         p = [rng.choice((-1, 1)) for _ in range(t)]
         v0 = sum(x << (s * i) for i, x in enumerate(p))
-        pair1 = 2 * W[2] + W[1]
+        pair1 = sum(W[1 + c] << c for c in range(kgf))  # the G group added at column 1
         targets = {  # event -> the total u1 + u2 d it needs (v0 = u2's assumed column 0)
             ("dbl", 0, "G"): 2 * W[0],
             ("inf", 0, "G"): 0,
@@ -243,7 +244,7 @@ def fold_crafted(curve, t: int, s: int, seed: int = 17, tries: int = 20000,
             u2 = (total - u1) * pow(d, -1, n) % n
             if not u2:
                 continue
-            ev, inf = fold_events(u1, u2, d, n, t, s)
+            ev, inf = fold_events(u1, u2, d, n, t, s, kgf)
             if key not in [e for e in ev if e[0] != "from_inf"][:1]:
                 continue
             if low_s and not inf:

@@ -22,8 +22,8 @@ static const uint32_t* gtab_for() {
     g.assign(kGTabAllWords, 0);
     for (uint32_t t = 0; t < (uint32_t)(kCombWindows * kCombEntries); t++)
       gtab_entry<P>(t, g.data() + (size_t)t * kGEntry);
-    for (uint32_t t = 0; t < kG2Ent + kG1Ent; t++)
-      gtab2_entry<P>(t, g.data() + kGCombWords + (size_t)t * kLLAff);
+    for (uint32_t k = 0; k < kGBase; k++) gtab2_base<P>(k, g.data() + kGCombWords);
+    for (uint32_t t = 0; t < kG2Ent + kG1Ent; t++) gtab2_entry<P>(t, g.data() + kGCombWords);
   }
   return g.data();
 }
@@ -39,6 +39,8 @@ static int g_ll = 0;
 extern "C" void hs_set_ll(int on) { g_ll = on; }
 // the comb's shape as built (teeth << 8 | spacing), for the crafted-scalar tests
 extern "C" uint32_t hs_ll_shape() { return ((uint32_t)kLLTeeth << 8) | (uint32_t)kLLSpace; }
+// u1 columns per folded G entry as built (BH_GFOLD)
+extern "C" uint32_t hs_gfold() { return (uint32_t)kGF; }
 // the G comb's window width as built (BH_GCOMB_BITS)
 extern "C" uint32_t hs_gcomb_bits() { return (uint32_t)kGW; }
 

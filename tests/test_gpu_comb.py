@@ -106,7 +106,8 @@ def p256_edge_batch(golden):
         want += [0 if k % 2 == 0 else 9] * 4
     # round 5: the folded u1 G (k_keycomb's q_llcomb_g) on records whose joint
     # Horner takes each degenerate branch (tests/comb_cases.py fold_crafted)
-    fold = records_for_fold(c, fold_crafted(c, 7, 37, seed=33, low_s=True), low_s=True)
+    kgf = int(os.environ.get("BH_GFOLD", 3))  # the library's G group size (verify.h kGF)
+    fold = records_for_fold(c, fold_crafted(c, 7, 37, seed=33, low_s=True, kgf=kgf), low_s=True)
     assert len(fold) >= 13
     for qx, qy, sig, dg, exp in fold:
         for _ in range(4):

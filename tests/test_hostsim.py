@@ -328,12 +328,13 @@ def test_hostsim_folded_g_crafted_events(hs, curve):
     c = getattr(O, curve)
     sh = hs.hs_ll_shape()
     t, s = sh >> 8, sh & 0xFF
-    triples = fold_crafted(c, t, s, seed=31)
+    kgf = hs.hs_gfold()
+    triples = fold_crafted(c, t, s, seed=31, kgf=kgf)
     kinds = {x[3] for x in triples}
     assert {("dbl", 0, "G"), ("inf", 0, "G"), ("dbl", 1, "G"), ("inf", 1, "G"),
             ("dbl", 0, "Q"), ("neg", 0, "Q"), ("inf", 0, "Q"), ("inf", 1, "Q")} <= kinds
     for u1, u2, d, key, _ in triples:
-        assert key in fold_events(u1, u2, d, c.n, t, s)[0]
+        assert key in fold_events(u1, u2, d, c.n, t, s, kgf)[0]
     recs = records_for_fold(c, triples, low_s=False)
     pub = np.frombuffer(b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big")
                                  for x, y, _, _, _ in recs), np.uint8)
