@@ -298,6 +298,51 @@ BH_HD bool j_madd_co(J30& r, J30& pz, const J30& p, const uint32_t x2[9], const 
   return degenerate;
 }
 
+// j_add that also returns pz = p rescaled to r's Z: (U1 H^2, S1 H^3, Z3) with
+// U1 = X1 Z2^2, S1 = Y1 Z2^3 (Z3 = Z1 Z2 H) -- intermediates of the addition,
+// the co-Z partner j_zaddu needs for 2 p + q = (p + q) + p. Requirements and
+// degenerate contract as j_add (r may alias p). pz beta (2, 2, 2).
+template <class F>
+BH_HD bool j_add_co(J30& r, J30& pz, const J30& p, const J30& q, bool* same_y) {
+  uint32_t z1z1[9], z2z2[9], u1[9], u2[9], s1[9], s2[9], h[9], rr[9], t[9], hh[9], hhh[9];
+  f_sqr<F>(z1z1, p.Z);                    // [b2]
+  f_sqr<F>(z2z2, q.Z);                    // [b2]
+  f_mul<F>(u1, p.X, z2z2);                // [b2]
+  f_mul<F>(u2, q.X, z1z1);                // [b2]
+  f_mul<F>(t, q.Z, z2z2);                 // [b2]
+  f_mul<F>(s1, p.Y, t);                   // [b2]
+  f_mul<F>(t, p.Z, z1z1);                 // [b2]
+  f_mul<F>(s2, q.Y, t);                   // [b2]
+  f_sub<F, 32>(h, u2, u1);                // [b34]
+  f_sub<F, 32>(rr, s2, s1);               // [b34]
+  f_sqr<F>(hh, h);                        // [b2]
+  f_mul<F>(hhh, hh, h);                   // [b2]
+  f_mul<F>(pz.X, u1, hh);                 // [b2]  V = U1 H^2
+  f_sqr<F>(t, rr);                        // [b2]  r^2
+  f_mulc<2>(u2, pz.X);                    // [b4]
+  f_add(u2, u2, hhh);                     // [b6]
+  f_sub<F, 32>(r.X, t, u2);               // [b34]  X3 = r^2 - H^3 - 2V
+  f_mulc<3>(u2, pz.X);                    // [b6]
+  f_add(u2, u2, hhh);                     // [b8]
+  f_sub<F, 32>(u2, u2, t);                // [b40]
+  f_mul<F>(u2, rr, u2);                   // [b2]  34*40
+  f_mul<F>(pz.Y, s1, hhh);                // [b2]  S1 H^3
+  f_sub<F, 32>(r.Y, u2, pz.Y);            // [b34]
+  f_mul<F>(t, p.Z, q.Z);                  // [b2]
+  f_mul<F>(r.Z, t, h);                    // [b2]
+  f_copy(pz.Z, r.Z);
+  const bool degenerate = f_is_zero2<F>(r.Z);
+  if (degenerate) {
+    f_reduce<F>(t, rr);
+    uint32_t z = 0;
+    for (int i = 0; i < 9; i++) z |= t[i];
+    *same_y = (z == 0);
+  } else {
+    *same_y = false;
+  }
+  return degenerate;
+}
+
 // y^2 == x^3 + a x + b for Montgomery-domain x, y with beta <= 2.
 template <class F>
 BH_HD bool j_on_curve(const uint32_t x[9], const uint32_t y[9]) {

@@ -1770,6 +1770,146 @@ BH_HD bool stage_keycomb_fold(const Work& w, uint32_t i, const uint32_t* tab, ui
   return finish_check<P>(w, i, A, a_inf, A, true);
 }
 
+// ---- variable-base ladder with u1 G folded in (round 5; P-256) ---------------
+// u2 Q by odd signed 5-bit windows -- the regular recoding: k = u2, or u2 + n
+// when u2 is even, is odd; digit i = 2 b_i - 31 with b_i = bits [5i+1, 5i+5]
+// of k (odd, nonzero, in [-31, 31]), the top digit (i = 51) 2 bit_256 + 1 > 0
+// -- so every window is A = 32 A + d_i Q = 2 (16 A) + d_i Q: 4 doublings and
+// the composite (A + T) + A (j_dbladd: j_add_co + j_zaddu, 16 + 7 F_p ops
+// against a doubling's 8 + an addition's 16) with no zero digit to skip. The
+// table holds the odd multiples Q, 3 Q, ..., 31 Q from a co-Z chain (DBLU + 15
+// ZADDU: 114 F_p ops against 162 for 1..16 Q). u1 G is folded into the same
+// doubling chain: the folded G groups of k_keycomb (g2_column: kGF columns of
+// u1's 7 x 37 comb, weight 2^j at j = 0, 1, 1 + kGF, ..., 37 - kGF) are mixed
+// additions at the doubling positions with that weight (the last 7 windows):
+// 13 of them against the 13-bit G comb's 20 plus the final A + B. Per verify
+// ~3,070 F_p ops against ~3,280 (3,200).
+//
+// A = 2 A + T for a Jacobian T (already signed), degenerate cases as
+// ll_dbladd: A at infinity -> T; A == T -> 3 T; A == -T -> A (unchanged);
+// A + T == -A -> infinity.
+template <class P>
+BH_HD void j_dbladd(J30& A, bool& a_inf, const J30& T) {
+  if (a_inf) {  // rare: 2 inf + T
+    j_copy(A, T);
+    a_inf = false;
+    return;
+  }
+  J30 R, Az;
+  bool same;
+  if (j_add_co<P>(R, Az, A, T, &same)) {  // rare: A == +-T
+    if (same) {
+      J30 D;
+      j_dbl<P>(D, T);
+      (void)j_add<P>(A, D, T, &same);  // 2 T + T: 2 T != +-T (prime order)
+    }  // else A == -T: 2 A + T = A, unchanged
+    return;
+  }
+  j_zaddu<P>(A, R, Az);
+  if (f_is_zero2<P>(A.Z)) a_inf = true;  // rare: A + T == -A
+}
+
+// the doubling positions (remaining doublings = weight exponent) that take a
+// folded G entry: 0 (column 0) and the groups' lowest columns 1, 1 + kGF, ...
+BH_HD bool g_fold_pos(int p) { return p == 0 || (p >= 1 && p <= kLLSpace - kGF && (p - 1) % kGF == 0); }
+
+template <class P>
+BH_HD void q_ladder_odd_g(J30& A, bool& a_inf, const Work& w, uint32_t i, uint32_t wave,
+                          uint32_t lane, const uint32_t* g2) {
+  using Cv = CvOf<P>;
+  uint32_t u2[8], u1[8], qx[9], qy[9], one[9];
+  ld8(u2, w.r, i, w.ns);
+  ld8(u1, w.e, i, w.ns);
+  ld9(qx, w.qx, i, w.ns);
+  ld9(qy, w.qy, i, w.ns);
+  f_const(one, P::r1);
+  // odd multiples (2m + 1) Q, m = 0..15: DBLU, then S += D by ZADDU (D rescaled)
+  {
+    J30 Qa, D, S;
+    f_copy(Qa.X, qx);
+    f_copy(Qa.Y, qy);
+    f_copy(Qa.Z, one);
+    j_dblu<P>(D, S, Qa);  // D = 2 Q, S = Q on D's Z
+    qtab_store(w.qtab, wave, 0, lane, S);
+#pragma unroll 1
+    for (uint32_t m = 1; m < (uint32_t)kQTab; m++) {
+      J30 Sn;
+      j_zaddu<P>(Sn, D, S);  // Sn = (2m + 1) Q; D onto Sn's Z (never degenerate)
+      qtab_store(w.qtab, wave, m, lane, Sn);
+      j_copy(S, Sn);
+    }
+  }
+  // k = u2 (odd) or u2 + n, shifted so bit b sits at 288-bit position b + 30:
+  // window i's bits [5i+1, 5i+5] reach K[8] bits 25..29 after 50 - i shifts
+  uint32_t K[9];
+  {
+    const uint32_t add = (u2[0] & 1u) ? 0u : ~0u;
+    uint32_t k[9];
+    uint64_t cy = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      cy += (uint64_t)u2[q] + (Cv::n[q] & add);
+      k[q] = (uint32_t)cy;
+      cy >>= 32;
+    }
+    k[8] = (uint32_t)cy;
+    K[0] = k[0] << 30;
+#pragma unroll
+    for (int q = 1; q < 9; q++) K[q] = (k[q] << 30) | (k[q - 1] >> 2);
+  }
+  uint64_t gl[kLLTeeth];
+  ll_slices<P>(gl, u1);
+  uint32_t gx[9], gy[9], gidx;
+  bool gneg;
+  int gp = kLLSpace - kGF;  // the next folded G position (descending)
+  g2_column(gl, gp, gidx, gneg);
+  llaff_load(gx, gy, g2, gidx);
+  auto g_add = [&]() {
+    ll_madd<P>(A, a_inf, gx, gy, gneg, one);
+    if (gp > 0) {
+      gp = gp > kGF ? gp - kGF : 0;
+      g2_column(gl, gp, gidx, gneg);
+      llaff_load(gx, gy, g2, gidx);
+    }
+  };
+  qtab_load(A, w.qtab, wave, (K[8] >> 30) & 1u, lane);  // top digit 2 bit_256 + 1: Q or 3 Q
+  a_inf = false;
+#pragma unroll 1
+  for (int win = 50; win >= 0; win--) {
+    const uint32_t b = (K[8] >> 25) & 31u;
+#pragma unroll
+    for (int q = 8; q > 0; q--) K[q] = (K[q] << 5) | (K[q - 1] >> 27);
+    K[0] <<= 5;
+    const bool neg = b < 16u;
+    const uint32_t mag = neg ? 31u - 2u * b : 2u * b - 31u;
+    J30 T;
+    qtab_load(T, w.qtab, wave, (mag - 1u) >> 1, lane);  // issued before the doublings
+#pragma unroll 1
+    for (int d = 1; d <= 4; d++) {
+      j_dbl<P>(A, A);  // (while a_inf, A is a placeholder the next point replaces)
+      if (g_fold_pos(5 * win + 5 - d)) g_add();
+    }
+    if (neg) f_neg<P, 64>(T.Y, T.Y);
+    j_dbladd<P>(A, a_inf, T);
+    if (g_fold_pos(5 * win)) g_add();
+  }
+}
+
+// One-lane ladder records: P-256 through the odd-window ladder with u1 G
+// folded in; secp256k1 through the GLV ladder + the 13-bit G comb.
+template <class P>
+BH_HD bool stage_ladder_fold(const Work& w, const uint32_t* gtab, uint32_t i, uint32_t wave,
+                             uint32_t lane) {
+  if constexpr (P::a_is_minus3) {
+    J30 A;
+    bool a_inf;
+    q_ladder_odd_g<P>(A, a_inf, w, i, wave, lane, g2_of(gtab));
+    return finish_check<P>(w, i, A, a_inf, A, true);
+  } else {
+    return stage_ladder<P>(w, gtab, i, wave, lane);
+  }
+}
+
 template <class P>
 BH_HD bool stage_keycomb(const Work& w, const uint32_t* gtab, uint32_t i, const uint32_t* tab) {
   J30 A, B;

@@ -406,7 +406,7 @@ __device__ __forceinline__ void ktab_ladder_body(const Work& w, const Plan& pl, 
   const bool active = j0 < cnt;
   const uint32_t j = active ? j0 : cnt - 1;
   const uint32_t i = pl.ladder_list[j];
-  const bool ok = stage_ladder<P>(w, gtab, i, j0 >> 6, threadIdx.x & 63u);
+  const bool ok = stage_ladder_fold<P>(w, gtab, i, j0 >> 6, threadIdx.x & 63u);
   if (active) reason[i] = ok ? R_OK : R_MATH;
 }
 

@@ -81,7 +81,14 @@ MAC_PER_FP = 128
 G_COMB_BITS = 13
 G_WINDOWS = (257 + G_COMB_BITS - 1) // G_COMB_BITS
 LL_TABLES = os.environ.get("BH_LL", "1") != "0"
-FP_LADDER, FP_GPART = 3200, G_WINDOWS * 11
+# The P-256 ladder (round 5, verify.h q_ladder_odd_g): odd multiples Q..31 Q by
+# a co-Z chain (a DBLU ~9 + 15 ZADDU x 7), 51 windows of 4 doublings (8) + the
+# composite 2 A + T (16 + 7), 13 folded G additions (11), the x check (~7).
+# SURVEY 8(d)'s fixed schedule S0 prices any verify at 3,200 (s0_schedule_frac).
+FP_S0 = 3200
+FP_LADDER = 9 + 15 * 7 + 51 * (4 * 8 + 16 + 7) + ((-(-257 // 7) - 1) // int(
+    os.environ.get("BH_GFOLD", 3)) + 1) * 11 + 7
+FP_GPART = G_WINDOWS * 11
 LL_T = int(os.environ.get("BH_LL_T", 7))  # the comb shape the library was built with (verify.h)
 LL_S = -(-257 // LL_T)
 FP_INV_SG = 85
@@ -104,7 +111,7 @@ FOLD_G_ADDS = (LL_S - 1) // G_FOLD + 1
 # Each Horner step A = 2 A + V_j Q is (A + T) + A: a mixed addition that also
 # rescales A (8M + 3S) + a co-Z addition (5M + 2S) = 18 ops (verify.h ll_dbladd)
 FP_KEYCOMB = ((LL_S - 1) * 18 + FOLD_G_ADDS * 11 + 7) if LL_TABLES else 65 * 16 + 23
-MACS_PER_VERIFY = FP_LADDER * MAC_PER_FP
+MACS_PER_VERIFY = FP_S0 * MAC_PER_FP
 KERNELS = {"build_ladder_ms": "k_ktab_ladder", "keycomb_ms": "k_keycomb"}
 MAX_LANES = 4  # bdls_hip.cpp kMaxLanes
 
@@ -911,7 +918,7 @@ def bench_throughput(a, rank, world, local):
     out["roofline"]["whole_step"] = {
         "fp_ops_per_step": step_ops,
         "frac_of_peak": round(step_ops * MAC_PER_FP / step_s / peak, 4) if peak else None,
-        "s0_schedule_frac": round(rate * FP_LADDER * MAC_PER_FP / peak, 4) if peak else None,
+        "s0_schedule_frac": round(rate * FP_S0 * MAC_PER_FP / peak, 4) if peak else None,
         "note": "per GPU, HBM-resident step; s0_schedule_frac prices every verify at SURVEY "
                 "8(d)'s 3,200 F_p ops (schedule S0)"}
     src, counters, stale = load_counters(a.config, n)

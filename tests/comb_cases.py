@@ -294,3 +294,128 @@ def records_for_fold(curve, triples, seed: int = 23, low_s: bool = True):
         out.append((qx, qy, sig, e.to_bytes(32, "big"), 0))
         out.append((qx, qy, sig, (e ^ 1).to_bytes(32, "big"), 9))
     return out
+
+
+# ---- the variable-base ladder with u1 G folded in (round 5, verify.h q_ladder_odd_g) ----
+def ladder_digits(u2: int, n: int):
+    """Odd signed 5-bit windows of k = u2 (odd) or u2 + n: (top digit, [d_0 .. d_50])."""
+    k = u2 if u2 & 1 else u2 + n
+    d = [2 * ((k >> (5 * i + 1)) & 31) - 31 for i in range(51)]
+    top = 2 * ((k >> 256) & 1) + 1
+    assert (top << 255) + sum(x << (5 * i) for i, x in enumerate(d)) == k
+    return top, d
+
+
+def ladder_events(u1: int, u2: int, d: int, n: int, t: int = 7, s: int = 37, kgf: int = 3):
+    """q_ladder_odd_g on u1 G + u2 Q (Q = d G) as integers mod n, in the
+    kernel's order: A = top digit Q; per window 50 .. 0: 4 doublings, each
+    followed by the folded G group whose weight exponent equals the doublings
+    still to come (p = 0, 1, 1 + kgf, ..., s - kgf), then the composite
+    2 A + d_i Q (kind "Q": "dbl" A == T, "neg" A == -T, "inf" 2 A + T == 0)
+    and the G entry at p = 5 i. G additions: kind "G<p>" ("dbl" / "inf").
+    Returns ([(event, window, kind)], total is infinity)."""
+    top, dig = ladder_digits(u2, n)
+    W = comb_columns(u1, n, t, s)
+
+    def gpos(p):
+        return p == 0 or (1 <= p <= s - kgf and (p - 1) % kgf == 0)
+
+    def gval(p):
+        return W[0] if p == 0 else sum(W[p + c] << c for c in range(kgf))
+    ev, a, inf = [], top * d % n, False
+
+    def gadd(win, p):
+        nonlocal a, inf
+        T = gval(p) % n
+        if inf:
+            a, inf = T, False
+            ev.append(("from_inf", win, f"G{p}"))
+        elif (a - T) % n == 0:
+            ev.append(("dbl", win, f"G{p}"))
+            a = 2 * T % n
+        elif (a + T) % n == 0:
+            ev.append(("inf", win, f"G{p}"))
+            a, inf = 0, True
+        else:
+            a = (a + T) % n
+    for win in range(50, -1, -1):
+        for dd in range(1, 5):
+            if not inf:
+                a = 2 * a % n
+            if gpos(5 * win + 5 - dd):
+                gadd(win, 5 * win + 5 - dd)
+        T = dig[win] * d % n
+        if inf:
+            a, inf = T, False
+            ev.append(("from_inf", win, "Q"))
+        elif (a - T) % n == 0:
+            ev.append(("dbl", win, "Q"))
+            a = 3 * T % n
+        elif (a + T) % n == 0:
+            ev.append(("neg", win, "Q"))
+        elif (2 * a + T) % n == 0:
+            ev.append(("inf", win, "Q"))
+            a, inf = 0, True
+        else:
+            a = (2 * a + T) % n
+        if gpos(5 * win):
+            gadd(win, 5 * win)
+    assert (inf and (u1 + u2 * d) % n == 0) or (not inf and a == (u1 + u2 * d) % n)
+    return ev, inf
+
+
+def ladder_crafted(curve, seed: int = 19, tries: int = 20000, low_s: bool = False,
+                   kgf: int = 3, t: int = 7, s: int = 37):
+    """(u1, u2, d) triples whose folded ladder takes each degenerate branch
+    reachable by construction in the last window: the column-0 G entry
+    doubling / cancelling the sum, the composite of digit d_0 meeting A == T,
+    A == -T and 2 A + T == 0, the G groups at weight 2^1 and 2^(1 + kgf)
+    doubling / cancelling the partial sum. u1 is drawn, u2 solved from the
+    total u1 + u2 d each event needs, kept when u2's own d_0 is the digit
+    assumed (~1/32)."""
+    import random
+    n = curve.n
+    rng = random.Random(seed)
+    g4 = 1 + kgf
+    want = {("dbl", 0, "G0"), ("inf", 0, "G0"), ("dbl", 0, "Q"), ("neg", 0, "Q"),
+            ("inf", 0, "Q"), ("dbl", 0, "G1"), ("inf", 0, "G1"), ("dbl", 0, f"G{g4}"),
+            ("inf", 0, f"G{g4}")}
+    found, out = set(), []
+    for _ in range(tries):
+        if found == want:
+            break
+        d = rng.randrange(1, n)
+        u1 = rng.randrange(1, n)
+        W = comb_columns(u1, n, t, s)
+        G1 = sum(W[1 + c] << c for c in range(kgf))
+        G4 = sum(W[g4 + c] << c for c in range(kgf))
+        d0 = rng.choice([x for x in range(-31, 32, 2)])
+        sh = 2 ** (g4 - 1)  # doublings between the G4 and G1 additions, times 2
+        targets = {
+            ("dbl", 0, "G0"): 2 * W[0],
+            ("inf", 0, "G0"): 0,
+            ("dbl", 0, "Q"): 3 * d0 * d + W[0],
+            ("neg", 0, "Q"): -d0 * d + W[0],
+            ("inf", 0, "Q"): W[0],
+            ("dbl", 0, "G1"): 4 * G1 + d0 * d + W[0],
+            ("inf", 0, "G1"): d0 * d + W[0],
+            ("dbl", 0, f"G{g4}"): 2 * (2 * sh * G4 + G1) + d0 * d + W[0],
+            ("inf", 0, f"G{g4}"): 2 * G1 + d0 * d + W[0],
+        }
+        for key, total in targets.items():
+            if key in found:
+                continue
+            u2 = (total - u1) * pow(d, -1, n) % n
+            if not u2 or ladder_digits(u2, n)[1][0] != d0:
+                continue
+            ev, inf = ladder_events(u1, u2, d, n, t, s, kgf)
+            if key not in [e for e in ev if e[0] != "from_inf"][:1]:
+                continue
+            if low_s and not inf:
+                q = O.scalar_mult(curve, d, (curve.gx, curve.gy))
+                r = O.double_scalar(curve, u1, u2, q)[0] % n
+                if r == 0 or r * pow(u2, -1, n) % n > n // 2:
+                    continue
+            found.add(key)
+            out.append((u1, u2, d, key, inf))
+    return out

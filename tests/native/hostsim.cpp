@@ -183,7 +183,7 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
       j_acc<P>(C0, i0, C1, i1);
       ok = finish_check<P>(w, i, C0, i0, C0, true);
     } else {
-      ok = stage_ladder<P>(w, gtab, i, i / 64, i % 64);
+      ok = stage_ladder_fold<P>(w, gtab, i, i / 64, i % 64);
     }
     reason[i] = ok ? R_OK : R_MATH;
   }

@@ -210,3 +210,44 @@ def test_unique_keys_one_pass_of_4m(L):
         s = bytes(w.sig[w.sig_off[i]:w.sig_off[i] + w.sig_len[i]])
         dg = hashlib.sha256(bytes(w.msg[w.msg_off[i]:w.msg_off[i] + w.msg_len[i]])).digest()
         assert orc.csp_verify(q, s, dg) == w.reason[i], i
+
+
+def test_ladder_route_crafted_events_p256(L):
+    """Round 5: the one-lane P-256 ladder (verify.h q_ladder_odd_g: odd signed
+    windows, the composite 2 A + T, u1 G folded into the last doublings) on
+    records crafted so that its last window takes every degenerate branch
+    reachable by construction (tests/comb_cases.py ladder_crafted), in a
+    40,960-record batch of distinct keys (every record on the ladder): bitmap
+    and reasons equal the construction, the filler's against the C oracle."""
+    from tests.comb_cases import ladder_crafted
+    c = O.P256
+    kgf = int(os.environ.get("BH_GFOLD", 3))
+    recs, want = [], []
+    for seed in (43, 44, 45):
+        for qx, qy, sig, dg, exp in records_for_fold(
+                c, ladder_crafted(c, seed=seed, low_s=True, kgf=kgf), low_s=True):
+            recs.append((qx.to_bytes(32, "big") + qy.to_bytes(32, "big"), sig, dg))
+            want.append(exp)
+    assert len(recs) >= 3 * 9
+    fill = 40_960 - len(recs)
+    w = workload.generate(fill, fill, 64, 16, seed=49)  # distinct keys
+    for i in range(w.n):
+        m = bytes(w.msg[w.msg_off[i]:w.msg_off[i] + w.msg_len[i]])
+        recs.append((bytes(w.pub[64 * i:64 * i + 64]),
+                     bytes(w.sig[w.sig_off[i]:w.sig_off[i] + w.sig_len[i]]),
+                     hashlib.sha256(m).digest()))
+    want += [int(x) for x in w.reason]
+    want = np.array(want, np.uint8)
+    n = len(recs)
+    bits, reason, tm = _dev_verify(L, _pack(recs), n)
+    bad = np.nonzero(reason != want)[0]
+    assert not len(bad), [(int(i), int(reason[i]), int(want[i])) for i in bad[:10]]
+    assert (bits == (want == 0)).all()
+    # (a crafted key that took several events has >= 4 records: a key table)
+    math = int(((want == 0) | (want == 9)).sum())
+    assert tm.wide == 1 and tm.n_ladder + tm.n_keycomb == math
+    assert tm.n_ladder >= math - (n - w.n)
+    base = n - w.n
+    for i in np.random.default_rng(5).choice(w.n, 100, replace=False):
+        q, s, dg = recs[base + i]
+        assert orc.csp_verify(q, s, dg) == want[base + i]

@@ -363,3 +363,39 @@ def test_hostsim_folded_g_crafted_events(hs, curve):
     finally:
         hs.hs_set_ll(0)
     assert [int(o) for o in out] == [r[4] for r in recs]
+
+
+def test_hostsim_ladder_folded_crafted_events(hs):
+    """Round 5: the P-256 variable-base ladder (odd signed 5-bit windows, the
+    composite 2 A + T, u1 G folded into its last doublings: verify.h
+    q_ladder_odd_g). Records crafted (tests/comb_cases.py ladder_crafted) so
+    that its last window takes every degenerate branch reachable by
+    construction -- the column-0 G entry and the G groups at weight 2^1 and
+    2^(1 + kGF) doubling / cancelling the running sum, the composite meeting
+    A == T, A == -T and 2 A + T == 0 -- plus a total at infinity, with every
+    record on the ladder (no key tables): verdicts equal the construction."""
+    from oracle import ecdsa_ref as O
+    from tests.comb_cases import ladder_crafted, ladder_events, records_for_fold
+    c = O.P256
+    kgf = hs.hs_gfold()
+    triples = ladder_crafted(c, seed=41, kgf=kgf)
+    assert len({x[3] for x in triples}) == 9
+    for u1, u2, d, key, _ in triples:
+        assert key in ladder_events(u1, u2, d, c.n, kgf=kgf)[0]
+    recs = records_for_fold(c, triples, low_s=False)
+    pub = np.frombuffer(b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big")
+                                 for x, y, _, _, _ in recs), np.uint8)
+    sigs, dgs = [r[2] for r in recs], [r[3] for r in recs]
+    sl = np.array([len(x) for x in sigs], np.uint32)
+    dl = np.array([len(x) for x in dgs], np.uint32)
+    so = np.concatenate([[0], np.cumsum(sl[:-1])]).astype(np.uint64)
+    do = np.concatenate([[0], np.cumsum(dl[:-1])]).astype(np.uint64)
+    sig = np.frombuffer(b"".join(sigs), np.uint8)
+    dg = np.frombuffer(b"".join(dgs), np.uint8)
+    out = np.zeros(len(recs), np.uint8)
+    ncomb = ctypes.c_uint32()
+    hs.hs_verify2(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
+                  dg.ctypes.data, do.ctypes.data, dl.ctypes.data, len(recs), 2, 4, 1000,
+                  out.ctypes.data, ctypes.byref(ncomb))
+    assert ncomb.value == 0
+    assert [int(o) for o in out] == [r[4] for r in recs]
