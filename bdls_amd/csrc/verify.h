@@ -1069,9 +1069,27 @@ BH_HD void ktab_build(uint32_t* tab, const Work& w, uint32_t rec) {
   }
 }
 
+// Registry slots (round 5) also hold the 4-bit windows AFFINE at kRegWin
+// (built below, after the comb layout); aff selects that form.
+BH_HD uint32_t reg_win_offset();
+BH_HD void llaff_load(uint32_t x[9], uint32_t y[9], const uint32_t* tab, uint32_t b);
+template <class P>
+BH_HD void win_entry(J30& T, const uint32_t* tab, uint32_t win, uint32_t j, bool aff,
+                     const uint32_t one[9]) {
+  if (aff) {
+    llaff_load(T.X, T.Y, tab + reg_win_offset(), win * (uint32_t)kKEnt + j);
+    f_copy(T.Z, one);
+  } else {
+    ktab_load(T, tab, win, j);
+  }
+}
+
 // u2 Q from a key table: kKW-bit signed windows (least significant first).
 template <class P>
-BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab) {
+BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint32_t* tab,
+                     bool aff = false) {
+  uint32_t one[9];
+  f_const(one, P::r1);
   uint32_t k2[8];
   ld8(k2, w.r, i, w.ns);
   a_inf = true;
@@ -1090,11 +1108,12 @@ BH_HD void q_keycomb(J30& A, bool& a_inf, const Work& w, uint32_t i, const uint3
     const uint32_t mag = neg ? 16u - t : t;
     carry = neg ? 1u : 0u;
     J30 T;
-    ktab_load(T, tab, win, mag ? mag - 1 : 0);
+    win_entry<P>(T, tab, win, mag ? mag - 1 : 0, aff, one);
     if (neg) f_neg<P, 64>(T.Y, T.Y);
     J30 R;
     bool same;
-    const bool deg = j_add<P>(R, A, T, &same);
+    // (affine entries: a mixed addition, 11 F_p ops instead of 16)
+    const bool deg = aff ? j_madd<P>(R, A, T.X, T.Y, &same) : j_add<P>(R, A, T, &same);
     const bool take = mag != 0;
     const bool use_t = take && a_inf;
     const bool use_r = take && !a_inf && !deg;
@@ -1413,6 +1432,98 @@ BH_HD void lltab_build(uint32_t* tab, const Work& w, uint32_t rec) {
     f_sub<P, 32>(y, y, ly);                  // [b34]
     llaff_store(tab, m, x, y);
   }
+}
+
+// ---- registry slots (round 5) ---------------------------------------------------
+// A key kept in the device registry (bh_keys_register, BH_F_KEEP_KEYS) pays
+// one build and is used for as long as it lives, so its slot holds BOTH forms
+// a batch may need: the signed comb of one-lane batches (lltab_build's layout
+// at offset 0: k_keycomb's folded Horner, 798 F_p ops per use instead of the
+// windows' 1,040 + the 13-bit G comb's 220 + a final addition) and the 4-bit
+// windows made AFFINE (kRegWin: 65 x 8 entries in the 80-byte llaff layout)
+// for the multi-lane kernels of small batches, which split the windows over
+// their lanes (a comb's doubling chain cannot be split): mixed additions, 11
+// F_p ops per window instead of 16. Per-batch tables keep one form each.
+constexpr uint32_t kRegWin = (kLLPre + 12u * kLLEnt + 3u) & ~3u;
+constexpr uint32_t kRegWinRaw = kRegWin + (uint32_t)kKWin * kKEnt * kLLAff;
+constexpr uint32_t kRegWinPre = kRegWinRaw + 28u * kKEnt;
+static_assert(kRegWinPre + 12u * kKEnt <= kKTabWords && kRegWin % 4 == 0, "registry slot layout");
+BH_HD uint32_t reg_win_offset() { return kRegWin; }
+
+BH_HD void z_store(uint32_t* p, const uint32_t z[9]) {
+  W4* d = reinterpret_cast<W4*>(p);
+  d[0] = W4{z[0], z[1], z[2], z[3]};
+  d[1] = W4{z[4], z[5], z[6], z[7]};
+  d[2] = W4{z[8], 0u, 0u, 0u};
+}
+BH_HD void z_load(uint32_t z[9], const uint32_t* p) {
+  const W4* s = reinterpret_cast<const W4*>(p);
+  const W4 a = s[0], b = s[1], c = s[2];
+  z[0] = a.x; z[1] = a.y; z[2] = a.z; z[3] = a.w;
+  z[4] = b.x; z[5] = b.y; z[6] = b.z; z[7] = b.w;
+  z[8] = c.x;
+}
+
+// The affine 4-bit windows of a registry slot: per window the co-Z chain of
+// ktab_build (1 B .. 8 B, Jacobian, each on its own Z) into 8 raw scratch
+// slots with the running product of their Z, one inversion, and a backward
+// pass storing the affine entries -- ~140 F_p ops per window on top of the
+// chain's 58. Never degenerate (ktab_build).
+template <class P>
+BH_HD void ktab_build_aff(uint32_t* tab, const Work& w, uint32_t rec) {
+  uint32_t* raw = tab + kRegWinRaw;
+  uint32_t* pre = tab + kRegWinPre;
+  J30 B, Bz, S;
+  ld9(B.X, w.qx, rec, w.ns);
+  ld9(B.Y, w.qy, rec, w.ns);
+  f_const(B.Z, P::r1);
+#pragma unroll 1
+  for (uint32_t win = 0; win < (uint32_t)kKWin; win++) {
+    uint32_t z[9];
+    ktab_store(raw, 0, 0, B);                 // 1 B
+    f_copy(z, B.Z);
+    z_store(pre, z);
+    j_dblu<P>(S, Bz, B);                      // S = 2B, Bz = B on S's Z
+    ktab_store(raw, 0, 1, S);
+    f_mul<P>(z, z, S.Z);
+    z_store(pre + 12, z);
+#pragma unroll 1
+    for (uint32_t j = 2; j < (uint32_t)kKEnt; j++) {
+      J30 T;
+      j_zaddu<P>(T, Bz, S);                   // T = (j+1) B; Bz onto T's Z
+      ktab_store(raw, 0, j, T);
+      f_mul<P>(z, z, T.Z);
+      z_store(pre + 12 * j, z);
+      j_copy(S, T);
+    }
+    j_dbl<P>(B, S);                           // 16 B: the next window's base
+    uint32_t inv[9];
+    f_inv_sg<P>(inv, z);
+#pragma unroll 1
+    for (uint32_t j = (uint32_t)kKEnt; j-- > 0;) {
+      J30 E;
+      ktab_load(E, raw, 0, j);
+      uint32_t zi[9], x[9], y[9];
+      if (j > 0) {
+        uint32_t pz[9];
+        z_load(pz, pre + 12 * (j - 1));
+        f_mul<P>(zi, inv, pz);
+        f_mul<P>(inv, inv, E.Z);
+      } else {
+        f_copy(zi, inv);
+      }
+      ll_to_affine<P>(x, y, E, zi);
+      llaff_store(tab + kRegWin, win * (uint32_t)kKEnt + j, x, y);
+    }
+  }
+}
+
+// A registry slot: the comb, then the affine windows (one lane, ~16.8k F_p
+// ops once per key).
+template <class P>
+BH_HD void reg_build(uint32_t* tab, const Work& w, uint32_t rec) {
+  lltab_build<P>(tab, w, rec);
+  ktab_build_aff<P>(tab, w, rec);
 }
 
 // Curve constants of a base-field class (the order n for u2 + n).
@@ -1911,10 +2022,11 @@ BH_HD bool stage_ladder_fold(const Work& w, const uint32_t* gtab, uint32_t i, ui
 }
 
 template <class P>
-BH_HD bool stage_keycomb(const Work& w, const uint32_t* gtab, uint32_t i, const uint32_t* tab) {
+BH_HD bool stage_keycomb(const Work& w, const uint32_t* gtab, uint32_t i, const uint32_t* tab,
+                         bool aff = false) {
   J30 A, B;
   bool a_inf, b_inf;
-  q_keycomb<P>(A, a_inf, w, i, tab);
+  q_keycomb<P>(A, a_inf, w, i, tab, aff);
   uint32_t u1[8];
   ld8(u1, w.e, i, w.ns);
   g_comb<P>(B, b_inf, gtab, u1);
@@ -1946,11 +2058,11 @@ BH_HD void stage_gpart(const Work& w, const uint32_t* gtab, uint32_t i, uint32_t
 
 template <class P>
 BH_HD bool stage_keycomb_q(const Work& w, uint32_t i, uint32_t j, const uint32_t* tab,
-                           bool ll = false, uint32_t stride = 0) {
+                           bool ll = false, uint32_t stride = 0, bool aff = false) {
   J30 A, B;
   bool a_inf;
   if (ll) q_llcomb<P>(A, a_inf, w, i, tab, stride);  // a per-batch Lim-Lee comb table
-  else q_keycomb<P>(A, a_inf, w, i, tab);
+  else q_keycomb<P>(A, a_inf, w, i, tab, aff);
   const uint32_t* o = w.gpart + j;
 #pragma unroll
   for (int k = 0; k < 9; k++) {
@@ -2145,8 +2257,9 @@ BH_HD void g_comb_part(J30& C, bool& c_inf, const uint32_t* gtab, const uint32_t
 // Lane l's u2 Q windows (win = l, l + L, ...) of the key table.
 template <class P, int L>
 BH_HD void keycomb_q_part(J30& C, bool& c_inf, const Work& w, uint32_t i, const uint32_t* tab,
-                          uint32_t l) {
-  uint32_t k[8], v[9], sv[9];
+                          uint32_t l, bool aff = false) {
+  uint32_t k[8], v[9], sv[9], one[9];
+  f_const(one, P::r1);
   f_const(C.X, P::r1);
   f_const(C.Y, P::r1);
   f_const(C.Z, P::r1);
@@ -2161,9 +2274,10 @@ BH_HD void keycomb_q_part(J30& C, bool& c_inf, const Work& w, uint32_t i, const 
     if (win < (uint32_t)kKWin) {
       const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
       J30 T;
-      ktab_load(T, tab, win, mag ? mag - 1 : 0);
+      win_entry<P>(T, tab, win, mag ? mag - 1 : 0, aff, one);
       if (d < 0) f_neg<P, 64>(T.Y, T.Y);
-      j_acc<P>(C, c_inf, T, mag == 0);
+      if (aff) j_acc_aff<P>(C, c_inf, T.X, T.Y, one, mag == 0);  // mixed: 11 F_p ops
+      else j_acc<P>(C, c_inf, T, mag == 0);
     }
   }
 }
@@ -2172,8 +2286,8 @@ BH_HD void keycomb_q_part(J30& C, bool& c_inf, const Work& w, uint32_t i, const 
 // + G-comb digit points).
 template <class P, int L>
 BH_HD void keycomb_part(J30& C, bool& c_inf, const Work& w, const uint32_t* gtab, uint32_t i,
-                        const uint32_t* tab, uint32_t l) {
-  keycomb_q_part<P, L>(C, c_inf, w, i, tab, l);  // u2 Q: 4-bit windows win = l + m L
+                        const uint32_t* tab, uint32_t l, bool aff = false) {
+  keycomb_q_part<P, L>(C, c_inf, w, i, tab, l, aff);  // u2 Q: 4-bit windows win = l + m L
   uint32_t k[8];
   ld8(k, w.e, i, w.ns);
   g_comb_part<P, L>(C, c_inf, gtab, k, l);        // u1 G: kGW-bit windows win = l + m L

@@ -391,11 +391,13 @@ __device__ __forceinline__ void ktab_ladder_body(const Work& w, const Plan& pl, 
     const uint32_t base = blockIdx.x * kBuildPerBlock;
     const uint32_t t = base + threadIdx.x;
     if (t < nt) {
-      // per-batch tables of one-lane-per-record batches are Lim-Lee combs;
-      // registry tables (and small batches') keep the 4-bit windows
+      // per-batch tables of one-lane-per-record batches are Lim-Lee combs,
+      // small batches' 4-bit windows; registry slots get both forms (verify.h
+      // reg_build: the comb + affine windows)
       const uint32_t id = pl.tab_dst[t];
       uint32_t* tab = const_cast<uint32_t*>(tab_ptr(pl, g, id));
-      if (ll && (id & kLocal)) lltab_build<P>(tab, w, pl.tab_rec[t]);
+      if (!(id & kLocal)) reg_build<P>(tab, w, pl.tab_rec[t]);
+      else if (ll) lltab_build<P>(tab, w, pl.tab_rec[t]);
       else ktab_build<P>(tab, w, pl.tab_rec[t]);
     }
     return;
@@ -583,7 +585,9 @@ __global__ __launch_bounds__(256) BH_KEYCOMB_ATTR void k_keycomb(Work w, Plan pl
     if (j >= cnt) return;
     const uint32_t i = pl.comb_order[j];
     const uint32_t id = pl.rec_tab[i];
-    const bool ok = stage_keycomb_q<P>(w, i, j, tab_ptr(pl, g, id), ll && (id & kLocal));
+    const bool ok = ll ? stage_keycomb_fold<P>(w, i, tab_ptr(pl, g, id), kLLAff, g2_of(gtab))
+                       : stage_keycomb_q<P>(w, i, j, tab_ptr(pl, g, id), false, 0u,
+                                            !(id & kLocal));  // registry: affine windows
     reason[i] = ok ? R_OK : R_MATH;
     return;
   }
@@ -599,7 +603,9 @@ __global__ __launch_bounds__(256) BH_KEYCOMB_ATTR void k_keycomb(Work w, Plan pl
     i = pl.comb_order[j];
     id = pl.rec_tab[i];
   }
-  const bool lcl = have && (id & kLocal);  // a per-batch comb table
+  // every table of a one-lane comb batch has a comb (per-batch tables are
+  // combs, registry slots carry one at offset 0): all are staged by runs
+  const bool lcl = have && id != kNone;
   s_id[t] = lcl ? id : kNone;
   __syncthreads();
   // runs of equal ids -> slots: inclusive count of run starts up to this lane
@@ -631,10 +637,9 @@ __global__ __launch_bounds__(256) BH_KEYCOMB_ATTR void k_keycomb(Work w, Plan pl
   if (!have) return;
   const bool in_lds = lcl && slot < kLdsTabs;
   const uint32_t* tab = in_lds ? s_tab + slot * kLdsTabWords : tab_ptr(pl, g, id);
-  // per-batch comb tables: u1 G folded into the Horner (round 5, verify.h
-  // q_llcomb_g); registry (windowed) tables: their windows + the 13-bit G comb
-  const bool ok = lcl ? stage_keycomb_fold<P>(w, i, tab, in_lds ? kLLLds : kLLAff, g2_of(gtab))
-                      : stage_keycomb<P>(w, gtab, i, tab);
+  // the key's comb (per-batch or registry slot) with u1 G folded into the
+  // Horner (round 5, verify.h q_llcomb_g)
+  const bool ok = stage_keycomb_fold<P>(w, i, tab, in_lds ? kLLLds : kLLAff, g2_of(gtab));
   reason[i] = ok ? R_OK : R_MATH;
 }
 
@@ -649,9 +654,11 @@ __global__ __launch_bounds__(256) void k_keycomb_wide(Work w, Plan pl, KeyReg g,
   const uint32_t cnt = pl.counters[0];
   if (j >= cnt) return;  // whole groups exit together
   const uint32_t i = pl.comb_order[j];
+  const uint32_t id = pl.rec_tab[i];
   J30 C;
   bool c_inf;
-  keycomb_part<P, L>(C, c_inf, w, gtab, i, tab_ptr(pl, g, pl.rec_tab[i]), l);
+  // registry slots: their affine windows (mixed additions)
+  keycomb_part<P, L>(C, c_inf, w, gtab, i, tab_ptr(pl, g, id), l, !(id & kLocal));
   group_sum<P, L>(C, c_inf);
   if (l == 0) reason[i] = finish_check<P>(w, i, C, c_inf, C, true) ? R_OK : R_MATH;
 }
@@ -667,9 +674,10 @@ __global__ __launch_bounds__(256) void k_keycomb_wide_q(Work w, Plan pl, KeyReg 
   const uint32_t cnt = pl.counters[0];
   if (j >= cnt) return;
   const uint32_t i = pl.comb_order[j];
+  const uint32_t id = pl.rec_tab[i];
   J30 C;
   bool c_inf;
-  keycomb_q_part<P, L>(C, c_inf, w, i, tab_ptr(pl, g, pl.rec_tab[i]), l);
+  keycomb_q_part<P, L>(C, c_inf, w, i, tab_ptr(pl, g, id), l, !(id & kLocal));
   part_store(w, pbase + gid, pstride, C, c_inf);
 }
 
@@ -742,7 +750,7 @@ __global__ __launch_bounds__(256) void k_small(BatchIn in, Work w, KeyReg g,
   }
   J30 C;
   bool c_inf;
-  keycomb_part<P, kSmallL>(C, c_inf, w, gtab, j, g.tables + (size_t)t * kKTabWords, l);
+  keycomb_part<P, kSmallL>(C, c_inf, w, gtab, j, g.tables + (size_t)t * kKTabWords, l, true);
   group_sum<P, kSmallL>(C, c_inf);
   if (l == 0) reason[j] = finish_check<P>(w, j, C, c_inf, C, true) ? R_OK : R_MATH;
 }

