@@ -57,14 +57,13 @@ def phase(msg: str) -> None:
     sys.stderr.flush()
 
 # Algorithmic work per verify in SURVEY.md 8(d) units: F_p mul/sqr x 128 u32
-# MACs (64 product + 64 reduction). The variable-base ladder is schedule S0
-# (3.2e3 F_p ops = 4.1e5 MACs). The per-key comb path is split over two
-# kernels: k_ktab_ladder builds the key tables and, beside them, the u1 G half
-# of every key-comb record (G_WINDOWS mixed adds of 11 ops over the 10-bit G
-# comb: BH_GCOMB_BITS in verify.h); k_keycomb adds the key-table part and the
-# stored u1 G and checks x (~23 ops). Per-batch tables of large batches are
-# signed Lim-Lee combs (round 4, verify.h lltab_build; BH_LL=0: 4-bit windows)
-# with LL_T teeth spaced LL_S bits (BH_LL_T, 7 x 37), 2^(LL_T-1) entries:
+# MACs (64 product + 64 reduction). SURVEY's fixed schedule S0 prices any
+# verify at 3.2e3 F_p ops (4.1e5 MACs). The per-key comb path is split over two
+# kernels: k_ktab_ladder builds the key tables (and runs the ladder records),
+# k_keycomb walks each record's comb with u1 G folded into the same doublings
+# and checks x. Per-batch tables of large batches are signed Lim-Lee combs
+# (verify.h lltab_build; BH_LL=0: 4-bit windows) with LL_T teeth spaced LL_S
+# bits (BH_LL_T, 7 x 37), 2^(LL_T-1) entries:
 #   build (round 5, verify.h lltab_build): (LL_T-1) LL_S doublings (8 ops);
 #     the 2 (LL_T-1) chain points made affine (prefix products + 6 per point +
 #     an inversion); L over a = (LL_T-1)//2 low digits and H over the rest by
@@ -73,10 +72,11 @@ def phase(msg: str) -> None:
 #     affine (6 per point + an inversion); each entry E = H + L one affine
 #     addition whose denominators share an inversion (6 per entry); three
 #     safegcd inversions (~14k VALU instructions each, ~85 F_p-op equivalents)
-#   comb: LL_S - 1 doublings + LL_S - 1 mixed additions per record (the top
-#     column is loaded, every column is nonzero)
+#   comb: LL_S - 1 composite steps 2A + T per record (the top column is
+#     loaded, every column is nonzero) + the folded G groups (below)
 # windows: build 65 x 58 = 3,770 per table (co-Z chain), comb 65 additions
-# (16 ops: the tables are Jacobian) = 1,040 per record.
+# (16 ops: the tables are Jacobian) = 1,040 per record + the 13-bit G comb
+# (G_WINDOWS mixed additions, computed beside the builds: FP_GPART).
 MAC_PER_FP = 128
 G_COMB_BITS = 13
 G_WINDOWS = (257 + G_COMB_BITS - 1) // G_COMB_BITS
