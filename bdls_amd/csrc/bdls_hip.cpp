@@ -44,6 +44,7 @@ hipError_t launch_small(int curve, const BatchIn& in, const Work& w, const KeyRe
 hipError_t launch_register(int curve, const uint8_t* pub, const Work& w, const Plan& pl,
                            const KeyReg& g, uint32_t n, uint8_t* status, hipStream_t s);
 size_t expand_temp_bytes(uint32_t m);
+hipError_t launch_result_out(const void* src, void* host_dst, size_t bytes, hipStream_t s);
 hipError_t launch_expand(const uint8_t* keys, const uint32_t* key_idx, uint8_t* pub,
                          const uint32_t* sig_len, uint64_t* sig_off, const uint32_t* msg_len,
                          uint64_t* msg_off, uint32_t* msg_len_out, uint32_t stride, void* temp,
@@ -142,11 +143,12 @@ struct Registry {
 struct HostBuf {
   void* p = nullptr;
   size_t cap = 0;
+  unsigned flags = hipHostMallocPortable;
   int ensure(size_t bytes) {
     if (bytes <= cap) return BH_OK;
     release();
     const size_t want = std::max<size_t>(bytes, 4096);
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocPortable);
+    hipError_t e = hipHostMalloc(&p, want, flags);
     if (e != hipSuccess) {
       p = nullptr;
       return fail(BH_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
@@ -161,7 +163,7 @@ struct HostBuf {
   }
 };
 
-// One of the host-API pipeline slots of a device (triple-buffered): its own
+// One of the host-API pipeline slots of a device (four-deep): its own
 // device staging for the inputs, device and pinned-host buffers for the
 // outputs, and the events that order upload -> verify -> download. While the
 // compute stream verifies one slot's batch, the copy stream uploads the next.
@@ -169,12 +171,17 @@ struct Slot {
   HostBuf host_in;  // latency path: the small batch packed on the host
   DevBuf stage;     // inputs (H2D on the copy stream)
   DevBuf out;       // bitmap words + reasons (device)
-  HostBuf host_out; // bitmap words + reasons (pinned, D2H on the compute stream)
+  // bitmap words + reasons (pinned, coherent: written by the compute stream's
+  // k_result_out, read by the host after the slot's done event)
+  HostBuf host_out{nullptr, 0, hipHostMallocPortable | hipHostMallocCoherent};
   hipEvent_t uploaded = nullptr, done = nullptr;
   bh_job* owner = nullptr;  // job whose results are in flight / sit in host_out
   size_t owner_part = 0;
 };
-constexpr int kSlots = 3;  // up to 3 host batches in flight per device
+// up to 4 host batches in flight per device: batch k + 4's upload is queued when
+// batch k is collected, so the copy engine has three uploads of runway while a
+// pass computes (3 slots left it idle ~0.3 ms per batch at config 2)
+constexpr int kSlots = 4;
 
 // The extra compute lanes of a device (round 3: one; round 4: up to
 // kMaxLanes - 1). Host-API batches rotate over lane 0 (Dev::stream / aux / ws)
@@ -923,9 +930,16 @@ int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, 
   uint64_t* dbm = (uint64_t*)sl.out.p;
   uint8_t* drs = (uint8_t*)(dbm + round64(m) / 64);
   if ((rc = run_dev(d, curve, dev_batch(db), m, flags, dbm, drs, s, nullptr, lane))) return rc;
-  HIPCHK(hipMemcpyAsync(sl.host_out.p, dbm, round64(m) / 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync((uint8_t*)sl.host_out.p + round64(m) / 8, drs, m,
-                        hipMemcpyDeviceToHost, s));
+  // results: words then reasons, contiguous on both sides. A kernel, not a
+  // D2H copy: a copy-engine command that waits on this pass would hold the
+  // engine's later commands -- the next batches' uploads -- until the pass
+  // ends (measured: batch k+1's upload started only after batch k's D2H)
+  (void)drs;
+  if (getenv("BH_D2H_COPY")) {
+    HIPCHK(hipMemcpyAsync(sl.host_out.p, dbm, round64(m) / 8 + m, hipMemcpyDeviceToHost, s));
+  } else {
+    HIPCHK(bh::launch_result_out(dbm, sl.host_out.p, round64(m) / 8 + m, s));
+  }
   HIPCHK(hipEventRecord(sl.done, s));
   sl.owner = j;
   sl.owner_part = j->parts.size();

@@ -888,6 +888,29 @@ hipError_t launch_expand(const uint8_t* keys, const uint32_t* key_idx, uint8_t* 
   return hipGetLastError();
 }
 
+// Results to page-locked host memory by the compute stream's own kernel: a
+// device-to-host copy engine command that waits on a pass holds every later
+// command of its engine ring, uploads of the next batches included
+// (bdls_hip.cpp enqueue_part). Both pointers 16-byte aligned.
+__global__ __launch_bounds__(256) void k_result_out(const uint4* __restrict__ src,
+                                                    uint4* __restrict__ dst, size_t n16,
+                                                    const uint8_t* __restrict__ src_b,
+                                                    uint8_t* __restrict__ dst_b, size_t nb) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t k = i; k < n16; k += stride) dst[k] = src[k];
+  for (size_t k = n16 * 16 + i; k < nb; k += stride) dst_b[k] = src_b[k];
+}
+
+hipError_t launch_result_out(const void* src, void* host_dst, size_t bytes, hipStream_t s) {
+  if (!bytes) return hipSuccess;
+  const size_t n16 = bytes / 16;
+  const uint32_t blocks = (uint32_t)std::min<size_t>(1024, (n16 + 255) / 256 + 1);
+  hipLaunchKernelGGL(k_result_out, dim3(blocks), dim3(256), 0, s, (const uint4*)src,
+                     (uint4*)host_dst, n16, (const uint8_t*)src, (uint8_t*)host_dst, bytes);
+  return hipGetLastError();
+}
+
 hipError_t launch_gtab_build(int curve, uint32_t* gtab, hipStream_t s) {
   const int nt = kCombWindows * kCombEntries + (int)kGBase, nt2 = (int)(kG2Ent + kG1Ent);
   if (curve == 0) {

@@ -674,7 +674,8 @@ def bench_throughput(a, rank, world, local):
                                         w.msg_len, alloc=alloc)
         layout_s = time.time() - t
         phase(f"compact layout built in {layout_s:.2f} s")
-    depth = 3  # batches in flight (the library keeps 3 pipeline slots per device)
+    # batches in flight (the library keeps 4 pipeline slots per device)
+    depth = int(os.environ.get("BENCH_HOST_DEPTH", "4"))
     outs = [(np.zeros((n + 7) // 8, np.uint8), np.zeros(n, np.uint8)) for _ in range(depth)]
     multipass = n > (1 << 22)
 

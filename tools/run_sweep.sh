@@ -11,7 +11,7 @@ for pass in $(seq ${PASSES:-1}); do
     e=$(echo "$envs" | tr '+' ' ')
     [ -n "$lib" ] && e="$e BDLS_HIP_LIB=$PWD/exp/libbdlship_$lib.so"
     env $e timeout -k 10 300 python bench.py --steps ${STEPS_N:-20} --warmup 5 --cpu-baseline 0 --side-configs 0 > gpurun_out/sweep/${name}_p$pass.json 2> gpurun_out/sweep/${name}_p$pass.err; rc=$?
-    echo "$name p$pass rc=$rc $(python3 -c "import json;d=json.load(open('gpurun_out/sweep/${name}_p$pass.json'));print(round(d['value']/1e6,1), d['parity'])" 2>/dev/null)"
+    echo "$name p$pass rc=$rc $(python3 -c "import json;d=json.load(open('gpurun_out/sweep/${name}_p$pass.json'));h=d.get('host_path') or {};print(round(d['value']/1e6,1), d['parity'], 'host', round(h.get('value',0)/1e6,1), h.get('pcie_frac'))" 2>/dev/null)"
     case $rc in 0|3) ;; *) echo "STOP"; exit $rc ;; esac
   done
 done
