@@ -1018,10 +1018,16 @@ int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, si
   const int lane = lanes() > 1 ? (int)(d.next_lane++ % lanes()) : 0;
   const LaneRef L = lane_ref(d, lane);
   hipStream_t s = L.stream;
+  // The upload waits on nothing (the slot's staging is free: its previous
+  // owner was collected above), so it goes to the copy stream; the kernel
+  // waits for it, the lane's last pass and the last registry write. A
+  // copy-engine command carrying a wait holds its engine's later commands.
+  char* dv = (char*)sl.stage.p;
+  HIPCHK(hipMemcpyAsync(dv, h, total, hipMemcpyHostToDevice, d.copy));
+  HIPCHK(hipEventRecord(sl.uploaded, d.copy));
+  HIPCHK(hipStreamWaitEvent(s, sl.uploaded, 0));
   if (*L.done_recorded) HIPCHK(hipStreamWaitEvent(s, L.done, 0));
   if (d.reg_written_recorded) HIPCHK(hipStreamWaitEvent(s, d.reg_written, 0));
-  char* dv = (char*)sl.stage.p;
-  HIPCHK(hipMemcpyAsync(dv, h, total, hipMemcpyHostToDevice, s));
   bh::Work w;
   bh::Plan pl;
   if ((rc = carve_work(d, m, &w, &pl, false, L.ws))) return rc;
@@ -1034,7 +1040,11 @@ int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, si
   g_dev_records.fetch_add(m, std::memory_order_relaxed);
   HIPCHK(bh::launch_small(curve, in, w, d.reg[curve].g, d.gtab[curve], (uint32_t)m,
                           (uint8_t*)sl.out.p, s, small_block));
-  HIPCHK(hipMemcpyAsync(sl.host_out.p, sl.out.p, m, hipMemcpyDeviceToHost, s));
+  if (getenv("BH_D2H_COPY")) {
+    HIPCHK(hipMemcpyAsync(sl.host_out.p, sl.out.p, m, hipMemcpyDeviceToHost, s));
+  } else {
+    HIPCHK(bh::launch_result_out(sl.out.p, sl.host_out.p, m, s));
+  }
   HIPCHK(hipEventRecord(sl.done, s));
   HIPCHK(hipEventRecord(L.done, s));
   *L.done_recorded = true;

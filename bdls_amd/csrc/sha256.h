@@ -25,34 +25,61 @@ static const uint32_t kSha256K[64] = {
 
 BH_HD uint32_t rotr32(uint32_t x, uint32_t n) { return (x >> n) | (x << (32 - n)); }
 
+// The round's operations in the forms CDNA4 issues in one instruction each:
+// a rotation is v_alignbit_b32, a three-way xor one v_bitop3_b32 (truth table
+// 0x96; the compiler forms bitop3 for Ch / Maj but not for these sums), Ch a
+// v_bfi_b32. Host builds (the CPU harness) take the plain expressions.
+BH_HD uint32_t sha_rotr(uint32_t x, uint32_t n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(x, x, n);
+#else
+  return rotr32(x, n);
+#endif
+}
+BH_HD uint32_t sha_xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+#else
+  return a ^ b ^ c;
+#endif
+}
+
+// one round; wk = W[t] + K[t]
+BH_HD void sha256_round(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
+                        uint32_t& f, uint32_t& g, uint32_t& hh, uint32_t wk) {
+  const uint32_t S1 = sha_xor3(sha_rotr(e, 6), sha_rotr(e, 11), sha_rotr(e, 25));
+  const uint32_t ch = g ^ (e & (f ^ g));
+  const uint32_t t1 = (hh + wk) + S1 + ch;
+  const uint32_t S0 = sha_xor3(sha_rotr(a, 2), sha_rotr(a, 13), sha_rotr(a, 22));
+  const uint32_t mj = (a & b) | (c & (a | b));
+  hh = g;
+  g = f;
+  f = e;
+  e = d + t1;
+  d = c;
+  c = b;
+  b = a;
+  a = t1 + S0 + mj;
+}
+
+// schedule word t >= 16 into the 16-word ring
+BH_HD uint32_t sha256_sched(uint32_t w[16], int i) {
+  const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+  const uint32_t s0 = sha_xor3(sha_rotr(w15, 7), sha_rotr(w15, 18), w15 >> 3);
+  const uint32_t s1 = sha_xor3(sha_rotr(w2, 17), sha_rotr(w2, 19), w2 >> 10);
+  const uint32_t wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+  w[i & 15] = wi;
+  return wi;
+}
+
 BH_HD void sha256_block(uint32_t h[8], uint32_t w[16]) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
 #pragma unroll
   for (int i = 0; i < 64; i++) {
-    uint32_t wi;
-    if (i < 16) {
-      wi = w[i];
-    } else {
-      uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-      uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
-      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-      w[i & 15] = wi;
-    }
-    uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
-    uint32_t ch = (e & f) ^ (~e & g);
-    uint32_t t1 = hh + S1 + ch + kSha256K[i] + wi;
-    uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
-    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
-    uint32_t t2 = S0 + mj;
-    hh = g;
-    g = f;
-    f = e;
-    e = d + t1;
-    d = c;
-    c = b;
-    b = a;
-    a = t1 + t2;
+    const uint32_t wi = i < 16 ? w[i] : sha256_sched(w, i);
+    sha256_round(a, b, c, d, e, f, g, hh, wi + kSha256K[i]);
   }
   h[0] += a; h[1] += b; h[2] += c; h[3] += d;
   h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
@@ -127,6 +154,29 @@ BH_HD uint32_t sha256_word2(const uint8_t* m1, uint64_t l1, const uint8_t* m2, u
   return w;
 }
 
+// ---- split compression (round 5): the message schedule of a block depends on
+// the block alone, so it can be expanded by other lanes ahead of the serial
+// chain of rounds (k_digest_grp). sched: wk[t] = W[t] + K[t], t < 64;
+// rounds: the 64 rounds over a precomputed wk. sha256_rounds_wk(h,
+// sha256_sched_wk(w)) == sha256_block(h, w).
+BH_HD void sha256_sched_wk(uint32_t wk[64], uint32_t w[16]) {
+#pragma unroll
+  for (int i = 0; i < 64; i++) wk[i] = (i < 16 ? w[i] : sha256_sched(w, i)) + kSha256K[i];
+}
+
+BH_HD void sha256_rounds_wk(uint32_t h[8], const uint32_t wk[64]) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+  for (int i = 0; i < 64; i++) sha256_round(a, b, c, d, e, f, g, hh, wk[i]);
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d;
+  h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// The 16 big-endian words of padded block blk (byte offset) of the two-span
+// message m1[0, l1) || m2[0, len - l1) (one span: l1 = len, m2 unused).
+BH_HD void sha256_load_block(uint32_t w[16], const uint8_t* m1, uint64_t l1, const uint8_t* m2,
+                             uint64_t len, uint64_t total, uint64_t blk);
+
 BH_HD void sha256_msg2(uint32_t out[8], const uint8_t* m1, uint64_t l1, const uint8_t* m2,
                        uint64_t l2) {
   uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
@@ -150,6 +200,21 @@ BH_HD void sha256_msg2(uint32_t out[8], const uint8_t* m1, uint64_t l1, const ui
   }
 #pragma unroll
   for (int i = 0; i < 8; i++) out[i] = h[i];
+}
+
+BH_HD void sha256_load_block(uint32_t w[16], const uint8_t* m1, uint64_t l1, const uint8_t* m2,
+                             uint64_t len, uint64_t total, uint64_t blk) {
+  const uint8_t* src = blk + 64 <= l1 ? m1 + blk
+                       : (blk >= l1 && blk + 64 <= len) ? m2 + (blk - l1)
+                                                        : nullptr;
+  if (src) {
+    load_le_words<16>(w, src);
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = bswap32(w[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = sha256_word2(m1, l1, m2, len, total, blk + 4 * i);
+  }
 }
 
 }  // namespace bh
