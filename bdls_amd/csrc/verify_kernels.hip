@@ -163,16 +163,35 @@ __device__ __forceinline__ uint64_t qperm(uint64_t x) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// 64-bit rotation right by N as two v_alignbit_b32 (the shift / or form the
+// compiler picks for 24 and 63 costs ~4 more instructions per G)
+template <int N>
+__device__ __forceinline__ uint64_t b2_rotr(uint64_t x) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t rl, rh;
+  if constexpr (N == 32) {
+    rl = hi;
+    rh = lo;
+  } else if constexpr (N < 32) {
+    rl = __builtin_amdgcn_alignbit(hi, lo, N);
+    rh = __builtin_amdgcn_alignbit(lo, hi, N);
+  } else {
+    rl = __builtin_amdgcn_alignbit(lo, hi, N - 32);
+    rh = __builtin_amdgcn_alignbit(hi, lo, N - 32);
+  }
+  return ((uint64_t)rh << 32) | rl;
+}
+
 __device__ __forceinline__ void b2_gq(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d,
                                       uint64_t x, uint64_t y) {
   a = a + b + x;
-  d = rotr64(d ^ a, 32);
+  d = b2_rotr<32>(d ^ a);
   c = c + d;
-  b = rotr64(b ^ c, 24);
+  b = b2_rotr<24>(b ^ c);
   a = a + b + y;
-  d = rotr64(d ^ a, 16);
+  d = b2_rotr<16>(d ^ a);
   c = c + d;
-  b = rotr64(b ^ c, 63);
+  b = b2_rotr<63>(b ^ c);
 }
 
 template <class C>
