@@ -675,6 +675,7 @@ VarField span(const uint64_t* off, const uint32_t* len, size_t lo, size_t m) {
 struct Uploader {
   char* base;
   hipStream_t s;
+  HostBuf* gather = nullptr;  // the slot's page-locked scratch (compact key gather)
   size_t used = 0;
   hipError_t err = hipSuccess;
   template <class T>
@@ -695,7 +696,8 @@ struct Uploader {
 
 struct HostFields {
   std::vector<VarField> var;
-  size_t bytes = 0;  // staging bytes
+  size_t bytes = 0;      // staging bytes
+  bool gather = false;   // compact shard: keys gathered per record on the host
 };
 
 HostFields fields(const bh_batch* b, size_t lo, size_t m) {
@@ -806,30 +808,46 @@ HostFields fields(const CompactHost* h, size_t lo, size_t m) {
   }
   f.var.push_back(VarField{s0, s1});
   f.var.push_back(VarField{m0, m1});
+  // a shard that references fewer records than the batch has distinct keys
+  // (mostly distinct keys, or a small shard of a multi-device batch) takes its
+  // keys gathered per record: fewer bytes than the whole key table + indices
+  f.gather = c.key_idx && c.nkeys > m;
+  const bool idx = c.key_idx && !f.gather;
   auto r = [](size_t b) { return round256(b + 1); };
-  f.bytes = r(c.key_idx ? c.nkeys * 64 : m * 64) + (c.key_idx ? r(m * 4) + r(m * 64) : 0) +
-            r(s1) + r(m * 4) + r(m1) + r(m * 4) + 2 * r(m * 8) +
-            r(bh::expand_temp_bytes((uint32_t)m));
+  f.bytes = r(idx ? c.nkeys * 64 : m * 64) + (idx ? r(m * 4) + r(m * 64) : 0) + r(s1) +
+            r(m * 4) + r(m1) + r(m * 4) + 2 * r(m * 8) + r(bh::expand_temp_bytes((uint32_t)m));
   return f;
 }
 
 CompactDev upload(Uploader& u, const CompactHost* h, size_t lo, size_t m, const HostFields& f) {
   const bh_cbatch& c = h->c;
   CompactDev d;
-  d.keys = c.key_idx ? u.put(c.keys, c.nkeys * 64) : u.put(c.keys + lo * 64, m * 64);
-  d.key_idx = c.key_idx ? u.put(c.key_idx + lo, m) : nullptr;
+  const bool idx = c.key_idx && !f.gather;
+  if (f.gather) {
+    if (!u.gather || u.gather->ensure(m * 64)) {
+      u.err = hipErrorOutOfMemory;
+    } else {
+      uint8_t* g = (uint8_t*)u.gather->p;
+      for (size_t i = 0; i < m; i++)
+        std::memcpy(g + i * 64, c.keys + (size_t)c.key_idx[lo + i] * 64, 64);
+    }
+    d.keys = u.put(u.err == hipSuccess ? (const uint8_t*)u.gather->p : nullptr, m * 64);
+  } else {
+    d.keys = idx ? u.put(c.keys, c.nkeys * 64) : u.put(c.keys + lo * 64, m * 64);
+  }
+  d.key_idx = idx ? u.put(c.key_idx + lo, m) : nullptr;
   const uint8_t* sig = u.put<uint8_t>(c.sig ? c.sig + f.var[0].lo : nullptr, f.var[0].bytes);
   d.sig_len = u.put(c.sig_len + lo, m);
   const uint8_t* msg = u.put<uint8_t>(c.msg ? c.msg + f.var[1].lo : nullptr, f.var[1].bytes);
   d.msg_len = c.msg_len ? u.put(c.msg_len + lo, m) : nullptr;
   d.msg_len_out = c.msg_len ? nullptr : const_cast<uint32_t*>(u.put<uint32_t>(nullptr, m));
-  d.pub = c.key_idx ? const_cast<uint8_t*>(u.put<uint8_t>(nullptr, m * 64)) : nullptr;
+  d.pub = idx ? const_cast<uint8_t*>(u.put<uint8_t>(nullptr, m * 64)) : nullptr;
   d.sig_off = const_cast<uint64_t*>(u.put<uint64_t>(nullptr, m));
   d.msg_off = const_cast<uint64_t*>(u.put<uint64_t>(nullptr, m));
   d.temp_bytes = bh::expand_temp_bytes((uint32_t)m);
   d.temp = const_cast<uint8_t*>(u.put<uint8_t>(nullptr, d.temp_bytes));
   d.stride = c.msg_stride;
-  d.b = bh_batch{c.key_idx ? d.pub : d.keys, sig, d.sig_off, d.sig_len, msg, d.msg_off,
+  d.b = bh_batch{idx ? d.pub : d.keys, sig, d.sig_off, d.sig_len, msg, d.msg_off,
                  c.msg_len ? d.msg_len : d.msg_len_out};
   return d;
 }
@@ -917,7 +935,7 @@ int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, 
   const size_t out_bytes = round64(m) / 8 + m + 1024;
   if ((rc = sl.out.ensure(out_bytes))) return rc;
   if ((rc = sl.host_out.ensure(out_bytes))) return rc;
-  Uploader u{(char*)sl.stage.p, d.copy};
+  Uploader u{(char*)sl.stage.p, d.copy, &sl.host_in};
   const auto db = upload(u, b, lo, m, f);
   HIPCHK(u.err);
   HIPCHK(hipEventRecord(sl.uploaded, d.copy));
@@ -1122,11 +1140,17 @@ int submit_job(int curve, const B* b, size_t n, uint32_t flags, uint8_t* bitmap,
     *out = j;
     return BH_OK;
   }
-  const size_t nd = bh::shard_devices(n, devs.size());
+  // BH_HOST_SHARDS (default 1): shards per device, dealt round-robin -- the
+  // multi-device shard path (per-shard staging, compact key gather, bitmap
+  // merge at 64-record boundaries) on one device, and a finer upload/compute
+  // pipeline for very large host batches
+  size_t per = 1;
+  if (const char* e = getenv("BH_HOST_SHARDS")) per = (size_t)std::max(1, std::min(atoi(e), kSlots));
+  const size_t nd = bh::shard_devices(n, devs.size() * per);
   for (size_t k = 0; k < nd; k++) {
     const bh::Shard sh = bh::shard_of(n, nd, k);
     if (!sh.len) break;
-    Dev& d = *devs[k];
+    Dev& d = *devs[k % devs.size()];
     int rc;
     {
       std::lock_guard<std::mutex> g(d.mu);

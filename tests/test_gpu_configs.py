@@ -359,6 +359,31 @@ def test_compact_layout_ragged_messages_and_passes(L, small_chunks):
     assert (want == 2).sum() > 0  # empty digests -> BH_R_EMPTY_DIGEST
 
 
+@pytest.fixture
+def host_shards():
+    os.environ["BH_HOST_SHARDS"] = "3"
+    yield 3
+    del os.environ["BH_HOST_SHARDS"]
+
+
+@pytest.mark.parametrize("nkeys", [40_000, 3000])
+def test_compact_layout_shards_gather_keys(L, host_shards, nkeys):
+    """A host batch dealt as 3 shards (the multi-device shard path on one
+    device, BH_HOST_SHARDS): with more distinct keys than a shard has records
+    each shard uploads its keys gathered per record (no whole key table per
+    shard); with few keys the table + indices. Same bits and reasons as the
+    one-shard bh_batch layout, both entry points."""
+    n = 70_001  # shards of 23,360 / 23,360 / 23,281 records (64-record groups)
+    w = workload.generate(n, nkeys, 96, 8, seed=64)
+    arrs, cb = _lib.compact_layout(*w.arrays())
+    assert (cb.nkeys > n // 3) == (nkeys > n // 3)
+    for submit in (False, True):
+        bits, reason = _compact_verify(L, cb, n, submit=submit)
+        assert (reason == w.reason).all() and (bits == w.expected_valid).all(), submit
+    valid, r2 = host_verify(L, w)  # the plain layout, sharded the same way
+    assert (r2 == w.reason).all() and (valid == w.expected_valid).all()
+
+
 def test_compact_layout_rejects_bad_input(L):
     w = workload.generate(1000, 10, 32, 0, seed=63)
     arrs, cb = _lib.compact_layout(*w.arrays())
