@@ -118,3 +118,37 @@ def test_bench_refuses_foreign_counters(tmp_path, monkeypatch):
     tf.write_text(json.dumps(good))
     src, kernels, why = bench.load_counters(2, 1048576)
     assert why is None and cur in src and kernels == good["kernels"]
+
+
+def test_hostpath_timeline(tmp_path):
+    """tools/hostpath_timeline.py on a synthetic trace: 3 warm + 4 timed
+    batches on the copy stream (a 0.1 ms index copy + a 4 ms message copy
+    each), a resident upload on another stream, one k_bitmap per pass; the
+    first timed batch's upload is followed by a 2 ms gap."""
+    ms = lambda x: int(x * 1e6)
+    copies, kernels, t = [], [], 0.0
+    for b in range(7):
+        if b == 4:
+            t += 2.0  # the gap behind timed batch 0
+        copies.append(("2", t, t + 0.1))
+        copies.append(("2", t + 0.1, t + 4.1))
+        kernels.append(t + 9.0)  # its pass ends 4.9 ms after its upload
+        t += 4.1
+    copies.append(("1", t + 20, t + 24))  # resident upload
+    with open(tmp_path / "x_memory_copy_trace.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Direction", "Stream_Id", "Start_Timestamp", "End_Timestamp"])
+        for s, a, b in copies:
+            w.writerow(["MEMORY_COPY_HOST_TO_DEVICE", s, ms(a), ms(b)])
+    with open(tmp_path / "x_kernel_trace.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        for e in kernels:
+            w.writerow(["k_bitmap", ms(e - 0.01), ms(e)])
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "hostpath_timeline.py"),
+                          str(tmp_path), "--steps", "3"], capture_output=True, check=True)
+    d = json.loads(out.stdout)
+    assert d["batches"] == 3
+    assert abs(d["upload_spacing_mean_ms"] - 4.1) < 1e-3
+    assert abs(d["drain_ms"] - 4.9) < 1e-3
+    assert abs(d["timed_span_ms"] - (2 * 4.1 + 9.0)) < 1e-3
