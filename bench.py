@@ -10,9 +10,9 @@ One "step" = one verify pass over the whole batch with its inputs already
 resident in HBM (bh_verify_dev: DER parse, checks, SHA-256, batched inversion,
 u1 G + u2 Q, bitmap): `value` is that rate, barrier + device sync around the
 K timed steps. The PCIe-inclusive rate SURVEY 8(d) also names for config 2
-(H2D + verify + D2H per step through bh_verify_submit from page-locked host
-buffers, three batches in flight, so batch k+1's upload runs under batch k's
-kernels) is measured first and reported beside it as `host_path`.
+(H2D + verify + results to page-locked memory per step through
+bh_verify_submit from page-locked host buffers, four batches in flight, so
+batch k+1's upload runs under batch k's kernels) is measured first and reported beside it as `host_path`.
 
 `--config 5`: ONE seeded batch of 67,108,864 records with a distinct key per
 record, split over the ranks by dist.shard_range (8,388,608 per rank at 8 GPUs,
@@ -710,7 +710,7 @@ def bench_throughput(a, rank, world, local):
     phase(f"host path: {a.warmup} warmup batches")
     run_host(a.warmup)
     _lib.check(L.bh_sync(local))
-    # one batch alone (nothing in flight): H2D + verify + D2H latency, and the
+    # one batch alone (nothing in flight): H2D + verify + results latency, and the
     # page-locked H2D bandwidth of the batch's largest array
     phase("host path: one batch alone")
     t = time.perf_counter()
@@ -853,7 +853,7 @@ def bench_throughput(a, rank, world, local):
                          "compute lanes, BH_F_ANY_LANE), barrier + device sync around the "
                          "timed steps" if resident else
                          "host C ABI BatchVerify (bh_verify_submit/wait) from page-locked host "
-                         "buffers: H2D + verify + D2H per step (--hbm-resident 0)"),
+                         "buffers: H2D + verify + results to page-locked memory per step (--hbm-resident 0)"),
         },
         "parity": parity_ok,
         "hbm_resident": resident,
@@ -862,7 +862,7 @@ def bench_throughput(a, rank, world, local):
                                 "bh_verify_wait, the compact bh_cbatch layout: distinct keys "
                                 "+ u32 indices, lengths only) " if compact else
                                 "host C ABI BatchVerify (bh_verify_submit/wait, bh_batch) ")
-                               + "from page-locked host buffers: H2D + verify + D2H per step, "
+                               + "from page-locked host buffers: H2D + verify + results to page-locked memory per step, "
                                "batches in flight over the compute lanes (SURVEY 8(d)'s "
                                "config-2 timed quantity, PCIe-inclusive)"),
                       "layout": layout,
