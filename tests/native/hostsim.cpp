@@ -281,6 +281,22 @@ extern "C" void hs_n_mont_inv(int curve, const uint32_t* a, uint32_t* r) {
 extern "C" void hs_sha256(const uint8_t* msg, uint32_t len, uint32_t* out) {
   sha256_msg(out, msg, len);
 }
+// k_digest_grp's split compression (sha256.h): every block loaded with
+// sha256_load_block, expanded by sha256_sched_wk, compressed by
+// sha256_rounds_wk; two spans m1 || m2 (l2 = 0: one span).
+extern "C" void hs_sha256_split(const uint8_t* m1, uint32_t l1, const uint8_t* m2, uint32_t l2,
+                                uint32_t* out) {
+  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  const uint64_t len = (uint64_t)l1 + l2, total = ((len + 9 + 63) / 64) * 64;
+  for (uint64_t blk = 0; blk < total; blk += 64) {
+    uint32_t w[16], wk[64];
+    sha256_load_block(w, m1, l2 ? l1 : len, l2 ? m2 : m1, len, total, blk);
+    sha256_sched_wk(wk, w);
+    sha256_rounds_wk(h, wk);
+  }
+  for (int i = 0; i < 8; i++) out[i] = h[i];
+}
 extern "C" void hs_sha3_256(const uint8_t* msg, uint32_t len, uint8_t* out) {
   sha3_256_msg(out, msg, len);
 }

@@ -331,6 +331,53 @@ def test_two_span_messages(csp, family):
     assert rc != 0
 
 
+DIGEST_LENS = [1, 2, 54, 55, 56, 57, 63, 64, 65, 118, 119, 120, 127, 128, 129, 1023, 1024,
+               1025, 1535, 4095, 4096, 4097, 13_337]
+
+
+def test_variable_length_digests(csp):
+    """Fused SHA-256 of a small batch (the split path: k_digest_grp, 16 lanes
+    per record, one schedule per 16 blocks) at every padding edge (55 / 56 /
+    64 / 119 / 120 bytes ...), up to 210 blocks, mixed in one batch so a
+    wave's records differ in length, plus empty messages; one span and two
+    spans (bh_verify_2seg, seams at 0, 1, block edges, len). Expected reasons
+    from construction, the empty messages' from the oracle (oracle/orc.c with
+    hashlib's digest)."""
+    import hashlib
+
+    from bdls_amd import workload
+    from oracle import orc
+    from tests.test_hostsim import split_layout
+    parts = [workload.generate(24, 5, ln, 6, seed=100 + k) for k, ln in enumerate(DIGEST_LENS)]
+    w = workload.concat(parts)
+    pub, sig, so, sl, msg, mo, ml = w.arrays()
+    ml = ml.copy()
+    want = w.reason.copy()
+    for i in range(0, 24 * 3, 11):  # empty messages: the digest of b""
+        ml[i] = 0
+        want[i] = orc.csp_verify(bytes(pub[64 * i:64 * i + 64]),
+                                 bytes(sig[int(so[i]):int(so[i]) + int(sl[i])]),
+                                 hashlib.sha256(b"").digest())
+    n = w.n
+    b = _lib.BhBatch(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
+                     msg.ctypes.data, mo.ctypes.data, ml.ctypes.data)
+    bitmap = np.zeros((n + 7) // 8, np.uint8)
+    reason = np.full(n, 255, np.uint8)
+    _lib.check(_lib.lib().bh_verify(0, ctypes.byref(b), n, _lib.BH_F_HASH_SHA256,
+                                    bitmap.ctypes.data, reason.ctypes.data))
+    assert (reason == want).all(), np.nonzero(reason != want)[0][:10]
+    assert (np.unpackbits(bitmap, bitorder="little")[:n].astype(bool) == (want == 0)).all()
+    msgs = [bytes(msg[int(o):int(o) + int(l)]) for o, l in zip(mo, ml)]
+    mbuf, o1, l1, o2, l2 = split_layout(msgs, 5)
+    b2 = _lib.BhBatch(pub.ctypes.data, sig.ctypes.data, so.ctypes.data, sl.ctypes.data,
+                      mbuf.ctypes.data, o1.ctypes.data, l1.ctypes.data)
+    reason2 = np.full(n, 255, np.uint8)
+    _lib.check(_lib.lib().bh_verify_2seg(_lib.BH_CURVE_P256, ctypes.byref(b2), o2.ctypes.data,
+                                         l2.ctypes.data, n, _lib.BH_F_HASH_SHA256,
+                                         bitmap.ctypes.data, reason2.ctypes.data))
+    assert (reason2 == want).all(), np.nonzero(reason2 != want)[0][:10]
+
+
 @pytest.mark.gpu
 def test_coalescer_cap_enforced():
     """BH_COALESCE_CAP bounds the records of one coalesced device batch: 32

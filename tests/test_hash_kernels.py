@@ -43,6 +43,28 @@ def test_sha256(L, align):
 
 
 @pytest.mark.parametrize("align", [0, 1, 2, 3])
+def test_sha256_split_compression(L, align):
+    """k_digest_grp's split form (sha256_load_block -> sha256_sched_wk ->
+    sha256_rounds_wk): one span, and two spans with the seam at 0, 1, a block
+    edge, the end and a random byte."""
+    rng = random.Random(100 + align)
+    out = (ctypes.c_uint32 * 8)()
+    L.hs_sha256_split.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                  ctypes.c_uint32, ctypes.c_void_p]
+    for n in LENS:
+        m = rng.randbytes(n)
+        want = hashlib.sha256(m).digest()
+        buf, p = placed(m, align)
+        L.hs_sha256_split(p, n, p, 0, out)
+        assert b"".join(struct.pack(">I", out[i]) for i in range(8)) == want, n
+        for k in {0, min(n, 1), min(n, 64), n, rng.randint(0, n)}:
+            b1, p1 = placed(m[:k], align)
+            b2, p2 = placed(m[k:], 3 - align)
+            L.hs_sha256_split(p1, k, p2, n - k, out)
+            assert b"".join(struct.pack(">I", out[i]) for i in range(8)) == want, (n, k)
+
+
+@pytest.mark.parametrize("align", [0, 1, 2, 3])
 def test_bdls_blake2b(L, align):
     # vendor/github.com/BDLS-bft/bdls/message.go:97-138 SignedProto.Hash framing
     rng = random.Random(10 + align)
