@@ -175,6 +175,7 @@ struct Slot {
   // k_result_out, read by the host after the slot's done event)
   HostBuf host_out{nullptr, 0, hipHostMallocPortable | hipHostMallocCoherent};
   hipEvent_t uploaded = nullptr, done = nullptr;
+  hipEvent_t keys_up = nullptr;  // the key half of the shard uploaded
   bh_job* owner = nullptr;  // job whose results are in flight / sit in host_out
   size_t owner_part = 0;
 };
@@ -399,6 +400,7 @@ int dev_init(Dev& d, int id) {
   for (Slot& sl : d.slot) {
     HIPCHK(hipEventCreateWithFlags(&sl.uploaded, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&sl.keys_up, hipEventDisableTiming));
   }
   for (int c = 0; c < 2; c++) {
     HIPCHK(hipMalloc(&d.gtab[c], kGtabWords * 4));
@@ -559,9 +561,13 @@ hipError_t launch(int curve, const bh::BdlsIn& in, const bh::Work& w, const bh::
 // lane 0 .. lanes() - 1: a host-API batch on that lane (after the lane's
 // previous pass; lanes >= 1 also after the last registry write).
 // BH_F_KEEP_KEYS passes write the registry and are always serialised.
+// records_ready (host shards uploaded key half first): the event of the
+// whole shard's upload; the pass waits for it after its key half (one-pass
+// shards: LaunchOpts::records_ready) or before anything.
 template <class B>
 int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* bitmap,
-            uint8_t* reason, hipStream_t s, bh_timing* t, int lane = -1) {
+            uint8_t* reason, hipStream_t s, bh_timing* t, int lane = -1,
+            hipEvent_t records_ready = nullptr) {
   if (t) *t = bh_timing{};
   if (flags & BH_F_KEEP_KEYS) lane = -1;
   if ((flags & BH_F_KEEP_KEYS) && d.reg[curve].g.cap == 0) {
@@ -580,6 +586,10 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
     if (lane > 0 && d.reg_written_recorded) HIPCHK(hipStreamWaitEvent(s, d.reg_written, 0));
   }
   const size_t chunk = max_chunk();
+  if (records_ready && (n > chunk || t || d.defer)) {
+    HIPCHK(hipStreamWaitEvent(s, records_ready, 0));
+    records_ready = nullptr;
+  }
   for (size_t base = 0; base < n; base += chunk) {
     const size_t m = std::min(chunk, n - base);
     bh::Work w;
@@ -594,6 +604,7 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
     o.aux = L.aux;
     o.ev_fork = L.fork;
     o.ev_join = L.join;
+    o.records_ready = records_ready;
     if (lane >= 0 && d.build_staggered && lanes() > 1) {
       // (an event never recorded is complete: the first builds do not wait)
       // builds take turns around the lanes: this lane's waits for the lane
@@ -676,8 +687,16 @@ struct Uploader {
   char* base;
   hipStream_t s;
   HostBuf* gather = nullptr;  // the slot's page-locked scratch (compact key gather)
+  hipEvent_t mark_ev = nullptr;  // recorded after the key arrays (records_ready passes)
+  bool marked = false;
   size_t used = 0;
   hipError_t err = hipSuccess;
+  // the arrays queued so far are the pass's key half (keys and lengths)
+  void mark() {
+    if (!mark_ev || err != hipSuccess) return;
+    err = hipEventRecord(mark_ev, s);
+    marked = err == hipSuccess;
+  }
   template <class T>
   const T* put(const T* src, size_t count) {
     char* dst = base + used;
@@ -716,6 +735,7 @@ bh_batch upload(Uploader& u, const bh_batch* b, size_t lo, size_t m, const HostF
   d.sig_len = u.put(b->sig_len + lo, m);
   d.msg_off = u.put(b->msg_off + lo, m);
   d.msg_len = u.put(b->msg_len + lo, m);
+  u.mark();
   d.sig = u.put(b->sig, f.var[0]);
   d.msg = u.put(b->msg, f.var[1]);
   return d;
@@ -836,10 +856,11 @@ CompactDev upload(Uploader& u, const CompactHost* h, size_t lo, size_t m, const 
     d.keys = idx ? u.put(c.keys, c.nkeys * 64) : u.put(c.keys + lo * 64, m * 64);
   }
   d.key_idx = idx ? u.put(c.key_idx + lo, m) : nullptr;
-  const uint8_t* sig = u.put<uint8_t>(c.sig ? c.sig + f.var[0].lo : nullptr, f.var[0].bytes);
   d.sig_len = u.put(c.sig_len + lo, m);
-  const uint8_t* msg = u.put<uint8_t>(c.msg ? c.msg + f.var[1].lo : nullptr, f.var[1].bytes);
   d.msg_len = c.msg_len ? u.put(c.msg_len + lo, m) : nullptr;
+  u.mark();  // keys + lengths: enough for the expansion and the key half of the pass
+  const uint8_t* sig = u.put<uint8_t>(c.sig ? c.sig + f.var[0].lo : nullptr, f.var[0].bytes);
+  const uint8_t* msg = u.put<uint8_t>(c.msg ? c.msg + f.var[1].lo : nullptr, f.var[1].bytes);
   d.msg_len_out = c.msg_len ? nullptr : const_cast<uint32_t*>(u.put<uint32_t>(nullptr, m));
   d.pub = idx ? const_cast<uint8_t*>(u.put<uint8_t>(nullptr, m * 64)) : nullptr;
   d.sig_off = const_cast<uint64_t*>(u.put<uint64_t>(nullptr, m));
@@ -915,6 +936,22 @@ int finish_part(bh_job* j, size_t k) {
   return BH_OK;
 }
 
+// Host layouts whose upload marks its key half (Uploader::mark): bh_batch and
+// compact shards; two-span and BDLS batches upload in one piece.
+bool keys_first_ok(const bh_batch*) { return true; }
+bool keys_first_ok(const CompactHost*) { return true; }
+template <class T>
+bool keys_first_ok(const T*) {
+  return false;
+}
+bool keys_first() {
+  static const bool on = [] {
+    const char* e = getenv("BH_KEYS_FIRST");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 // Enqueue shard [lo, lo + m) on device d (caller holds d.mu).
 template <class B>
 int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, uint32_t flags) {
@@ -936,6 +973,11 @@ int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, 
   if ((rc = sl.out.ensure(out_bytes))) return rc;
   if ((rc = sl.host_out.ensure(out_bytes))) return rc;
   Uploader u{(char*)sl.stage.p, d.copy, &sl.host_in};
+  // key half first (bh_batch and compact shards of one pass, no registry
+  // writes): the pass imports the keys, plans and builds its tables while the
+  // signatures and messages upload (BH_KEYS_FIRST=0: wait for the whole shard)
+  if (keys_first_ok(b) && !(flags & BH_F_KEEP_KEYS) && m <= max_chunk() && keys_first())
+    u.mark_ev = sl.keys_up;
   const auto db = upload(u, b, lo, m, f);
   HIPCHK(u.err);
   HIPCHK(hipEventRecord(sl.uploaded, d.copy));
@@ -943,11 +985,13 @@ int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, 
   // (BH_F_KEEP_KEYS) serialise on lane 0
   const int lane = (flags & BH_F_KEEP_KEYS) ? -1 : (int)(d.next_lane++ % lanes());
   hipStream_t s = lane > 0 ? lane_ref(d, lane).stream : d.stream;
-  HIPCHK(hipStreamWaitEvent(s, sl.uploaded, 0));
+  HIPCHK(hipStreamWaitEvent(s, u.marked ? sl.keys_up : sl.uploaded, 0));
   HIPCHK(expand_dev(db, m, s));
   uint64_t* dbm = (uint64_t*)sl.out.p;
   uint8_t* drs = (uint8_t*)(dbm + round64(m) / 64);
-  if ((rc = run_dev(d, curve, dev_batch(db), m, flags, dbm, drs, s, nullptr, lane))) return rc;
+  if ((rc = run_dev(d, curve, dev_batch(db), m, flags, dbm, drs, s, nullptr, lane,
+                    u.marked ? sl.uploaded : nullptr)))
+    return rc;
   // results: words then reasons, contiguous on both sides. A kernel, not a
   // D2H copy: a copy-engine command that waits on this pass would hold the
   // engine's later commands -- the next batches' uploads -- until the pass

@@ -132,6 +132,11 @@ struct LaunchOpts {
   // per-batch key tables of one-lane-per-record batches as Lim-Lee combs
   // (verify.h lltab_build; BH_LL=0 keeps the 4-bit windows everywhere)
   bool ll_tables = true;
+  // Host batches (round 5): the keys arrive before the signatures and
+  // messages. With this hipEvent_t set, the pass runs its key half (key
+  // import, plan, table builds) first and waits for the event -- the rest of
+  // the batch uploaded -- only before prep; otherwise it waits up front.
+  void* records_ready = nullptr;
 };
 
 // Lanes per record on the key-table path by batch size (records far below
@@ -229,6 +234,24 @@ BH_HD bool key_import(const uint8_t* q, uint32_t qx30[9], uint32_t qy30[9]) {
   f_canon<P>(qx30, qx30);
   f_canon<P>(qy30, qy30);
   return j_on_curve<P>(qx30, qy30);
+}
+
+// The key half of prep for a pass that plans and builds before its
+// signatures / messages arrive (LaunchOpts::records_ready): Q imported as in
+// stage_prep, st = R_OK or R_BAD_KEY (stage_prep rewrites both later; a record
+// whose signature then fails keeps its key's place in the plan, which only
+// decides which tables are built).
+template <class P, class C>
+BH_HD void stage_prep_key(const BatchIn& in, const Work& w, uint32_t i) {
+  uint32_t qx30[9], qy30[9];
+  const bool ok = key_import<P, C>(in.pub + (size_t)i * 64, qx30, qy30);
+  if (!ok) {
+    f_const(qx30, P::gx_m);
+    f_const(qy30, P::gy_m);
+  }
+  st9(w.qx, i, w.ns, qx30);
+  st9(w.qy, i, w.ns, qy30);
+  w.st[i] = ok ? (uint8_t)R_OK : (uint8_t)R_BAD_KEY;
 }
 
 // e = hashToNat(digest) mod n for record i: the given digest, or the fused

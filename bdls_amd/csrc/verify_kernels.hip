@@ -43,6 +43,14 @@ __global__ __launch_bounds__(256) void k_prep(IN in, Work w, uint32_t n) {
   else stage_prep<P, N, C>(in, w, i);
 }
 
+// The key half of prep (LaunchOpts::records_ready passes).
+template <class P, class C>
+__global__ __launch_bounds__(256) void k_prep_keys(BatchIn in, Work w, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  stage_prep_key<P, C>(in, w, i);
+}
+
 // e of every record (k_prep<..., DEFER>): the fused digests of a small batch
 // on the second stream, beside prep / inverse / plan / the u2 Q work.
 template <class C, int HK>
@@ -1177,6 +1185,42 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
 #define REC(k)                                                 \
   if (ev) {                                                    \
     if ((e = hipEventRecord(ev[k], s)) != hipSuccess) return e; \
+  }
+  // Host batches whose keys arrived first (records_ready): the key half --
+  // key import, plan, table builds -- runs while the signatures and messages
+  // are still uploading; the records' half after the event. One-lane comb
+  // batches without registry writes or stage timing; otherwise wait up front.
+  if (o.records_ready) {
+    const bool ll1 = o.ll_tables && o.wide <= 1;
+    if (kBdls || split || !ll1 || o.keep || ev) {
+      if ((e = hipStreamWaitEvent(s, (hipEvent_t)o.records_ready, 0))) return e;
+    } else if constexpr (!kBdls) {
+      if ((e = plan_reset(pl, s))) return e;
+      hipLaunchKernelGGL((k_prep_keys<P, C>), grd, blk, 0, s, in, w, n);
+      hipLaunchKernelGGL(k_key_insert, grd, blk, 0, s, w, pl, g, n);
+      launch_key_count(w, pl, key_bytes(in), n, grd, blk, s);
+      hipLaunchKernelGGL(k_key_plan, grd, blk, 0, s, w, pl, g, n, o.min_uses, o.min_batch, 0u,
+                         0u);
+      const uint32_t tb = (pl.max_tables + kBuildPerBlock - 1) / kBuildPerBlock;
+      if (o.ev_build_wait && (e = hipStreamWaitEvent(s, (hipEvent_t)o.ev_build_wait, 0)))
+        return e;
+      hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tb), blk, 0, s, w, pl, g, gtab, reason, tb, 0u,
+                         1u);
+      if (o.ev_build_done && (e = hipEventRecord((hipEvent_t)o.ev_build_done, s))) return e;
+      if ((e = hipStreamWaitEvent(s, (hipEvent_t)o.records_ready, 0))) return e;
+      launch_prep<P, N, C>(in, w, n, grd, blk, s);
+      hipLaunchKernelGGL((k_inv<N, true>), grc, blk, 0, s, w, n, nlanes);
+      hipLaunchKernelGGL(k_split, dim3((n + kSplitBlock - 1) / kSplitBlock), dim3(kSplitBlock), 0,
+                         s, w, pl, n, reason);
+      Plan plk;
+      if ((e = comb_sort(pl, g, n, s, &plk))) return e;
+      // the ladder records alone (no table blocks)
+      hipLaunchKernelGGL((k_ktab_ladder<P>), grd, blk, 0, s, w, plk, g, gtab, reason, 0u, grd.x,
+                         1u);
+      hipLaunchKernelGGL((k_keycomb<P>), grd, blk, 0, s, w, plk, g, gtab, reason, 1u);
+      hipLaunchKernelGGL(k_bitmap, grd, blk, 0, s, reason, n, bitmap);
+      return hipGetLastError();
+    }
   }
   if ((e = plan_reset(pl, s))) return e;
   REC(0);
