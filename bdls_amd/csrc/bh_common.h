@@ -13,9 +13,11 @@
 #include <hip/hip_runtime.h>
 #define BH_HD __host__ __device__ __forceinline__
 #define BH_HDNI __host__ __device__ __attribute__((noinline))
+#define BH_HDM __host__ __device__ __forceinline__  // member functions
 #else
 #define BH_HD static inline __attribute__((always_inline))
 #define BH_HDNI static __attribute__((noinline))
+#define BH_HDM inline __attribute__((always_inline))
 #endif
 
 namespace bh {

@@ -1487,66 +1487,92 @@ BH_HD void z_load(uint32_t z[9], const uint32_t* p) {
   z[8] = c.x;
 }
 
-// The affine 4-bit windows of a registry slot: per window the co-Z chain of
-// ktab_build (1 B .. 8 B, Jacobian, each on its own Z) into 8 raw scratch
-// slots with the running product of their Z, one inversion, and a backward
-// pass storing the affine entries -- ~140 F_p ops per window on top of the
-// chain's 58. Never degenerate (ktab_build).
+// The affine 4-bit windows of a registry slot. Window win from its base
+// B = 16^win Q: the multiples B .. 8B (a co-Z doubling, then co-Z additions,
+// as ktab_build; never degenerate), made affine with one inversion
+// (Montgomery's trick over the 8 Z) -- ~140 F_p ops per window on top of the
+// chain's 58. The raw points and the Z
+// prefix products go through `raw` (store / load / store_z / load_z): the
+// slot's own scratch when one lane builds every window (reg_build, the host
+// harness), a column of LDS when each window has its own lane (k_reg_win).
+template <class P, class Raw>
+BH_HD void reg_window(uint32_t* tab, uint32_t win, const J30& B, Raw& raw) {
+  J30 Bz, S;
+  uint32_t z[9];
+  raw.store(0u, B);
+  f_copy(z, B.Z);
+  raw.store_z(0u, z);
+  j_dblu<P>(S, Bz, B);  // S = 2B, Bz = B on S's Z
+  raw.store(1u, S);
+  f_mul<P>(z, z, S.Z);
+  raw.store_z(1u, z);
+#pragma unroll 1
+  for (uint32_t j = 2; j < (uint32_t)kKEnt; j++) {
+    J30 T;
+    j_zaddu<P>(T, Bz, S);  // T = (j+1) B; Bz onto T's Z
+    raw.store(j, T);
+    f_mul<P>(z, z, T.Z);
+    raw.store_z(j, z);
+    j_copy(S, T);
+  }
+  uint32_t inv[9];
+  f_inv_sg<P>(inv, z);
+#pragma unroll 1
+  for (uint32_t j = (uint32_t)kKEnt; j-- > 0;) {
+    J30 E;
+    raw.load(E, j);
+    uint32_t zi[9], x[9], y[9];
+    if (j > 0) {
+      uint32_t pz[9];
+      raw.load_z(pz, j - 1u);
+      f_mul<P>(zi, inv, pz);
+      f_mul<P>(inv, inv, E.Z);
+    } else {
+      f_copy(zi, inv);
+    }
+    ll_to_affine<P>(x, y, E, zi);
+    llaff_store(tab + kRegWin, win * (uint32_t)kKEnt + j, x, y);
+  }
+}
+
+// reg_window's scratch in the slot itself (kRegWinRaw / kRegWinPre).
+struct RegSlotRaw {
+  uint32_t* tab;
+  BH_HDM void store(uint32_t j, const J30& P) { ktab_store(tab + kRegWinRaw, 0, j, P); }
+  BH_HDM void load(J30& P, uint32_t j) const { ktab_load(P, tab + kRegWinRaw, 0, j); }
+  BH_HDM void store_z(uint32_t j, const uint32_t z[9]) { z_store(tab + kRegWinPre + 12u * j, z); }
+  BH_HDM void load_z(uint32_t z[9], uint32_t j) const { z_load(z, tab + kRegWinPre + 12u * j); }
+};
+
+// The bases 16^win Q by four doublings each; the windows one after another.
 template <class P>
 BH_HD void ktab_build_aff(uint32_t* tab, const Work& w, uint32_t rec) {
-  uint32_t* raw = tab + kRegWinRaw;
-  uint32_t* pre = tab + kRegWinPre;
-  J30 B, Bz, S;
+  J30 B;
   ld9(B.X, w.qx, rec, w.ns);
   ld9(B.Y, w.qy, rec, w.ns);
   f_const(B.Z, P::r1);
+  RegSlotRaw raw{tab};
 #pragma unroll 1
   for (uint32_t win = 0; win < (uint32_t)kKWin; win++) {
-    uint32_t z[9];
-    ktab_store(raw, 0, 0, B);                 // 1 B
-    f_copy(z, B.Z);
-    z_store(pre, z);
-    j_dblu<P>(S, Bz, B);                      // S = 2B, Bz = B on S's Z
-    ktab_store(raw, 0, 1, S);
-    f_mul<P>(z, z, S.Z);
-    z_store(pre + 12, z);
+    reg_window<P>(tab, win, B, raw);
+    if (win + 1u < (uint32_t)kKWin) {
 #pragma unroll 1
-    for (uint32_t j = 2; j < (uint32_t)kKEnt; j++) {
-      J30 T;
-      j_zaddu<P>(T, Bz, S);                   // T = (j+1) B; Bz onto T's Z
-      ktab_store(raw, 0, j, T);
-      f_mul<P>(z, z, T.Z);
-      z_store(pre + 12 * j, z);
-      j_copy(S, T);
-    }
-    j_dbl<P>(B, S);                           // 16 B: the next window's base
-    uint32_t inv[9];
-    f_inv_sg<P>(inv, z);
-#pragma unroll 1
-    for (uint32_t j = (uint32_t)kKEnt; j-- > 0;) {
-      J30 E;
-      ktab_load(E, raw, 0, j);
-      uint32_t zi[9], x[9], y[9];
-      if (j > 0) {
-        uint32_t pz[9];
-        z_load(pz, pre + 12 * (j - 1));
-        f_mul<P>(zi, inv, pz);
-        f_mul<P>(inv, inv, E.Z);
-      } else {
-        f_copy(zi, inv);
-      }
-      ll_to_affine<P>(x, y, E, zi);
-      llaff_store(tab + kRegWin, win * (uint32_t)kKEnt + j, x, y);
+      for (int d = 0; d < kKW; d++) j_dbl<P>(B, B);
     }
   }
 }
 
 // A registry slot: the comb, then the affine windows (one lane, ~16.8k F_p
-// ops once per key).
+// ops once per key; the device splits it: reg_build_comb in the build kernel,
+// the windows one lane each in k_reg_win).
 template <class P>
 BH_HD void reg_build(uint32_t* tab, const Work& w, uint32_t rec) {
   lltab_build<P>(tab, w, rec);
   ktab_build_aff<P>(tab, w, rec);
+}
+template <class P>
+BH_HD void reg_build_comb(uint32_t* tab, const Work& w, uint32_t rec) {
+  lltab_build<P>(tab, w, rec);
 }
 
 // Curve constants of a base-field class (the order n for u2 + n).

@@ -488,7 +488,7 @@ __device__ __forceinline__ void ktab_ladder_body(const Work& w, const Plan& pl, 
       // reg_build: the comb + affine windows)
       const uint32_t id = pl.tab_dst[t];
       uint32_t* tab = const_cast<uint32_t*>(tab_ptr(pl, g, id));
-      if (!(id & kLocal)) reg_build<P>(tab, w, pl.tab_rec[t]);
+      if (!(id & kLocal)) reg_build_comb<P>(tab, w, pl.tab_rec[t]);  // windows: k_reg_win
       else if (ll) lltab_build<P>(tab, w, pl.tab_rec[t]);
       else ktab_build<P>(tab, w, pl.tab_rec[t]);
     }
@@ -625,6 +625,93 @@ __global__ __launch_bounds__(256) void k_ladder2_g(Work w, Plan pl,
   g_comb_part<P, kLadGLanes>(C, c_inf, gtab, u1, l);
   group_sum<P, kLadGLanes>(C, c_inf);
   if (l == 0) reason[i] = finish_check<P>(w, i, C, c_inf, C, true) ? R_OK : R_MATH;
+}
+
+// The affine 4-bit windows of the registry slots built in this pass (round
+// 5), one workgroup per table: lane 0 walks the bases 16^win Q (four
+// doublings each) into LDS, then lane win builds window win (verify.h
+// reg_window) with its raw points and Z products in its own LDS column -- a
+// registration's critical path is the 256-doubling chain plus one window,
+// not 65 windows end to end (~16.8k F_p ops on one lane).
+constexpr uint32_t kRegWinBlock = 128;  // lanes 0 .. kKWin - 1 build windows
+static_assert(kKWin <= (int)kRegWinBlock, "one lane per window");
+struct RegLdsRaw {
+  uint32_t* pts;  // [point j][word k][lane]: 27 words per point
+  uint32_t* zs;   // [j][k][lane]: 9 words per product
+  uint32_t lane;
+  __device__ void store(uint32_t j, const J30& P) {
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      pts[((j * 27u) + k) * kKWin + lane] = P.X[k];
+      pts[((j * 27u) + 9u + k) * kKWin + lane] = P.Y[k];
+      pts[((j * 27u) + 18u + k) * kKWin + lane] = P.Z[k];
+    }
+  }
+  __device__ void load(J30& P, uint32_t j) const {
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      P.X[k] = pts[((j * 27u) + k) * kKWin + lane];
+      P.Y[k] = pts[((j * 27u) + 9u + k) * kKWin + lane];
+      P.Z[k] = pts[((j * 27u) + 18u + k) * kKWin + lane];
+    }
+  }
+  __device__ void store_z(uint32_t j, const uint32_t z[9]) {
+#pragma unroll
+    for (int k = 0; k < 9; k++) zs[(j * 9u + k) * kKWin + lane] = z[k];
+  }
+  __device__ void load_z(uint32_t z[9], uint32_t j) const {
+#pragma unroll
+    for (int k = 0; k < 9; k++) z[k] = zs[(j * 9u + k) * kKWin + lane];
+  }
+};
+template <class P>
+__global__ __launch_bounds__(kRegWinBlock) void k_reg_win(Work w, Plan pl, KeyReg g) {
+  __shared__ uint32_t s_base[kKWin * 27];
+  __shared__ uint32_t s_pts[kKEnt * 27 * kKWin];
+  __shared__ uint32_t s_zs[kKEnt * 9 * kKWin];
+  const uint32_t t = blockIdx.x;
+  const uint32_t nt = min(pl.counters[2], pl.max_tables);
+  if (t >= nt) return;  // the whole workgroup
+  const uint32_t id = pl.tab_dst[t];
+  if (id & kLocal) return;  // a per-batch table: no windows
+  uint32_t* tab = const_cast<uint32_t*>(tab_ptr(pl, g, id));
+  const uint32_t lane = threadIdx.x;
+  if (lane == 0) {
+    J30 B;
+    ld9(B.X, w.qx, pl.tab_rec[t], w.ns);
+    ld9(B.Y, w.qy, pl.tab_rec[t], w.ns);
+    f_const(B.Z, P::r1);
+#pragma unroll 1
+    for (uint32_t win = 0; win < (uint32_t)kKWin; win++) {
+#pragma unroll
+      for (int k = 0; k < 9; k++) {
+        s_base[win * 27u + k] = B.X[k];
+        s_base[win * 27u + 9u + k] = B.Y[k];
+        s_base[win * 27u + 18u + k] = B.Z[k];
+      }
+      if (win + 1u < (uint32_t)kKWin) {
+#pragma unroll 1
+        for (int d = 0; d < kKW; d++) j_dbl<P>(B, B);
+      }
+    }
+  }
+  __syncthreads();
+  if (lane >= (uint32_t)kKWin) return;
+  J30 B;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    B.X[k] = s_base[lane * 27u + k];
+    B.Y[k] = s_base[lane * 27u + 9u + k];
+    B.Z[k] = s_base[lane * 27u + 18u + k];
+  }
+  RegLdsRaw raw{s_pts, s_zs, lane};
+  reg_window<P>(tab, lane, B, raw);
+}
+
+template <class P>
+static void launch_reg_win(const Work& w, const Plan& pl, const KeyReg& g, hipStream_t s) {
+  if (pl.max_tables)
+    hipLaunchKernelGGL((k_reg_win<P>), dim3(pl.max_tables), dim3(kRegWinBlock), 0, s, w, pl, g);
 }
 
 // Publish registry tables built in this batch (after the builds completed).
@@ -1297,6 +1384,7 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
     // key tables (no u1), then the u2 Q halves; u1 G after the join
     hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, plc, g, gtab, reason,
                        tab_blocks, 0u, 0u);
+    if (o.keep) launch_reg_win<P>(w, plc, g, s);  // the new registry slots' windows
     if constexpr (!P::a_is_minus3)
       hipLaunchKernelGGL((k_ladder2_q<P>), wgrd(2 * n), wblk, 0, s, w, plc,
                          pstride);
@@ -1330,6 +1418,7 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   if (o.ev_build_wait && (e = hipStreamWaitEvent(s, (hipEvent_t)o.ev_build_wait, 0))) return e;
   hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks + grd.x + gp_blocks), blk, 0, s, w, plc,
                      g, gtab, reason, tab_blocks, grd.x, ll);
+  if (o.keep) launch_reg_win<P>(w, plc, g, s);  // the new registry slots' windows
   if (o.ev_build_done && (e = hipEventRecord((hipEvent_t)o.ev_build_done, s))) return e;
   REC(4);
   if (o.keep)
@@ -1406,6 +1495,7 @@ static hipError_t reg_seq(const uint8_t* pub, const Work& w, const Plan& pl, con
   const uint32_t tab_blocks = (pl.max_tables + kBuildPerBlock - 1) / kBuildPerBlock;
   hipLaunchKernelGGL((k_ktab_ladder<P>), dim3(tab_blocks), blk, 0, s, w, pl, g,
                      (const uint32_t*)nullptr, (uint8_t*)nullptr, tab_blocks, 0u, 0u);
+  launch_reg_win<P>(w, pl, g, s);
   hipLaunchKernelGGL(k_reg_publish, dim3((pl.max_tables + 255) / 256), blk, 0, s, w, pl, g);
   hipLaunchKernelGGL(k_reg_status, grd, blk, 0, s, w, pl, n, status);
   return hipGetLastError();
