@@ -2,7 +2,7 @@
 # single-verify A/B: BH_SMALL_COPY_STREAM x BH_D2H_COPY
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/sv
-for v in ${SV_VARIANTS:-"cs1_k:BH_SMALL_COPY_STREAM=1" "cs0_k:BH_SMALL_COPY_STREAM=0" "cs0_c:BH_SMALL_COPY_STREAM=0 BH_D2H_COPY=1"}; do
+for v in "cs1_k:BH_SMALL_COPY_STREAM=1" "cs0_k:BH_SMALL_COPY_STREAM=0" "cs0_c:BH_SMALL_COPY_STREAM=0 BH_D2H_COPY=1"; do
   name=${v%%:*}; envs=${v#*:}
   env $envs timeout -k 10 300 python bench.py --steps 3 --warmup 1 --cpu-baseline 0 > gpurun_out/sv/$name.json 2> gpurun_out/sv/$name.err || { echo "STOP $name"; exit 1; }
   python3 -c "
