@@ -488,8 +488,8 @@ __device__ __forceinline__ void ktab_ladder_body(const Work& w, const Plan& pl, 
       // reg_build: the comb + affine windows)
       const uint32_t id = pl.tab_dst[t];
       uint32_t* tab = const_cast<uint32_t*>(tab_ptr(pl, g, id));
-      if (!(id & kLocal)) reg_build_comb<P>(tab, w, pl.tab_rec[t]);  // windows: k_reg_win
-      else if (ll) lltab_build<P>(tab, w, pl.tab_rec[t]);
+      if (!(id & kLocal)) return;  // a registry slot: k_reg_win builds all of it
+      if (ll) lltab_build<P>(tab, w, pl.tab_rec[t]);
       else ktab_build<P>(tab, w, pl.tab_rec[t]);
     }
     return;
@@ -627,14 +627,15 @@ __global__ __launch_bounds__(256) void k_ladder2_g(Work w, Plan pl,
   if (l == 0) reason[i] = finish_check<P>(w, i, C, c_inf, C, true) ? R_OK : R_MATH;
 }
 
-// The affine 4-bit windows of the registry slots built in this pass (round
-// 5), one workgroup per table: lane 0 walks the bases 16^win Q (four
-// doublings each) into LDS, then lane win builds window win (verify.h
-// reg_window) with its raw points and Z products in its own LDS column -- a
-// registration's critical path is the 256-doubling chain plus one window,
-// not 65 windows end to end (~16.8k F_p ops on one lane).
-constexpr uint32_t kRegWinBlock = 128;  // lanes 0 .. kKWin - 1 build windows
-static_assert(kKWin <= (int)kRegWinBlock, "one lane per window");
+// The registry slots of this pass (round 5), one workgroup per table: the
+// first lane of the third wave builds the comb (verify.h lltab_build) while
+// lane 0 walks the bases 16^win Q (four doublings each) into LDS; then lane
+// win builds window win (verify.h reg_window) with its raw points and Z
+// products in its own LDS column. A registration's critical path is the
+// comb build plus one window, not the comb and 65 windows end to end
+// (~16.8k F_p ops on one lane).
+constexpr uint32_t kRegWinBlock = 192;  // lanes 0 .. kKWin - 1: windows; lane 128: the comb
+static_assert(kKWin <= 128, "one lane per window, the comb in the third wave");
 struct RegLdsRaw {
   uint32_t* pts;  // [point j][word k][lane]: 27 words per point
   uint32_t* zs;   // [j][k][lane]: 9 words per product
@@ -676,6 +677,7 @@ __global__ __launch_bounds__(kRegWinBlock) void k_reg_win(Work w, Plan pl, KeyRe
   if (id & kLocal) return;  // a per-batch table: no windows
   uint32_t* tab = const_cast<uint32_t*>(tab_ptr(pl, g, id));
   const uint32_t lane = threadIdx.x;
+  if (lane == 128u) reg_build_comb<P>(tab, w, pl.tab_rec[t]);
   if (lane == 0) {
     J30 B;
     ld9(B.X, w.qx, pl.tab_rec[t], w.ns);
