@@ -3,7 +3,8 @@
 #   1. rocprofv3 --kernel-trace --stats of the driver's bench command, and
 #      tools/prof_check.py tying the dominant kernel's dispatches to the line;
 #   2. rocprofv3 --pmc passes, one counter group each (FETCH_SIZE, WRITE_SIZE,
-#      SQ_INSTS_VALU + GRBM_GUI_ACTIVE) on the one-lane bench, summarised by
+#      SQ_INSTS_VALU + GRBM_GUI_ACTIVE) on the one-lane bench (BH_KEYS_FIRST=0:
+#      one build launch per pass, as the resident passes run), summarised by
 #      tools/pmc_summary.py into gpurun_out/pmc_summary.json and, stamped with
 #      the kernel-source hash, gpurun_out/traffic.json;
 #   3. the driver's bench command once more, plain (the line the counters join).
@@ -20,7 +21,7 @@ python3 tools/prof_check.py gpurun_out/prof/run_kernel_trace.csv gpurun_out/prof
   gpurun_out/prof_check.json; cat gpurun_out/prof_check.json | head -30
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU GRBM_GUI_ACTIVE"; do
   tag=$(echo $grp | tr ' ' '_' | cut -c1-40)
-  BH_LANES=1 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv \
+  BH_LANES=1 BH_KEYS_FIRST=0 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv \
     -d gpurun_out/pmc_$tag -o pmc -- python3 bench.py --steps 1 --warmup 0 --cpu-baseline 0 \
     --hbm-resident 0 --side-configs 0 > gpurun_out/pmc_$tag.log 2>&1
   rc=$?; [ $rc -eq 0 ] || [ $rc -eq 3 ] || stop "pmc $grp" $rc
