@@ -717,14 +717,37 @@ struct HostFields {
   std::vector<VarField> var;
   size_t bytes = 0;      // staging bytes
   bool gather = false;   // compact shard: keys gathered per record on the host
+  bool shared = false;   // signatures and messages in one host buffer: staged once
 };
 
-HostFields fields(const bh_batch* b, size_t lo, size_t m) {
+HostFields fields_plain(const bh_batch* b, size_t lo, size_t m) {
   HostFields f;
   f.var.push_back(span(b->sig_off, b->sig_len, lo, m));
   f.var.push_back(span(b->msg_off, b->msg_len, lo, m));
   f.bytes = round256(m * 64 + 1) + 4 * round256(m * 8 + 1) + round256(f.var[0].bytes + 1) +
             round256(f.var[1].bytes + 1);
+  return f;
+}
+
+// Signatures and messages indexed into the same host buffer (a serialized
+// block, bh_fabric_block_preverify): one staged range covering both spans
+// instead of two overlapping copies of most of the block.
+void share_spans(HostFields& f, bool same) {
+  if (!same) return;
+  VarField& a = f.var[0];
+  VarField& m = f.var[1];
+  const uint64_t lo = a.bytes ? (m.bytes ? std::min(a.lo, m.lo) : a.lo) : m.lo;
+  const uint64_t hi = std::max(a.lo + a.bytes, m.lo + m.bytes);
+  f.bytes -= round256(a.bytes + 1) + round256(m.bytes + 1);
+  a.lo = m.lo = lo;
+  a.bytes = m.bytes = hi > lo ? hi - lo : 0;
+  f.bytes += round256(a.bytes + 1);
+  f.shared = true;
+}
+
+HostFields fields(const bh_batch* b, size_t lo, size_t m) {
+  HostFields f = fields_plain(b, lo, m);
+  share_spans(f, b->sig == b->msg);
   return f;
 }
 
@@ -737,13 +760,13 @@ bh_batch upload(Uploader& u, const bh_batch* b, size_t lo, size_t m, const HostF
   d.msg_len = u.put(b->msg_len + lo, m);
   u.mark();
   d.sig = u.put(b->sig, f.var[0]);
-  d.msg = u.put(b->msg, f.var[1]);
+  d.msg = f.shared ? d.sig : u.put(b->msg, f.var[1]);
   return d;
 }
 
 // message bytes of both spans: one staged range [min start, max end)
 HostFields fields(const SegBatch* b, size_t lo, size_t m) {
-  HostFields f = fields(&b->b, lo, m);
+  HostFields f = fields_plain(&b->b, lo, m);
   const VarField v2 = span(b->msg2_off, b->msg2_len, lo, m);
   VarField& v = f.var[1];
   const uint64_t a = std::min(v.lo, v2.lo), z = std::max(v.lo + v.bytes, v2.lo + v2.bytes);
@@ -751,6 +774,7 @@ HostFields fields(const SegBatch* b, size_t lo, size_t m) {
   v.lo = a;
   v.bytes = z - a;
   f.bytes += round256(v.bytes + 1) + 2 * round256(m * 8 + 1);
+  share_spans(f, b->b.sig == b->b.msg);
   return f;
 }
 
