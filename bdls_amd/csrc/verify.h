@@ -1374,7 +1374,11 @@ BH_HD void ll_affine_back(uint32_t* tab, uint32_t cnt, uint32_t inv[9], Dst dst)
 }
 
 template <class P>
-BH_HD void lltab_build(uint32_t* tab, const Work& w, uint32_t rec) {
+BH_HD void lltab_build(uint32_t* tab, const Work& w, uint32_t rec, uint32_t* scr = nullptr) {
+  // scr: the build scratch (aux / L / H / raw points / prefix products at the
+  // slot's own offsets); the slot itself unless the caller has LDS for it
+  // (k_reg_win: one table per workgroup)
+  if (!scr) scr = tab;
   uint32_t one[9];
   f_const(one, P::r1);
   // 1. The doubling chain: chain point 2i = D_i = 2 B_i, 2i + 1 = B_(i+1);
@@ -1383,35 +1387,35 @@ BH_HD void lltab_build(uint32_t* tab, const Work& w, uint32_t rec) {
   J30 B;
   ld9(B.X, w.qx, rec, w.ns);
   ld9(B.Y, w.qy, rec, w.ns);
-  llaff_store(tab, kLLAux, B.X, B.Y);
+  llaff_store(scr, kLLAux, B.X, B.Y);
   f_copy(B.Z, one);
   uint32_t z[9];
 #pragma unroll 1
   for (uint32_t i = 0; i + 1 < (uint32_t)kLLTeeth; i++) {
     j_dbl<P>(B, B);
-    llraw_store(tab, 2u * i, B);
+    llraw_store(scr, 2u * i, B);
     if (i == 0) f_copy(z, B.Z);
     else f_mul<P>(z, z, B.Z);
-    llpre_store(tab, 2u * i, z);
+    llpre_store(scr, 2u * i, z);
 #pragma unroll 1
     for (int d = 1; d < kLLSpace; d++) j_dbl<P>(B, B);
-    llraw_store(tab, 2u * i + 1u, B);
+    llraw_store(scr, 2u * i + 1u, B);
     f_mul<P>(z, z, B.Z);
-    llpre_store(tab, 2u * i + 1u, z);
+    llpre_store(scr, 2u * i + 1u, z);
   }
   uint32_t inv[9];
   f_inv_sg<P>(inv, z);
   // D_i -> aux slot t + i; B_(i+1) -> aux slot i + 1
-  ll_affine_back<P>(tab, kLLChain, inv, [](uint32_t c) {
+  ll_affine_back<P>(scr, kLLChain, inv, [](uint32_t c) {
     return (c & 1u) ? kLLAux + (c >> 1) + 1u : kLLAux + kLLTeeth + (c >> 1);
   });
   // 2. L (digits 0 .. a-1) and H (digits a .. t-2 + the top tooth) by two
   //    Gray walks into raw slots [0, NL) and [NL, NL + NH), one product chain,
   //    made affine with one inversion into L / H slots (by Gray index).
-  ll_walk<P>(tab, 0u, kLLA, false, 0u, z, one);
-  ll_walk<P>(tab, (uint32_t)kLLA, kLLTeeth - 1 - kLLA, true, kLLNL, z, one);
+  ll_walk<P>(scr, 0u, kLLA, false, 0u, z, one);
+  ll_walk<P>(scr, (uint32_t)kLLA, kLLTeeth - 1 - kLLA, true, kLLNL, z, one);
   f_inv_sg<P>(inv, z);
-  ll_affine_back<P>(tab, kLLWalk, inv, [](uint32_t c) {
+  ll_affine_back<P>(scr, kLLWalk, inv, [](uint32_t c) {
     return kLLLH + (c < kLLNL ? ll_gray(c) : kLLNL + ll_gray(c - kLLNL));
   });
   // 3. E[m] = H[m >> a] + L[m & (NL - 1)]: affine additions, the denominators
@@ -1422,24 +1426,24 @@ BH_HD void lltab_build(uint32_t* tab, const Work& w, uint32_t rec) {
   uint32_t hx[9], hy[9], lx[9], ly[9], d[9];
 #pragma unroll 1
   for (uint32_t m = 0; m < kLLEnt; m++) {
-    if ((m & (kLLNL - 1u)) == 0u) llaff_load(hx, hy, tab, kLLLH + kLLNL + (m >> kLLA));
-    llaff_load(lx, ly, tab, kLLLH + (m & (kLLNL - 1u)));
+    if ((m & (kLLNL - 1u)) == 0u) llaff_load(hx, hy, scr, kLLLH + kLLNL + (m >> kLLA));
+    llaff_load(lx, ly, scr, kLLLH + (m & (kLLNL - 1u)));
     f_sub<P, 32>(d, hx, lx);                 // [b34], nonzero (H != +-L)
     if (m == 0) f_copy(z, d);
     else f_mul<P>(z, z, d);
-    if (m + 1u < kLLEnt) llpre_store(tab, m, z);
+    if (m + 1u < kLLEnt) llpre_store(scr, m, z);
   }
   f_inv_sg<P>(inv, z);
 #pragma unroll 1
   for (uint32_t m = kLLEnt; m-- > 0;) {
     if (m == kLLEnt - 1u || (m & (kLLNL - 1u)) == kLLNL - 1u)
-      llaff_load(hx, hy, tab, kLLLH + kLLNL + (m >> kLLA));
-    llaff_load(lx, ly, tab, kLLLH + (m & (kLLNL - 1u)));
+      llaff_load(hx, hy, scr, kLLLH + kLLNL + (m >> kLLA));
+    llaff_load(lx, ly, scr, kLLLH + (m & (kLLNL - 1u)));
     f_sub<P, 32>(d, hx, lx);
     uint32_t di[9], lam[9], t[9], x[9], y[9];
     if (m > 0u) {
       uint32_t pre[9];
-      llpre_load(pre, tab, m - 1u);
+      llpre_load(pre, scr, m - 1u);
       f_mul<P>(di, inv, pre);                // (x_H - x_L)^-1
       f_mul<P>(inv, inv, d);
     } else {
@@ -1571,8 +1575,8 @@ BH_HD void reg_build(uint32_t* tab, const Work& w, uint32_t rec) {
   ktab_build_aff<P>(tab, w, rec);
 }
 template <class P>
-BH_HD void reg_build_comb(uint32_t* tab, const Work& w, uint32_t rec) {
-  lltab_build<P>(tab, w, rec);
+BH_HD void reg_build_comb(uint32_t* tab, const Work& w, uint32_t rec, uint32_t* scr = nullptr) {
+  lltab_build<P>(tab, w, rec, scr);
 }
 
 // Curve constants of a base-field class (the order n for u2 + n).

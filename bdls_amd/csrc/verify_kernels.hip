@@ -670,6 +670,10 @@ __global__ __launch_bounds__(kRegWinBlock) void k_reg_win(Work w, Plan pl, KeyRe
   __shared__ uint32_t s_base[kKWin * 27];
   __shared__ uint32_t s_pts[kKEnt * 27 * kKWin];
   __shared__ uint32_t s_zs[kKEnt * 9 * kKWin];
+  // the comb build's scratch at the slot's offsets (the entries' words unused):
+  // LDS instead of the slot's global scratch, whose round trips (~1 us each on a
+  // lone wave) made the build ~2.5x slower than its arithmetic
+  __shared__ __attribute__((aligned(16))) uint32_t s_comb[kLLPre + 12u * kLLEnt];
   const uint32_t t = blockIdx.x;
   const uint32_t nt = min(pl.counters[2], pl.max_tables);
   if (t >= nt) return;  // the whole workgroup
@@ -677,12 +681,20 @@ __global__ __launch_bounds__(kRegWinBlock) void k_reg_win(Work w, Plan pl, KeyRe
   if (id & kLocal) return;  // a per-batch table: no windows
   uint32_t* tab = const_cast<uint32_t*>(tab_ptr(pl, g, id));
   const uint32_t lane = threadIdx.x;
-  if (lane == 128u) reg_build_comb<P>(tab, w, pl.tab_rec[t]);
+  // The record index is workgroup-uniform, so the compiler would run a lone
+  // lane's build on the SALU (scalar 32-bit multiplies: ~3x slower than the
+  // VALU's v_mad_u64_u32, measured in tools/lat_chain.hip); an empty asm with
+  // a VGPR operand makes it a per-lane value and keeps the work on the VALU.
+  uint32_t rec = pl.tab_rec[t];
+  asm volatile("" : "+v"(rec));
+  if (lane == 128u) reg_build_comb<P>(tab, w, rec, s_comb);
   if (lane == 0) {
     J30 B;
-    ld9(B.X, w.qx, pl.tab_rec[t], w.ns);
-    ld9(B.Y, w.qy, pl.tab_rec[t], w.ns);
+    ld9(B.X, w.qx, rec, w.ns);
+    ld9(B.Y, w.qy, rec, w.ns);
     f_const(B.Z, P::r1);
+#pragma unroll
+    for (int k = 0; k < 9; k++) asm volatile("" : "+v"(B.Z[k]));
 #pragma unroll 1
     for (uint32_t win = 0; win < (uint32_t)kKWin; win++) {
 #pragma unroll
