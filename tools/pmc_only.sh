@@ -9,6 +9,6 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU GRBM_GUI_ACTIVE"; do
   rc=$?; [ $rc -eq 0 ] || [ $rc -eq 3 ] || { echo "STOP pmc $grp $rc"; exit $rc; }
 done
 python3 tools/pmc_summary.py gpurun_out gpurun_out/pmc_summary.json --traffic \
-  --workload=config2:n1048576 --source=profiles/r05/v12 \
+  --workload=config2:n1048576 --source=profiles/r05/${PROF_TAG:-v14} \
   --traffic-out=gpurun_out/traffic.json > gpurun_out/pmc_summary.txt 2>&1 || echo "pmc_summary failed"
 echo DONE
