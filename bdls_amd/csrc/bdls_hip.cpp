@@ -499,6 +499,15 @@ uint32_t env_block(const char* name, uint32_t dflt) {
   return (v == 64 || v == 128 || v == 256) ? (uint32_t)v : dflt;
 }
 
+// BH_ROUTE: 0 default, 1 "noreg", 2 "ladder" (see run_dev)
+int env_route() {
+  const char* e = getenv("BH_ROUTE");
+  if (!e) return 0;
+  if (!strcmp(e, "ladder")) return 2;
+  if (!strcmp(e, "noreg")) return 1;
+  return 0;
+}
+
 bh::LaunchOpts launch_opts(size_t m, uint32_t flags) {
   bh::LaunchOpts o;
   // records per inversion lane: ~2 waves per SIMD at 1M records (measured
@@ -601,6 +610,13 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
       const char* e = getenv("BH_LL");
       o.ll_tables = !(e && atoi(e) == 0);
     }
+    // BH_ROUTE (read per call; tests): "noreg" skips the registry lookup,
+    // "ladder" also builds no per-batch table, so every record that reaches
+    // the group equation takes the variable-base ladder
+    const int route = env_route();
+    bh::KeyReg g = d.reg[curve].g;
+    if (route >= 1 && !(flags & BH_F_KEEP_KEYS)) g.cap = 0;
+    if (route >= 2 && !(flags & BH_F_KEEP_KEYS)) o.min_uses = UINT32_MAX;
     o.aux = L.aux;
     o.ev_fork = L.fork;
     o.ev_join = L.join;
@@ -621,7 +637,7 @@ int run_dev(Dev& d, int curve, const B* b, size_t n, uint32_t flags, uint64_t* b
       }
       ev = d.ev_pool[d.ev_used++].data();
     }
-    HIPCHK(launch(curve, slice(b, base, flags), w, pl, d.reg[curve].g, d.gtab[curve],
+    HIPCHK(launch(curve, slice(b, base, flags), w, pl, g, d.gtab[curve],
                   (uint32_t)m, o, bitmap + base / 64, reason + base, s, ev));
     d.last_counters = pl.counters;
     d.last_max_tables = pl.max_tables;
@@ -736,11 +752,15 @@ void share_spans(HostFields& f, bool same) {
   if (!same) return;
   VarField& a = f.var[0];
   VarField& m = f.var[1];
+  // only spans that hold bytes bound the shared copy (an empty span's offset
+  // may lie anywhere, even past the caller's buffer)
   const uint64_t lo = a.bytes ? (m.bytes ? std::min(a.lo, m.lo) : a.lo) : m.lo;
-  const uint64_t hi = std::max(a.lo + a.bytes, m.lo + m.bytes);
+  const uint64_t hi = a.bytes ? (m.bytes ? std::max(a.lo + a.bytes, m.lo + m.bytes)
+                                         : a.lo + a.bytes)
+                              : m.lo + m.bytes;
   f.bytes -= round256(a.bytes + 1) + round256(m.bytes + 1);
   a.lo = m.lo = lo;
-  a.bytes = m.bytes = hi > lo ? hi - lo : 0;
+  a.bytes = m.bytes = (a.bytes || m.bytes) && hi > lo ? hi - lo : 0;
   f.bytes += round256(a.bytes + 1);
   f.shared = true;
 }
@@ -968,6 +988,14 @@ template <class T>
 bool keys_first_ok(const T*) {
   return false;
 }
+// BH_D2H_COPY=1: results by a D2H copy instead of k_result_out (A/B switch)
+bool d2h_copy() {
+  static const bool on = [] {
+    const char* e = getenv("BH_D2H_COPY");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
 bool keys_first() {
   static const bool on = [] {
     const char* e = getenv("BH_KEYS_FIRST");
@@ -1021,7 +1049,7 @@ int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, 
   // engine's later commands -- the next batches' uploads -- until the pass
   // ends (measured: batch k+1's upload started only after batch k's D2H)
   (void)drs;
-  if (getenv("BH_D2H_COPY")) {
+  if (d2h_copy()) {
     HIPCHK(hipMemcpyAsync(sl.host_out.p, dbm, round64(m) / 8 + m, hipMemcpyDeviceToHost, s));
   } else {
     HIPCHK(bh::launch_result_out(dbm, sl.host_out.p, round64(m) / 8 + m, s));
@@ -1133,7 +1161,7 @@ int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, si
   g_dev_records.fetch_add(m, std::memory_order_relaxed);
   HIPCHK(bh::launch_small(curve, in, w, d.reg[curve].g, d.gtab[curve], (uint32_t)m,
                           (uint8_t*)sl.out.p, s, small_block));
-  if (getenv("BH_D2H_COPY")) {
+  if (d2h_copy()) {
     HIPCHK(hipMemcpyAsync(sl.host_out.p, sl.out.p, m, hipMemcpyDeviceToHost, s));
   } else {
     HIPCHK(bh::launch_result_out(sl.out.p, sl.host_out.p, m, s));

@@ -97,9 +97,22 @@ def _alloc_workload(n: int, msg_len: int, alloc) -> Workload:
         cls=np.empty(n, np.uint8))
 
 
+def _gen_fingerprint() -> str:
+    """First 12 hex digits of the generator library's sha256 (a
+    rebuilt generator never reads a cache another build wrote)."""
+    import hashlib
+    if not os.path.exists(_LIB):
+        return "nolib"
+    h = hashlib.sha256()
+    with open(_LIB, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()[:12]
+
+
 def cache_key(n_total, lo, count, nkeys, msg_len, corrupt_den, seed, family="SHA2") -> str:
     return (f"p256_{family}_t{n_total}_lo{lo}_c{count}_k{nkeys}_m{msg_len}_d{corrupt_den}"
-            f"_s{seed}_v1")
+            f"_s{seed}_g{_gen_fingerprint()}_v2")
 
 
 def generate_shard_cached(n_total: int, lo: int, count: int, nkeys: int, msg_len: int = 256,
@@ -129,7 +142,15 @@ def generate_shard_cached(n_total: int, lo: int, count: int, nkeys: int, msg_len
         import json
         with open(meta_path) as f:
             meta = json.load(f)
-        if meta.get("key") == key:
+        sizes = meta.get("sizes") or {}
+        ok = meta.get("key") == key and all(
+            sizes.get(name) == getattr(w, name).nbytes
+            and os.path.getsize(os.path.join(path, name + ".bin")) == getattr(w, name).nbytes
+            for name, _, _ in _FIELDS if os.path.exists(os.path.join(path, name + ".bin")))
+        ok = ok and all(os.path.exists(os.path.join(path, name + ".bin")) for name, _, _ in _FIELDS)
+        if not ok:
+            log(f"cache: {path} does not match this shard / generator, regenerating")
+        if ok:
             for name, _, _ in _FIELDS:
                 a = getattr(w, name)
                 mv = memoryview(a.view(np.uint8).reshape(-1))
@@ -189,7 +210,8 @@ def generate_shard_cached(n_total: int, lo: int, count: int, nkeys: int, msg_len
             getattr(w, name).tofile(os.path.join(path, name + ".bin"))
             log(f"cache: wrote {name}")
         with open(meta_path + ".tmp", "w") as f:
-            json.dump({"key": key, "bytes": need}, f)
+            json.dump({"key": key, "bytes": need,
+                       "sizes": {name: getattr(w, name).nbytes for name, _, _ in _FIELDS}}, f)
         os.replace(meta_path + ".tmp", meta_path)
         info.update(saved=path, save_s=round(__import__("time").time() - t1, 2))
     return w, info

@@ -372,7 +372,9 @@ def ladder_crafted(curve, seed: int = 19, tries: int = 20000, low_s: bool = Fals
     A == -T and 2 A + T == 0, the G groups at weight 2^1 and 2^(1 + kgf)
     doubling / cancelling the partial sum. u1 is drawn, u2 solved from the
     total u1 + u2 d each event needs, kept when u2's own d_0 is the digit
-    assumed (~1/32)."""
+    assumed (~1/32). Every triple has its own d (one event per draw), so a
+    key carries two records (the valid signature and its twin) and stays
+    below kMinUses: no per-batch key table, every record on the ladder."""
     import random
     n = curve.n
     rng = random.Random(seed)
@@ -418,4 +420,75 @@ def ladder_crafted(curve, seed: int = 19, tries: int = 20000, low_s: bool = Fals
                     continue
             found.add(key)
             out.append((u1, u2, d, key, inf))
+            break  # one event per key: a key stays below the table threshold
+    return out
+
+
+def distinct_key_classes(curve, seed: int = 61, reps: int = 4):
+    """The golden file's group-equation classes rebuilt on a fresh key per
+    record (tests/golden/gen_golden.py builds them on shared keys): x(R) in
+    [n, p) accepted through x mod n == r (u1 = 0 as in the golden record, and
+    a random u1), u1 G + u2 Q = infinity, and u1 G == u2 Q (the final addition
+    doubles). Q is solved from the wanted R: Q = u2^-1 (R - u1 G).
+    [(qx, qy, der_sig, digest, expected reason, tag)]; reason 0 verifies,
+    9 = R_MATH (the (false, nil) of verifyNISTEC)."""
+    c = curve
+    n, p = c.n, c.p
+    rng = random.Random(seed)
+    G = (c.gx, c.gy)
+
+    def neg(P):
+        return (P[0], (-P[1]) % p)
+
+    def wrap_point():
+        while True:
+            x = n + rng.randrange(p - n)
+            rhs = (x * x * x + c.a * x + c.b) % p
+            y = pow(rhs, (p + 1) // 4, p)
+            if y * y % p == rhs:
+                return x, y
+
+    def low_s_u2(r):  # u2 with s = r / u2 <= n / 2
+        while True:
+            u2 = rng.randrange(1, n)
+            s = r * pow(u2, -1, n) % n
+            if s <= n // 2:
+                return u2, s
+
+    out = []
+    for _ in range(reps):
+        # x-wrap: R fixed, r = x(R) - n
+        for u1_zero in (True, False):
+            R = wrap_point()
+            r = R[0] - n
+            u2, s = low_s_u2(r)
+            u1 = 0 if u1_zero else rng.randrange(1, n)
+            RmG = R if u1 == 0 else O.point_add(c, R, neg(O.scalar_mult(c, u1, G)))
+            Q = O.scalar_mult(c, pow(u2, -1, n), RmG)
+            e = u1 * s % n
+            sig = O.marshal_ecdsa_signature(r, s)
+            out.append((Q[0], Q[1], sig, e.to_bytes(32, "big"), 0, "xwrap_accept"))
+            R2 = wrap_point()  # R = R2 again, but r = x(R2) - n + 1: its own key
+            r2 = R2[0] - n
+            u2, s = low_s_u2(r2 + 1)
+            Q2 = O.scalar_mult(c, pow(u2, -1, n), R2)
+            out.append((Q2[0], Q2[1], O.marshal_ecdsa_signature(r2 + 1, s), b"\0" * 32, 9,
+                        "xwrap_wrong_r"))
+        # u1 G + u2 Q = infinity: Q = -(u1 / u2) G
+        r = rng.randrange(1, n)
+        u2, s = low_s_u2(r)
+        u1 = rng.randrange(1, n)
+        Q = neg(O.scalar_mult(c, u1 * pow(u2, -1, n) % n, G))
+        out.append((Q[0], Q[1], O.marshal_ecdsa_signature(r, s), (u1 * s % n).to_bytes(32, "big"),
+                    9, "sum_infinity"))
+        # u1 G == u2 Q: Q = (u1 / u2) G, R = 2 u1 G
+        for wrong in (False, True):
+            u1 = rng.randrange(1, n)
+            r = O.scalar_mult(c, 2 * u1 % n, G)[0] % n
+            rr = r if not wrong else (r % (n - 1)) + 1  # the verifier still doubles
+            u2, s = low_s_u2(rr)
+            Q = O.scalar_mult(c, u1 * pow(u2, -1, n) % n, G)
+            out.append((Q[0], Q[1], O.marshal_ecdsa_signature(rr, s),
+                        (u1 * s % n).to_bytes(32, "big"), 9 if wrong else 0,
+                        "u1G_eq_u2Q_wrong_r" if wrong else "u1G_eq_u2Q_accept"))
     return out

@@ -212,23 +212,43 @@ def test_unique_keys_one_pass_of_4m(L):
         assert orc.csp_verify(q, s, dg) == w.reason[i], i
 
 
-def test_ladder_route_crafted_events_p256(L):
-    """Round 5: the one-lane P-256 ladder (verify.h q_ladder_odd_g: odd signed
-    windows, the composite 2 A + T, u1 G folded into the last doublings) on
-    records crafted so that its last window takes every degenerate branch
-    reachable by construction (tests/comb_cases.py ladder_crafted), in a
-    40,960-record batch of distinct keys (every record on the ladder): bitmap
-    and reasons equal the construction, the filler's against the C oracle."""
-    from tests.comb_cases import ladder_crafted
+@pytest.mark.parametrize("route", ["default", "noreg", "ladder"])
+def test_ladder_route_crafted_events_p256(L, golden, route):
+    """The one-lane P-256 ladder (verify.h q_ladder_odd_g: odd signed windows,
+    the composite 2 A + T, u1 G folded into the last doublings) on records
+    crafted so that its last window takes every degenerate branch reachable
+    by construction (tests/comb_cases.py ladder_crafted, one key per event),
+    plus the golden file's x-wrap / infinity / u1 G == u2 Q classes rebuilt on
+    a fresh key each (comb_cases.distinct_key_classes), in a > 32,768-record
+    batch of distinct keys: bitmap and reasons equal the construction (and
+    the C oracle), and EVERY record that reaches the group equation ran on
+    the ladder. route: "default" routing, "noreg"
+    (BH_ROUTE: no registry lookup), "ladder" (no registry, no per-batch
+    tables), the last also carrying every golden record on its shared keys."""
+    from tests.comb_cases import distinct_key_classes, ladder_crafted
     c = O.P256
     kgf = int(os.environ.get("BH_GFOLD", 3))
     recs, want = [], []
     for seed in (43, 44, 45):
-        for qx, qy, sig, dg, exp in records_for_fold(
-                c, ladder_crafted(c, seed=seed, low_s=True, kgf=kgf), low_s=True):
+        trip = ladder_crafted(c, seed=seed, low_s=True, kgf=kgf)
+        assert len(trip) == 9 and len({t[2] for t in trip}) == 9
+        for qx, qy, sig, dg, exp in records_for_fold(c, trip, low_s=True):
             recs.append((qx.to_bytes(32, "big") + qy.to_bytes(32, "big"), sig, dg))
             want.append(exp)
     assert len(recs) >= 3 * 9
+    for qx, qy, sig, dg, exp, _tag in distinct_key_classes(c, seed=61, reps=4):
+        recs.append((qx.to_bytes(32, "big") + qy.to_bytes(32, "big"), sig, dg))
+        want.append(exp)
+    # the crafted records against the C oracle as well
+    assert all(orc.csp_verify(*r) == w for r, w in zip(recs, want))
+    if route == "ladder":  # the golden records keep their shared keys
+        for r in golden:
+            recs.append((bytes.fromhex(r["qx"] + r["qy"]), bytes.fromhex(r["sig"]),
+                         bytes.fromhex(r["digest"])))
+            want.append(r["reason"])
+    keys = [r[0] for r in recs]
+    if route != "ladder":
+        assert len(set(keys)) * 2 >= len(keys)  # <= 2 records per crafted key
     fill = 40_960 - len(recs)
     w = workload.generate(fill, fill, 64, 16, seed=49)  # distinct keys
     for i in range(w.n):
@@ -239,14 +259,19 @@ def test_ladder_route_crafted_events_p256(L):
     want += [int(x) for x in w.reason]
     want = np.array(want, np.uint8)
     n = len(recs)
-    bits, reason, tm = _dev_verify(L, _pack(recs), n)
+    assert n > 32_768
+    if route != "default":
+        os.environ["BH_ROUTE"] = route
+    try:
+        bits, reason, tm = _dev_verify(L, _pack(recs), n)
+    finally:
+        os.environ.pop("BH_ROUTE", None)
     bad = np.nonzero(reason != want)[0]
     assert not len(bad), [(int(i), int(reason[i]), int(want[i])) for i in bad[:10]]
     assert (bits == (want == 0)).all()
-    # (a crafted key that took several events has >= 4 records: a key table)
     math = int(((want == 0) | (want == 9)).sum())
-    assert tm.wide == 1 and tm.n_ladder + tm.n_keycomb == math
-    assert tm.n_ladder >= math - (n - w.n)
+    assert tm.wide == 1 and tm.n_keycomb == 0 and tm.n_keytables == 0
+    assert tm.n_ladder == math
     base = n - w.n
     for i in np.random.default_rng(5).choice(w.n, 100, replace=False):
         q, s, dg = recs[base + i]

@@ -171,7 +171,16 @@ def test_crafted_through_registry(dev, filler):
     c = O.P256
     crafted = [(x, y, sg, dg, 0 if k % 2 == 0 else 9) for k, (x, y, sg, dg) in
                enumerate(records_for_u2(c, signed_comb_u2(c.n, 7, 37), seed=93, low_s=True))]
-    crafted += records_for_fold(c, fold_crafted(c, 7, 37, seed=35, low_s=True), low_s=True)
+    import os
+    from tests.comb_cases import fold_events
+    kgf = int(os.environ.get("BH_GFOLD", 3))  # the library's G group size (verify.h kGF)
+    trip = fold_crafted(c, 7, 37, seed=35, low_s=True, kgf=kgf)
+    # the folded Horner's degenerate branches, as the kernel orders them
+    kinds = {e for u1, u2, d, *_ in trip for e in fold_events(u1, u2, d, c.n, 7, 37, kgf)[0]
+             if e[0] != "from_inf"}
+    assert {("dbl", 0, "G"), ("inf", 0, "G"), ("dbl", 0, "Q"), ("neg", 0, "Q"),
+            ("inf", 0, "Q")} <= kinds, kinds
+    crafted += records_for_fold(c, trip, low_s=True)
     recs = [(x.to_bytes(32, "big") + y.to_bytes(32, "big"), sg, dg) for x, y, sg, dg, _ in crafted]
     want = [e for *_, e in crafted]
     st = register(dev, CURVE_P256, np.frombuffer(b"".join(r[0] for r in recs), np.uint8))

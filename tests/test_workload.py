@@ -56,3 +56,23 @@ def test_config5_shard_chunks_and_cache(tmp_path):
     got = orc.batch_verify(w2.pub.reshape(-1, 64), w2.msg, w2.msg_off, w2.msg_len, w2.sig,
                            w2.sig_off, w2.sig_len, fused=True, nthreads=4)
     assert (got == w2.reason).all()
+
+
+def test_config5_cache_rejects_tampered_copy(tmp_path):
+    """the cache key carries the generator library's fingerprint and
+    meta.json every array's byte count; a copy whose file sizes disagree (a
+    longer file, a foreign write) is regenerated, never loaded."""
+    n_total, lo, count = 1 << 20, 0, 200
+    key = workload.cache_key(n_total, lo, count, n_total, 256, 64, 5)
+    assert "_g" in key and not key.endswith("_gnolib_v2")
+    w, info = workload.generate_shard_cached(n_total, lo, count, n_total, 256, 64, seed=5,
+                                             nthreads=2, cache_dir=str(tmp_path))
+    assert info.get("saved")
+    with open(tmp_path / key / "pub.bin", "ab") as f:  # one byte too many
+        f.write(b"\0")
+    logs = []
+    w2, info2 = workload.generate_shard_cached(n_total, lo, count, n_total, 256, 64, seed=5,
+                                               nthreads=2, cache_dir=str(tmp_path),
+                                               save=False, log=logs.append)
+    assert info2["source"] == "generator" and any("does not match" in m for m in logs)
+    assert (w2.pub == w.pub).all()
