@@ -40,7 +40,7 @@ oracle:
 # test-only host build of the device arithmetic (never linked into the product)
 tests/native/build/libhostsim.so: tests/native/hostsim.cpp $(HDRS)
 	@mkdir -p tests/native/build
-	$(CLANGXX) -O2 -std=c++17 -shared -fPIC -o $@ $<
+	$(CLANGXX) -O2 -std=c++17 -shared -fPIC -o $@ $< -lpthread
 
 # build-kernel experiments (profiles/r02/exp_build): not part of `all`
 EXP_VARIANTS := base:

@@ -34,6 +34,8 @@ EXPORTS = (
     "bh_envelopes_preverify", "bh_block_signatures_preverify",
     "bh_block_signatures_preverify_bft", "bh_fabric_block_preverify_refs", "bh_device_stats",
     "bh_verify_compact", "bh_verify_compact_submit",
+    "bh_batch_verify", "bh_batch_verify_submit", "bh_batch_verify_ptrs",
+    "bh_batch_verify_ptrs_submit", "bh_pack_stats",
 )
 KEY_FULL = 255  # bh_keys_register status: registry full
 
@@ -57,6 +59,18 @@ class BhCBatch(ctypes.Structure):
                 ("nkeys", ctypes.c_size_t), ("sig", ctypes.c_void_p),
                 ("sig_len", ctypes.c_void_p), ("msg", ctypes.c_void_p),
                 ("msg_len", ctypes.c_void_p), ("msg_stride", ctypes.c_uint32)]
+
+
+class BhPBatch(ctypes.Structure):
+    """include/bdls_hip.h bh_pbatch: per-record pointers (the staged
+    BatchVerify's Go-side form)."""
+    _fields_ = [("pub", ctypes.c_void_p), ("sig", ctypes.c_void_p),
+                ("sig_len", ctypes.c_void_p), ("msg", ctypes.c_void_p),
+                ("msg_len", ctypes.c_void_p)]
+
+
+PACK_STATS = ("pass_a_ms", "pass_b_ms", "threads", "chunks", "dedup", "nkeys", "records",
+              "est_distinct", "rebuilds", "shards")
 
 
 class BhBdlsBatch(ctypes.Structure):
@@ -163,6 +177,21 @@ def lib() -> ctypes.CDLL:
             L.bh_verify_compact_submit.argtypes = [i32, ctypes.POINTER(BhCBatch), sz, u32, vp, vp,
                                                    ctypes.POINTER(vp)]
             L.bh_verify_compact_submit.restype = i32
+        except AttributeError:
+            pass
+        try:  # round 6: the staged BatchVerify
+            L.bh_batch_verify.argtypes = [i32, ctypes.POINTER(BhBatch), sz, u32, vp, vp]
+            L.bh_batch_verify.restype = i32
+            L.bh_batch_verify_submit.argtypes = [i32, ctypes.POINTER(BhBatch), sz, u32, vp, vp,
+                                                 ctypes.POINTER(vp)]
+            L.bh_batch_verify_submit.restype = i32
+            L.bh_batch_verify_ptrs.argtypes = [i32, ctypes.POINTER(BhPBatch), sz, u32, vp, vp]
+            L.bh_batch_verify_ptrs.restype = i32
+            L.bh_batch_verify_ptrs_submit.argtypes = [i32, ctypes.POINTER(BhPBatch), sz, u32,
+                                                      vp, vp, ctypes.POINTER(vp)]
+            L.bh_batch_verify_ptrs_submit.restype = i32
+            L.bh_pack_stats.argtypes = [vp]
+            L.bh_pack_stats.restype = i32
         except AttributeError:
             pass
         L.bh_host_alloc.argtypes = [sz, ctypes.POINTER(vp)]
@@ -378,3 +407,11 @@ def compact_layout(pub, sig, sig_off, sig_len, msg, msg_off, msg_len, dedup: boo
                   out["msg_len"].ctypes.data if out["msg_len"] is not None else None,
                   int(msg_len[0]) if fixed else 0)
     return out, cb
+
+
+def pack_stats() -> dict:
+    """bh_pack_stats: the last staged shard's packing (include/bdls_hip.h)."""
+    import numpy as np
+    out = np.zeros(10, np.float64)
+    check(lib().bh_pack_stats(out.ctypes.data))
+    return {k: float(v) for k, v in zip(PACK_STATS, out)}

@@ -27,6 +27,7 @@
 
 #include "../../include/bdls_hip.h"
 #include "verify.h"
+#include "pack.h"
 #include "shard.h"
 
 namespace bh {
@@ -176,6 +177,10 @@ struct Slot {
   HostBuf host_out{nullptr, 0, hipHostMallocPortable | hipHostMallocCoherent};
   hipEvent_t uploaded = nullptr, done = nullptr;
   hipEvent_t keys_up = nullptr;  // the key half of the shard uploaded
+  // staged host batches (bh_batch_verify*): the shard packed by pack.h into
+  // library-owned page-locked memory, reused batch after batch -- keys, key
+  // indices and lengths; signature and message bytes
+  HostBuf pk_small, pk_bytes;
   bh_job* owner = nullptr;  // job whose results are in flight / sit in host_out
   size_t owner_part = 0;
 };
@@ -460,6 +465,8 @@ void dev_free(Dev& d) {
     sl.stage.release();
     sl.out.release();
     sl.host_out.release();
+    sl.pk_small.release();
+    sl.pk_bytes.release();
     if (sl.uploaded) (void)hipEventDestroy(sl.uploaded);
     if (sl.done) (void)hipEventDestroy(sl.done);
   }
@@ -839,6 +846,11 @@ bh_bdls_batch upload(Uploader& u, const bh_bdls_batch* b, size_t lo, size_t m,
 // the compute stream, ahead of the verify passes.
 struct CompactHost {
   bh_cbatch c;
+  // staged shards (pack.h): the signature / message bytes are copied chunk by
+  // chunk while they are packed (upload() only reserves their device range),
+  // and their sums are known (-1: sum the lengths)
+  bool defer_bytes = false;
+  int64_t sig_bytes = -1, msg_bytes = -1;
 };
 struct CompactDev {
   bh_batch b;  // the expanded batch (device pointers)
@@ -861,9 +873,15 @@ HostFields fields(const CompactHost* h, size_t lo, size_t m) {
   const bh_cbatch& c = h->c;
   HostFields f;
   uint64_t s0 = 0, s1 = 0, m0 = 0, m1 = 0;
-  for (size_t i = 0; i < lo; i++) s0 += c.sig_len[i];
-  for (size_t i = lo; i < lo + m; i++) s1 += c.sig_len[i];
-  if (c.msg_len) {
+  if (h->sig_bytes >= 0 && lo == 0) {
+    s1 = (uint64_t)h->sig_bytes;
+  } else {
+    for (size_t i = 0; i < lo; i++) s0 += c.sig_len[i];
+    for (size_t i = lo; i < lo + m; i++) s1 += c.sig_len[i];
+  }
+  if (h->msg_bytes >= 0 && lo == 0) {
+    m1 = (uint64_t)h->msg_bytes;
+  } else if (c.msg_len) {
     for (size_t i = 0; i < lo; i++) m0 += c.msg_len[i];
     for (size_t i = lo; i < lo + m; i++) m1 += c.msg_len[i];
   } else {
@@ -903,8 +921,11 @@ CompactDev upload(Uploader& u, const CompactHost* h, size_t lo, size_t m, const 
   d.sig_len = u.put(c.sig_len + lo, m);
   d.msg_len = c.msg_len ? u.put(c.msg_len + lo, m) : nullptr;
   u.mark();  // keys + lengths: enough for the expansion and the key half of the pass
-  const uint8_t* sig = u.put<uint8_t>(c.sig ? c.sig + f.var[0].lo : nullptr, f.var[0].bytes);
-  const uint8_t* msg = u.put<uint8_t>(c.msg ? c.msg + f.var[1].lo : nullptr, f.var[1].bytes);
+  const bool copy = !h->defer_bytes;
+  const uint8_t* sig =
+      u.put<uint8_t>(c.sig && copy ? c.sig + f.var[0].lo : nullptr, f.var[0].bytes);
+  const uint8_t* msg =
+      u.put<uint8_t>(c.msg && copy ? c.msg + f.var[1].lo : nullptr, f.var[1].bytes);
   d.msg_len_out = c.msg_len ? nullptr : const_cast<uint32_t*>(u.put<uint32_t>(nullptr, m));
   d.pub = idx ? const_cast<uint8_t*>(u.put<uint8_t>(nullptr, m * 64)) : nullptr;
   d.sig_off = const_cast<uint64_t*>(u.put<uint64_t>(nullptr, m));
@@ -1004,12 +1025,11 @@ bool keys_first() {
   return on;
 }
 
-// Enqueue shard [lo, lo + m) on device d (caller holds d.mu).
-template <class B>
-int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, uint32_t flags) {
-  HIPCHK(hipSetDevice(d.id));
-  const int k = (int)(d.next_slot++ % kSlots);
-  Slot& sl = d.slot[k];
+// Take the device's next pipeline slot, collecting the batch that still
+// holds it (caller holds d.mu).
+Slot& take_slot(Dev& d, int* k) {
+  *k = (int)(d.next_slot++ % kSlots);
+  Slot& sl = d.slot[*k];
   if (sl.owner) {  // the slot still holds an uncollected batch: collect it now
     bh_job* o = sl.owner;
     int rc = finish_part(o, sl.owner_part);
@@ -1018,31 +1038,26 @@ int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, 
       o->err = g_err;
     }
   }
-  const HostFields f = fields(b, lo, m);
-  int rc;
-  if ((rc = sl.stage.ensure(f.bytes + 4096))) return rc;
-  const size_t out_bytes = round64(m) / 8 + m + 1024;
-  if ((rc = sl.out.ensure(out_bytes))) return rc;
-  if ((rc = sl.host_out.ensure(out_bytes))) return rc;
-  Uploader u{(char*)sl.stage.p, d.copy, &sl.host_in};
-  // key half first (bh_batch and compact shards of one pass, no registry
-  // writes): the pass imports the keys, plans and builds its tables while the
-  // signatures and messages upload (BH_KEYS_FIRST=0: wait for the whole shard)
-  if (keys_first_ok(b) && !(flags & BH_F_KEEP_KEYS) && m <= max_chunk() && keys_first())
-    u.mark_ev = sl.keys_up;
-  const auto db = upload(u, b, lo, m, f);
-  HIPCHK(u.err);
-  HIPCHK(hipEventRecord(sl.uploaded, d.copy));
+  return sl;
+}
+
+// After a shard's upload is queued on the copy stream (sl.uploaded recorded;
+// keys_marked: sl.keys_up after its key half): the pass on a compute lane and
+// the results into the slot's page-locked buffer.
+template <class D>
+int launch_part(bh_job* j, Dev& d, int k, Slot& sl, int curve, const D& db, size_t lo, size_t m,
+                uint32_t flags, bool keys_marked) {
   // alternate the compute lanes (BH_LANES=1: lane 0 only); registry writers
   // (BH_F_KEEP_KEYS) serialise on lane 0
   const int lane = (flags & BH_F_KEEP_KEYS) ? -1 : (int)(d.next_lane++ % lanes());
   hipStream_t s = lane > 0 ? lane_ref(d, lane).stream : d.stream;
-  HIPCHK(hipStreamWaitEvent(s, u.marked ? sl.keys_up : sl.uploaded, 0));
+  HIPCHK(hipStreamWaitEvent(s, keys_marked ? sl.keys_up : sl.uploaded, 0));
   HIPCHK(expand_dev(db, m, s));
   uint64_t* dbm = (uint64_t*)sl.out.p;
   uint8_t* drs = (uint8_t*)(dbm + round64(m) / 64);
+  int rc;
   if ((rc = run_dev(d, curve, dev_batch(db), m, flags, dbm, drs, s, nullptr, lane,
-                    u.marked ? sl.uploaded : nullptr)))
+                    keys_marked ? sl.uploaded : nullptr)))
     return rc;
   // results: words then reasons, contiguous on both sides. A kernel, not a
   // D2H copy: a copy-engine command that waits on this pass would hold the
@@ -1059,6 +1074,131 @@ int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, 
   sl.owner_part = j->parts.size();
   j->parts.push_back(Part{&d, k, lo, m, false});
   return BH_OK;
+}
+
+// Enqueue shard [lo, lo + m) on device d (caller holds d.mu).
+template <class B>
+int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, uint32_t flags) {
+  HIPCHK(hipSetDevice(d.id));
+  int k;
+  Slot& sl = take_slot(d, &k);
+  const HostFields f = fields(b, lo, m);
+  int rc;
+  if ((rc = sl.stage.ensure(f.bytes + 4096))) return rc;
+  const size_t out_bytes = round64(m) / 8 + m + 1024;
+  if ((rc = sl.out.ensure(out_bytes))) return rc;
+  if ((rc = sl.host_out.ensure(out_bytes))) return rc;
+  Uploader u{(char*)sl.stage.p, d.copy, &sl.host_in};
+  // key half first (bh_batch and compact shards of one pass, no registry
+  // writes): the pass imports the keys, plans and builds its tables while the
+  // signatures and messages upload (BH_KEYS_FIRST=0: wait for the whole shard)
+  if (keys_first_ok(b) && !(flags & BH_F_KEEP_KEYS) && m <= max_chunk() && keys_first())
+    u.mark_ev = sl.keys_up;
+  const auto db = upload(u, b, lo, m, f);
+  HIPCHK(u.err);
+  HIPCHK(hipEventRecord(sl.uploaded, d.copy));
+  return launch_part(j, d, k, sl, curve, db, lo, m, flags, u.marked);
+}
+
+// ---- staged host batches (bh_batch_verify*, pack.h) ---------------------------
+// Record accessors over the caller's buffers: the SoA bh_batch (offsets into
+// one signature and one message buffer) and the per-record pointer form
+// bh_pbatch. A NULL pointer in the latter is a zero-length field (Go's nil
+// slice); a NULL key pointer reads as the all-zero point (BH_R_BAD_KEY).
+struct SrcPlain {
+  const bh_batch* b;
+  const uint8_t* key(size_t i) const { return b->pub + i * 64; }
+  const uint8_t* sig(size_t i) const { return b->sig + b->sig_off[i]; }
+  uint32_t sig_len(size_t i) const { return b->sig_len[i]; }
+  const uint8_t* msg(size_t i) const { return b->msg + b->msg_off[i]; }
+  uint32_t msg_len(size_t i) const { return b->msg_len[i]; }
+};
+const uint8_t kZeroKey[64] = {0};
+struct SrcPtrs {
+  const bh_pbatch* b;
+  const uint8_t* key(size_t i) const { return b->pub[i] ? b->pub[i] : kZeroKey; }
+  const uint8_t* sig(size_t i) const { return b->sig[i]; }
+  uint32_t sig_len(size_t i) const { return b->sig[i] ? b->sig_len[i] : 0u; }
+  const uint8_t* msg(size_t i) const { return b->msg[i]; }
+  uint32_t msg_len(size_t i) const { return b->msg[i] ? b->msg_len[i] : 0u; }
+};
+
+// one packer (worker pool) per process; one staged shard packs at a time
+std::mutex g_pack_mu;
+bh::pack::Packer& packer() {
+  static bh::pack::Packer* p = new bh::pack::Packer(bh::pack::default_threads());
+  return *p;
+}
+struct PackStats {
+  double a_ms = 0, b_ms = 0, est = 0;
+  uint64_t shards = 0, nkeys = 0, m = 0;
+  int threads = 0, chunks = 0, dedup = 0, rebuilds = 0;
+} g_pack_stats;
+
+// Pack shard [lo, lo + m) of src into slot k's page-locked buffers (pass A:
+// keys + indices + lengths), queue that key half's H2D, then pack the bytes
+// chunk by chunk (pass B), each chunk's H2D queued as soon as it is complete,
+// and launch the pass. Caller holds d.mu.
+template <class Src>
+int enqueue_staged(bh_job* j, Dev& d, int curve, const Src& src, size_t lo, size_t m,
+                   uint32_t flags) {
+  HIPCHK(hipSetDevice(d.id));
+  int k;
+  Slot& sl = take_slot(d, &k);
+  int rc;
+  const size_t o_idx = round256(m * 64), o_slen = o_idx + round256(m * 4),
+               o_mlen = o_slen + round256(m * 4), small_bytes = o_mlen + round256(m * 4);
+  if ((rc = sl.pk_small.ensure(small_bytes))) return rc;
+  char* hs = (char*)sl.pk_small.p;
+  bh::pack::Out out{(uint8_t*)hs, (uint32_t*)(hs + o_idx), (uint32_t*)(hs + o_slen),
+                    (uint32_t*)(hs + o_mlen)};
+  std::lock_guard<std::mutex> pg(g_pack_mu);
+  bh::pack::Packer& P = packer();
+  bh::pack::Result r;
+  P.pass_a(src, lo, m, out, &r);
+  const size_t o_msg = round256(r.sig_bytes + 1);
+  if ((rc = sl.pk_bytes.ensure(o_msg + r.msg_bytes + 256))) return rc;
+  uint8_t* hsig = (uint8_t*)sl.pk_bytes.p;
+  uint8_t* hmsg = hsig + o_msg;
+  CompactHost h;
+  h.c = bh_cbatch{out.keys, r.dedup ? out.key_idx : nullptr, r.nkeys, hsig, out.sig_len, hmsg,
+                  r.fixed_msg ? nullptr : out.msg_len, r.msg_stride};
+  h.defer_bytes = true;
+  h.sig_bytes = (int64_t)r.sig_bytes;
+  h.msg_bytes = (int64_t)r.msg_bytes;
+  const HostFields f = fields(&h, 0, m);
+  if ((rc = sl.stage.ensure(f.bytes + 4096))) return rc;
+  const size_t out_bytes = round64(m) / 8 + m + 1024;
+  if ((rc = sl.out.ensure(out_bytes))) return rc;
+  if ((rc = sl.host_out.ensure(out_bytes))) return rc;
+  Uploader u{(char*)sl.stage.p, d.copy, &sl.host_in};
+  if (!(flags & BH_F_KEEP_KEYS) && m <= max_chunk() && keys_first()) u.mark_ev = sl.keys_up;
+  const CompactDev db = upload(u, &h, 0, m, f);
+  HIPCHK(u.err);
+  uint8_t* dsig = const_cast<uint8_t*>(db.b.sig);
+  uint8_t* dmsg = const_cast<uint8_t*>(db.b.msg);
+  hipError_t ce = hipSuccess;
+  P.pass_b(src, hsig, hmsg, &r, [&](int c) {
+    const uint64_t s0 = r.sig_chunk[c], s1 = r.sig_chunk[c + 1];
+    const uint64_t m0 = r.msg_chunk[c], m1 = r.msg_chunk[c + 1];
+    if (ce == hipSuccess && s1 > s0)
+      ce = hipMemcpyAsync(dsig + s0, hsig + s0, s1 - s0, hipMemcpyHostToDevice, d.copy);
+    if (ce == hipSuccess && m1 > m0)
+      ce = hipMemcpyAsync(dmsg + m0, hmsg + m0, m1 - m0, hipMemcpyHostToDevice, d.copy);
+  });
+  HIPCHK(ce);
+  HIPCHK(hipEventRecord(sl.uploaded, d.copy));
+  g_pack_stats.a_ms = r.a_ms;
+  g_pack_stats.b_ms = r.b_ms;
+  g_pack_stats.est = r.est_distinct;
+  g_pack_stats.shards++;
+  g_pack_stats.nkeys = r.nkeys;
+  g_pack_stats.m = m;
+  g_pack_stats.threads = P.threads();
+  g_pack_stats.chunks = r.nchunks;
+  g_pack_stats.dedup = r.dedup;
+  g_pack_stats.rebuilds = r.rebuilds;
+  return launch_part(j, d, k, sl, curve, db, lo, m, flags, u.marked);
 }
 
 // ---- latency path ------------------------------------------------------------
@@ -1079,7 +1219,8 @@ bool small_ok(int, const SegBatch*, size_t, uint32_t) { return false; }
 bool small_ok(int, const bh_bdls_batch*, size_t, uint32_t) { return false; }
 bool small_ok(int, const CompactHost*, size_t, uint32_t) { return false; }
 
-int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, size_t m,
+template <class Src>
+int enqueue_small(bh_job* j, Dev& d, int curve, const Src& b, size_t lo, size_t m,
                   uint32_t flags) {
   HIPCHK(hipSetDevice(d.id));
   const int k = (int)(d.next_slot++ % kSlots);
@@ -1095,8 +1236,8 @@ int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, si
   // layout: pub | sig_off | sig_len | msg_off | msg_len | sig bytes | msg bytes
   size_t sig_bytes = 0, msg_bytes = 0;
   for (size_t i = lo; i < lo + m; i++) {
-    sig_bytes += b->sig_len[i];
-    msg_bytes += b->msg_len[i];
+    sig_bytes += b.sig_len(i);
+    msg_bytes += b.msg_len(i);
   }
   const size_t o_pub = 0, o_soff = round256(m * 64), o_slen = o_soff + round256(m * 8),
                o_moff = o_slen + round256(m * 4), o_mlen = o_moff + round256(m * 8),
@@ -1107,21 +1248,21 @@ int enqueue_small(bh_job* j, Dev& d, int curve, const bh_batch* b, size_t lo, si
       (rc = sl.out.ensure(m + 256)) || (rc = sl.host_out.ensure(m + 256)))
     return rc;
   char* h = (char*)sl.host_in.p;
-  std::memcpy(h + o_pub, b->pub + lo * 64, m * 64);
+  for (size_t i = 0; i < m; i++) std::memcpy(h + o_pub + i * 64, b.key(lo + i), 64);
   uint64_t* soff = (uint64_t*)(h + o_soff);
   uint32_t* slen = (uint32_t*)(h + o_slen);
   uint64_t* moff = (uint64_t*)(h + o_moff);
   uint32_t* mlen = (uint32_t*)(h + o_mlen);
   size_t sp = 0, mp = 0;
   for (size_t i = 0; i < m; i++) {
-    const size_t sl_ = b->sig_len[lo + i], ml = b->msg_len[lo + i];
+    const size_t sl_ = b.sig_len(lo + i), ml = b.msg_len(lo + i);
     soff[i] = sp;
     slen[i] = (uint32_t)sl_;
-    if (sl_) std::memcpy(h + o_sig + sp, b->sig + b->sig_off[lo + i], sl_);
+    if (sl_) std::memcpy(h + o_sig + sp, b.sig(lo + i), sl_);
     sp += sl_;
     moff[i] = mp;
     mlen[i] = (uint32_t)ml;
-    if (ml) std::memcpy(h + o_msg + mp, b->msg + b->msg_off[lo + i], ml);
+    if (ml) std::memcpy(h + o_msg + mp, b.msg(lo + i), ml);
     mp += ml;
   }
   // Small batches rotate over the compute lanes like host batches:
@@ -1233,7 +1374,8 @@ int submit_job(int curve, const B* b, size_t n, uint32_t flags, uint8_t* bitmap,
     int rc;
     {
       std::lock_guard<std::mutex> g(d.mu);
-      rc = enqueue_small(j, d, curve, reinterpret_cast<const bh_batch*>(b), 0, n, flags);
+      rc = enqueue_small(j, d, curve, SrcPlain{reinterpret_cast<const bh_batch*>(b)}, 0, n,
+                         flags);
     }
     if (rc) {
       const std::string err = g_err;
@@ -1276,6 +1418,47 @@ int host_verify(int curve, const B* b, size_t n, uint32_t flags, uint8_t* bitmap
   int rc = submit_job(curve, b, n, flags, bitmap, reason, &j);
   if (rc) return rc;
   return wait_job(j);
+}
+
+// Staged host batch (bh_batch_verify*): shards as submit_job deals them, each
+// packed into its slot's page-locked buffers by pack.h; small batches take the
+// latency path (which packs on the host anyway).
+template <class Src>
+int submit_staged(int curve, const Src& src, size_t n, uint32_t flags, uint8_t* bitmap,
+                  uint8_t* reason, bh_job** out) {
+  *out = nullptr;
+  std::vector<Dev*> devs = all_devs();
+  if (devs.empty()) return fail(BH_E_NOT_INIT, "bh_init not called");
+  bh_job* j = new bh_job();
+  j->bitmap = bitmap;
+  j->reason = reason;
+  j->n = n;
+  if (n) std::memset(bitmap, 0, (n + 7) / 8);
+  const bool small = curve == BH_CURVE_P256 && n && n <= kSmallMax &&
+                     !(flags & BH_F_KEEP_KEYS) && !getenv("BH_NO_SMALL");
+  size_t per = 1;
+  if (const char* e = getenv("BH_HOST_SHARDS")) per = (size_t)std::max(1, std::min(atoi(e), kSlots));
+  const size_t nd = small ? 1 : bh::shard_devices(n, devs.size() * per);
+  static std::atomic<uint32_t> rr{0};
+  const size_t first = small ? rr++ % devs.size() : 0;
+  for (size_t k = 0; k < nd; k++) {
+    const bh::Shard sh = small ? bh::Shard{0, n} : bh::shard_of(n, nd, k);
+    if (!sh.len) break;
+    Dev& d = *devs[(first + k) % devs.size()];
+    int rc;
+    {
+      std::lock_guard<std::mutex> g(d.mu);
+      rc = small ? enqueue_small(j, d, curve, src, 0, n, flags)
+                 : enqueue_staged(j, d, curve, src, sh.lo, sh.len, flags);
+    }
+    if (rc) {
+      const std::string err = g_err;
+      (void)wait_job(j);
+      return fail(rc, err);
+    }
+  }
+  *out = j;
+  return BH_OK;
 }
 
 int check_curve(int curve) {
@@ -1732,6 +1915,61 @@ int bh_verify_compact_submit(int curve, const bh_cbatch* b, size_t n, uint32_t f
   if (int rc = check_compact(b, n, bitmap, reason)) return rc;
   const CompactHost h{*b};
   return submit_job(curve, &h, n, flags, bitmap, reason, job);
+}
+
+// ---- staged BatchVerify (pack.h) ----
+static int check_staged(int curve, uint32_t flags, size_t n) {
+  if (curve != BH_CURVE_P256) return fail(BH_E_INVALID, "curve not supported by bh_batch_verify");
+  if (int rc = check_flags(flags)) return rc;
+  if (n > 0xffffffffull) return fail(BH_E_INVALID, "batch too large");
+  return BH_OK;
+}
+
+int bh_batch_verify_submit(int curve, const bh_batch* b, size_t n, uint32_t flags,
+                           uint8_t* bitmap, uint8_t* reason, bh_job** job) {
+  if (!job) return fail(BH_E_INVALID, "null job");
+  *job = nullptr;
+  if (!b || (n && (!b->pub || !b->sig_off || !b->sig_len || !b->msg_off || !b->msg_len ||
+                   !bitmap || !reason)))
+    return fail(BH_E_INVALID, "null pointer in batch");
+  if (int rc = check_staged(curve, flags, n)) return rc;
+  return submit_staged(curve, SrcPlain{b}, n, flags, bitmap, reason, job);
+}
+
+int bh_batch_verify(int curve, const bh_batch* b, size_t n, uint32_t flags, uint8_t* bitmap,
+                    uint8_t* reason) {
+  bh_job* j = nullptr;
+  if (int rc = bh_batch_verify_submit(curve, b, n, flags, bitmap, reason, &j)) return rc;
+  return wait_job(j);
+}
+
+int bh_batch_verify_ptrs_submit(int curve, const bh_pbatch* b, size_t n, uint32_t flags,
+                                uint8_t* bitmap, uint8_t* reason, bh_job** job) {
+  if (!job) return fail(BH_E_INVALID, "null job");
+  *job = nullptr;
+  if (!b || (n && (!b->pub || !b->sig || !b->sig_len || !b->msg || !b->msg_len || !bitmap ||
+                   !reason)))
+    return fail(BH_E_INVALID, "null pointer in batch");
+  if (int rc = check_staged(curve, flags, n)) return rc;
+  return submit_staged(curve, SrcPtrs{b}, n, flags, bitmap, reason, job);
+}
+
+int bh_batch_verify_ptrs(int curve, const bh_pbatch* b, size_t n, uint32_t flags,
+                         uint8_t* bitmap, uint8_t* reason) {
+  bh_job* j = nullptr;
+  if (int rc = bh_batch_verify_ptrs_submit(curve, b, n, flags, bitmap, reason, &j)) return rc;
+  return wait_job(j);
+}
+
+int bh_pack_stats(double out[10]) {
+  if (!out) return fail(BH_E_INVALID, "null out");
+  std::lock_guard<std::mutex> g(g_pack_mu);
+  const PackStats& p = g_pack_stats;
+  const double v[10] = {p.a_ms, p.b_ms, (double)p.threads, (double)p.chunks, (double)p.dedup,
+                        (double)p.nkeys, (double)p.m, p.est, (double)p.rebuilds,
+                        (double)p.shards};
+  std::memcpy(out, v, sizeof(v));
+  return BH_OK;
 }
 
 int bh_verify_wait(bh_job* job) {

@@ -160,6 +160,9 @@ def parse(argv=None):
     ap.add_argument("--host-layout", choices=["compact", "plain"], default="compact",
                     help="host path input layout: bh_cbatch (distinct keys + u32 indices, "
                          "lengths only) or bh_batch (per-record keys, u64 offsets)")
+    ap.add_argument("--e2e", type=int, default=1,
+                    help="time host_path_e2e: the staged BatchVerify (bh_batch_verify_submit) "
+                         "from pageable generator arrays, packing inside the timed region")
     ap.add_argument("--resident-lanes", type=int, default=1,
                     help="timed resident passes rotate over the compute lanes (BH_F_ANY_LANE)")
     ap.add_argument("--hbm-resident", type=int, default=1,
@@ -591,6 +594,98 @@ def cpu_baseline(a, w, n):
     }
 
 
+def measure_e2e(a, L, w, n, flags, local, world, depth, h2d_gbps):
+    """host_path_e2e: K BatchVerify calls through bh_batch_verify_submit /
+    bh_verify_wait from PAGEABLE arrays (the generator's, copied into ordinary
+    numpy memory), up to `depth` in flight. Timed: everything per batch --
+    the library's key dedup + packing into its page-locked ring (pack.h),
+    the H2D, the pass, the results. Its PCIe bound counts the bytes the staged
+    path uploads (the compact layout it builds: distinct keys + u32 indices,
+    lengths, signature and message bytes)."""
+    from collections import deque
+
+    from bdls_amd import _lib, dist
+    phase("host_path_e2e: pageable copies of the batch")
+    arrs = [np.array(x, copy=True) for x in w.arrays()]  # ordinary (pageable) memory
+    b = _lib.BhBatch(*[x.ctypes.data for x in arrs])
+    outs = [(np.zeros((n + 7) // 8, np.uint8), np.zeros(n, np.uint8)) for _ in range(depth)]
+
+    acc = {"submit_s": 0.0, "wait_s": 0.0}
+
+    def run(steps):
+        q = deque()
+        pc = time.perf_counter
+        for k in range(steps):
+            if len(q) == depth:
+                t = pc()
+                _lib.check(L.bh_verify_wait(q.popleft()))
+                acc["wait_s"] += pc() - t
+            bm, rs = outs[k % depth]
+            job = ctypes.c_void_p()
+            t = pc()
+            _lib.check(L.bh_batch_verify_submit(0, ctypes.byref(b), n, flags, bm.ctypes.data,
+                                                rs.ctypes.data, ctypes.byref(job)))
+            acc["submit_s"] += pc() - t
+            q.append(job)
+        t = pc()
+        while q:
+            _lib.check(L.bh_verify_wait(q.popleft()))
+        acc["wait_s"] += pc() - t
+
+    run(max(1, a.warmup))
+    _lib.check(L.bh_sync(local))
+    # one call alone: a BatchVerify's latency (pack + upload + pass + results)
+    t = time.perf_counter()
+    run(1)
+    single_ms = (time.perf_counter() - t) * 1e3
+    st1 = _lib.pack_stats()
+    dist.barrier(world)
+    shards0 = st1["shards"]
+    phase(f"host_path_e2e: {a.steps} timed batches")
+    acc.update(submit_s=0.0, wait_s=0.0)
+    t0 = time.perf_counter()
+    run(a.steps)
+    t1 = time.perf_counter()
+    st = _lib.pack_stats()
+    dist.barrier(world)
+    elapsed = dist.max_over_ranks(t1 - t0, world)
+    bm, rs = outs[(a.steps - 1) % depth]
+    bits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    ok = bool((rs == w.reason).all() and (bits == w.expected_valid).all())
+    # bytes the staged path uploads per batch (its compact layout)
+    nk = int(st["nkeys"])
+    fixed = bool((w.msg_len == w.msg_len[0]).all()) if n else True
+    up_bytes = (nk * 64 + (4 * n if st["dedup"] else 0) + 4 * n + (0 if fixed else 4 * n)
+                + int(w.sig_len.sum()) + int(w.msg_len.sum()))
+    value = dist.sum_over_ranks(n, world) * a.steps / elapsed
+    pcie_bound = world * n * h2d_gbps * 1e9 / up_bytes
+    ms = elapsed * 1e3 / a.steps
+    pack_ms = st["pass_a_ms"] + st["pass_b_ms"]
+    phase(f"host_path_e2e: {ms:.2f} ms per batch ({value / 1e6:.1f} M/s), pack "
+          f"{pack_ms:.2f} ms on {int(st['threads'])} threads, parity {ok}")
+    return {"value": round(value, 1), "ms_per_step": round(ms, 3), "parity": ok,
+            "what": ("bh_batch_verify_submit / bh_verify_wait over the generator's batch copied "
+                     "into pageable memory, up to %d in flight; timed per batch: key dedup + "
+                     "packing into the library's reused page-locked staging (pack.h worker "
+                     "pool), chunked H2D, the pass, results -- no untimed per-batch step" % depth),
+            "single_batch_ms": round(single_ms, 3),
+            "submit_ms_per_batch": round(acc["submit_s"] * 1e3 / a.steps, 3),
+            "wait_ms_per_batch": round(acc["wait_s"] * 1e3 / a.steps, 3),
+            "upload_bytes_per_batch": up_bytes,
+            "pcie_bound_verifies_per_s": round(pcie_bound, 1),
+            "pcie_frac": round(value / pcie_bound, 3),
+            "pack": {"pass_a_ms": round(st["pass_a_ms"], 3), "pass_b_ms": round(st["pass_b_ms"], 3),
+                     "threads": int(st["threads"]), "chunks": int(st["chunks"]),
+                     "dedup": bool(st["dedup"]), "keys_uploaded": nk,
+                     "est_distinct": round(st["est_distinct"], 1),
+                     "batches": int(st["shards"] - shards0),
+                     "note": "the last timed batch's passes (wall time on the submitting "
+                             "thread; pass B's H2D copies run under it)"},
+            "per_batch_ms": {"pack_cpu": round(pack_ms, 3),
+                             "pcie": round(up_bytes / (h2d_gbps * 1e9) * 1e3, 3)},
+            }
+
+
 def bench_throughput(a, rank, world, local):
     from bdls_amd import _lib, dist, workload
     if a.config == 5:
@@ -749,6 +844,16 @@ def bench_throughput(a, rank, world, local):
     bits = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
     parity_ok = bool((rs == w.reason).all() and (bits == w.expected_valid).all())
 
+    # host_path_e2e: what a Go BatchVerify caller gets --
+    # the records in ordinary pageable memory (copies of the generator's
+    # arrays), and every per-batch host step inside the timed region: the
+    # library's key de-duplication and packing into its own reused page-locked
+    # staging (pack.h worker pool), the chunked H2D, the pass, the results
+    e2e = None
+    if a.e2e and a.config != 5:
+        e2e = measure_e2e(a, L, w, n, flags, local, world, depth, h2d_gbps)
+        parity_ok = parity_ok and e2e["parity"]
+
     # the same passes on inputs already resident in HBM (no PCIe in the loop).
     # Timed: K passes rotating over the compute lanes (BH_F_ANY_LANE; one
     # output set per possible lane, so no in-flight pass shares its outputs),
@@ -807,6 +912,12 @@ def bench_throughput(a, rank, world, local):
         for x in d + [y for pair in outs_dev for y in pair]:
             x.free()
     parity_ok = dist.all_true(parity_ok, world)
+    if e2e:
+        # what bounds it: the longest per-batch stage of the three that overlap
+        pb = e2e["per_batch_ms"]
+        if resident:
+            pb["gpu_resident"] = resident["ms_per_step"]
+        e2e["bound"] = max(pb, key=pb.get)
     kern = {k: getattr(tm, k) for k in _lib.BhTiming.STAGES}
     routes = {"keycomb": tm.n_keycomb, "ladder": tm.n_ladder, "key_tables": tm.n_keytables}
 
@@ -878,6 +989,7 @@ def bench_throughput(a, rank, world, local):
                       "pcie_frac": round(host_value / (world * n * h2d_gbps * 1e9 / batch_bytes), 3),
                       "note": "value amortises the first batch's upload (pipeline fill) "
                               "over --steps batches"},
+        "host_path_e2e": e2e,
         "kernel_ms_per_step": {k: round(v / a.steps, 3) for k, v in kern.items()},
         "kernel_ms_source": ("K serialised HBM-resident passes (bh_verify_dev, HIP events) run "
                              "after the timed ones" if a.hbm_resident

@@ -210,6 +210,54 @@ int bh_verify_compact(int curve, const bh_cbatch *b, size_t n, uint32_t flags, u
 int bh_verify_compact_submit(int curve, const bh_cbatch *b, size_t n, uint32_t flags,
                              uint8_t *bitmap, uint8_t *reason, bh_job **job);
 
+/* ---- Staged BatchVerify (round 6) ------------------------------------------
+ * BatchVerify straight from the caller's own (pageable, per-record) buffers:
+ * the library packs each shard into page-locked staging it owns and reuses
+ * (pipeline slot buffers), on a pool of worker threads -- key de-duplication
+ * by a lock-free hash table (each distinct key uploaded once + a u32 index per
+ * record, the compact layout), lengths, and the signature and message bytes,
+ * the latter in chunks whose H2D copies start while the next chunk is packed;
+ * the device pass plans and builds its key tables while the bytes upload.
+ * Replaces the per-call packing a Go BatchVerify did on one goroutine into a
+ * fresh bh_host_alloc (INTEGRATION.md 2 packBatch) -- the batch points
+ * common/policies/policy.go:363-395 and core/committer/txvalidator/v20/
+ * validator.go:193-208 -- and the per-call bh_host_alloc/free. Results,
+ * flags, curve (BH_CURVE_P256) and job handles as bh_verify_submit (collect
+ * with bh_verify_wait); the caller's buffers must stay valid until the
+ * submit call RETURNS (everything is copied by then), not until the wait.
+ * Worker threads: BH_PACK_THREADS, default the CPUs the process may use
+ * (affinity, cgroup quota) less one, at most 15. */
+int bh_batch_verify(int curve, const bh_batch *b, size_t n, uint32_t flags, uint8_t *bitmap,
+                    uint8_t *reason);
+int bh_batch_verify_submit(int curve, const bh_batch *b, size_t n, uint32_t flags,
+                           uint8_t *bitmap, uint8_t *reason, bh_job **job);
+/* The same records as separate caller buffers -- the form a cgo binding
+ * hands over without flattening in Go (pointers pinned with runtime.Pinner,
+ * Go >= 1.21): per record its 64-byte key X || Y, its DER signature and its
+ * message (BH_F_HASH_*) or digest. A NULL signature / message pointer is a
+ * zero-length field (Go's nil slice: BH_R_EMPTY_SIG / BH_R_EMPTY_DIGEST or the
+ * hash of the empty message); a NULL key pointer reads as the all-zero point
+ * (BH_R_BAD_KEY). Records sharing a key may pass the same pointer or equal
+ * bytes: the library de-duplicates by content. */
+typedef struct bh_pbatch {
+  const uint8_t *const *pub;  /* n pointers to 64 bytes Q.x || Q.y                 */
+  const uint8_t *const *sig;  /* n pointers to DER signatures                     */
+  const uint32_t *sig_len;
+  const uint8_t *const *msg;  /* n pointers to messages (BH_F_HASH_*) or digests  */
+  const uint32_t *msg_len;
+} bh_pbatch;
+int bh_batch_verify_ptrs(int curve, const bh_pbatch *b, size_t n, uint32_t flags,
+                         uint8_t *bitmap, uint8_t *reason);
+int bh_batch_verify_ptrs_submit(int curve, const bh_pbatch *b, size_t n, uint32_t flags,
+                                uint8_t *bitmap, uint8_t *reason, bh_job **job);
+/* The last staged shard's packing: out[0] pass A ms (keys, indices, lengths),
+ * [1] pass B ms (bytes, H2D copies queued per chunk), [2] worker threads,
+ * [3] chunks, [4] keys de-duplicated (1/0), [5] keys uploaded, [6] records,
+ * [7] the sample's distinct-key estimate (0: no repeat seen), [8] table
+ * rebuilds, [9] staged shards since start. Not in the reference
+ * (operations metrics). */
+int bh_pack_stats(double out[10]);
+
 /* Device batches since bh_init over every entry point: out[0] batches launched
  * (one per device pass sequence of a call or shard, one per latency-path
  * batch), out[1] records they carried. Lets a consumer prove it issued no

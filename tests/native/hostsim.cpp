@@ -10,6 +10,7 @@
 
 #include "../../bdls_amd/csrc/verify.h"
 #include "../../bdls_amd/csrc/shard.h"
+#include "../../bdls_amd/csrc/pack.h"
 
 using namespace bh;
 
@@ -331,4 +332,72 @@ extern "C" int hs_shard_check(size_t n, size_t ndev, const uint8_t* valid, size_
   if (memcmp(want.data(), got.data(), want.size())) return 6;  // merged bitmap differs
   *nshards = used;
   return 0;
+}
+
+// ---- staged BatchVerify packing (bdls_amd/csrc/pack.h) ------------------------
+// Packs records [lo, lo + m) of a SoA batch exactly as bdls_hip.cpp
+// enqueue_staged does (pass A then pass B with the per-chunk callback).
+// force: -1 the sample decides, 0 / 1 de-duplication off / on. info[0..7] =
+// nkeys, dedup, fixed_msg, msg_stride, sig_bytes, msg_bytes, nchunks, rebuilds,
+// [8..9] pass A / pass B microseconds;
+// bounds: the chunk byte bounds (sig then msg, nchunks + 1 each) in the order
+// the callback saw them complete. Returns -1 when a chunk was reported before
+// its bytes were all written or out of order.
+struct HsSrc {
+  const uint8_t *pub, *sig, *msg;
+  const uint64_t *sig_off, *msg_off;
+  const uint32_t *sig_len, *msg_len;
+  const uint8_t* key(size_t i) const { return pub + i * 64; }
+  const uint8_t* sig_(size_t i) const { return sig + sig_off[i]; }
+};
+struct HsSrcA {
+  const HsSrc* s;
+  const uint8_t* key(size_t i) const { return s->key(i); }
+  const uint8_t* sig(size_t i) const { return s->sig_(i); }
+  uint32_t sig_len(size_t i) const { return s->sig_len[i]; }
+  const uint8_t* msg(size_t i) const { return s->msg + s->msg_off[i]; }
+  uint32_t msg_len(size_t i) const { return s->msg_len[i]; }
+};
+extern "C" int hs_pack(const uint8_t* pub, const uint8_t* sig, const uint64_t* sig_off,
+                       const uint32_t* sig_len, const uint8_t* msg, const uint64_t* msg_off,
+                       const uint32_t* msg_len, size_t lo, size_t m, int threads, int force,
+                       uint8_t* keys, uint32_t* key_idx, uint32_t* slen, uint32_t* mlen,
+                       uint8_t* sig_out, uint8_t* msg_out, uint64_t* info, uint64_t* bounds) {
+  static bh::pack::Packer* P[65] = {nullptr};
+  threads = std::max(1, std::min(64, threads));
+  if (!P[threads]) P[threads] = new bh::pack::Packer(threads);
+  HsSrc src{pub, sig, msg, sig_off, msg_off, sig_len, msg_len};
+  HsSrcA a{&src};
+  bh::pack::Out out{keys, key_idx, slen, mlen};
+  bh::pack::Result r;
+  P[threads]->pass_a(a, lo, m, out, &r, force);
+  int next = 0, bad = 0;
+  static const bool nocheck = getenv("HS_PACK_NOCHECK") != nullptr;  // tools/pack_bench.py
+  P[threads]->pass_b(a, sig_out, msg_out, &r, [&](int c) {
+    if (c != next++) bad = 1;
+    if (nocheck) return;
+    // every record of chunk c is in place when its callback runs
+    const size_t K = (size_t)r.nchunks, ca = (m * c) / K, cb = (m * (c + 1)) / K;
+    uint64_t so = r.sig_chunk[c], mo = r.msg_chunk[c];
+    for (size_t i = ca; i < cb; i++) {
+      if (sig_len[lo + i] && memcmp(sig_out + so, sig + sig_off[lo + i], sig_len[lo + i])) bad = 1;
+      if (msg_len[lo + i] && memcmp(msg_out + mo, msg + msg_off[lo + i], msg_len[lo + i])) bad = 1;
+      so += sig_len[lo + i];
+      mo += msg_len[lo + i];
+    }
+    if (so != r.sig_chunk[c + 1] || mo != r.msg_chunk[c + 1]) bad = 1;
+  });
+  const uint64_t v[10] = {r.nkeys, (uint64_t)r.dedup, (uint64_t)r.fixed_msg, r.msg_stride,
+                          r.sig_bytes, r.msg_bytes, (uint64_t)r.nchunks, (uint64_t)r.rebuilds,
+                          (uint64_t)(r.a_ms * 1e3), (uint64_t)(r.b_ms * 1e3)};
+  memcpy(info, v, sizeof(v));
+  for (int c = 0; c <= r.nchunks; c++) {
+    bounds[c] = r.sig_chunk[c];
+    bounds[r.nchunks + 1 + c] = r.msg_chunk[c];
+  }
+  return bad ? -1 : 0;
+}
+
+extern "C" double hs_estimate_distinct(size_t s, size_t ds) {
+  return bh::pack::estimate_distinct(s, ds);
 }
