@@ -389,6 +389,20 @@ int reg_alloc(Dev& d, int curve, size_t cap) {
   return BH_OK;
 }
 
+// Host waits on a pass block (hipEventBlockingSync) unless BH_BLOCKING_SYNC=0.
+// Measured (tools/sv_tail.py): HIP's default spin-wait
+// let 256 coalesced Verify callers exhaust the box's 16-CPU cgroup quota --
+// csp_load saw nr_throttled 1 / 646 ms throttled and a p99 of 80 ms; blocking
+// waits: no throttling, p99 2.9 ms, 184k verifies/s (was 63k), the lone
+// registered call's p50 unchanged (140 vs 142 us).
+bool blocking_sync() {
+  static const bool on = [] {
+    const char* e = getenv("BH_BLOCKING_SYNC");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 int dev_init(Dev& d, int id) {
   d.id = id;
   HIPCHK(hipSetDevice(id));
@@ -404,7 +418,11 @@ int dev_init(Dev& d, int id) {
   HIPCHK(hipEventCreateWithFlags(&d.join, hipEventDisableTiming));
   for (Slot& sl : d.slot) {
     HIPCHK(hipEventCreateWithFlags(&sl.uploaded, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    // a host wait on a pass (bh_verify_wait, the coalescer's completer)
+    // sleeps until the device signals instead of HIP's default spin
+    // (blocking_sync(); BH_BLOCKING_SYNC=0 restores the spin)
+    HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming |
+                                                 (blocking_sync() ? hipEventBlockingSync : 0u)));
     HIPCHK(hipEventCreateWithFlags(&sl.keys_up, hipEventDisableTiming));
   }
   for (int c = 0; c < 2; c++) {
@@ -850,6 +868,7 @@ struct CompactHost {
   // chunk while they are packed (upload() only reserves their device range),
   // and their sums are known (-1: sum the lengths)
   bool defer_bytes = false;
+  bool defer_small = false;  // keys, indices and lengths too (copied after packing)
   int64_t sig_bytes = -1, msg_bytes = -1;
 };
 struct CompactDev {
@@ -915,11 +934,14 @@ CompactDev upload(Uploader& u, const CompactHost* h, size_t lo, size_t m, const 
     }
     d.keys = u.put(u.err == hipSuccess ? (const uint8_t*)u.gather->p : nullptr, m * 64);
   } else {
-    d.keys = idx ? u.put(c.keys, c.nkeys * 64) : u.put(c.keys + lo * 64, m * 64);
+    const bool ds = h->defer_small;
+    d.keys = idx ? u.put(ds ? nullptr : c.keys, c.nkeys * 64)
+                 : u.put(ds ? nullptr : c.keys + lo * 64, m * 64);
   }
-  d.key_idx = idx ? u.put(c.key_idx + lo, m) : nullptr;
-  d.sig_len = u.put(c.sig_len + lo, m);
-  d.msg_len = c.msg_len ? u.put(c.msg_len + lo, m) : nullptr;
+  const bool ds = h->defer_small;
+  d.key_idx = idx ? u.put(ds ? nullptr : c.key_idx + lo, m) : nullptr;
+  d.sig_len = u.put(ds ? nullptr : c.sig_len + lo, m);
+  d.msg_len = c.msg_len ? u.put(ds ? nullptr : c.msg_len + lo, m) : nullptr;
   u.mark();  // keys + lengths: enough for the expansion and the key half of the pass
   const bool copy = !h->defer_bytes;
   const uint8_t* sig =
@@ -1135,10 +1157,11 @@ struct PackStats {
   int threads = 0, chunks = 0, dedup = 0, rebuilds = 0;
 } g_pack_stats;
 
-// Pack shard [lo, lo + m) of src into slot k's page-locked buffers (pass A:
-// keys + indices + lengths), queue that key half's H2D, then pack the bytes
-// chunk by chunk (pass B), each chunk's H2D queued as soon as it is complete,
-// and launch the pass. Caller holds d.mu.
+// Pack shard [lo, lo + m) of src into slot k's page-locked buffers and
+// upload it: pack.h plan (lengths -> every byte offset), the device staging
+// reserved for the compact layout, then ONE fill pass (lengths, keys, bytes)
+// whose chunks' H2D copies are queued as each completes; the keys, indices
+// and lengths follow, then the pass. Caller holds d.mu.
 template <class Src>
 int enqueue_staged(bh_job* j, Dev& d, int curve, const Src& src, size_t lo, size_t m,
                    uint32_t flags) {
@@ -1155,15 +1178,16 @@ int enqueue_staged(bh_job* j, Dev& d, int curve, const Src& src, size_t lo, size
   std::lock_guard<std::mutex> pg(g_pack_mu);
   bh::pack::Packer& P = packer();
   bh::pack::Result r;
-  P.pass_a(src, lo, m, out, &r);
+  P.plan(src, lo, m, &r);
   const size_t o_msg = round256(r.sig_bytes + 1);
   if ((rc = sl.pk_bytes.ensure(o_msg + r.msg_bytes + 256))) return rc;
   uint8_t* hsig = (uint8_t*)sl.pk_bytes.p;
   uint8_t* hmsg = hsig + o_msg;
+  // staging reserved for the largest key table (m keys); nothing copied yet
   CompactHost h;
-  h.c = bh_cbatch{out.keys, r.dedup ? out.key_idx : nullptr, r.nkeys, hsig, out.sig_len, hmsg,
+  h.c = bh_cbatch{out.keys, r.dedup ? out.key_idx : nullptr, m, hsig, out.sig_len, hmsg,
                   r.fixed_msg ? nullptr : out.msg_len, r.msg_stride};
-  h.defer_bytes = true;
+  h.defer_bytes = h.defer_small = true;
   h.sig_bytes = (int64_t)r.sig_bytes;
   h.msg_bytes = (int64_t)r.msg_bytes;
   const HostFields f = fields(&h, 0, m);
@@ -1172,24 +1196,27 @@ int enqueue_staged(bh_job* j, Dev& d, int curve, const Src& src, size_t lo, size
   if ((rc = sl.out.ensure(out_bytes))) return rc;
   if ((rc = sl.host_out.ensure(out_bytes))) return rc;
   Uploader u{(char*)sl.stage.p, d.copy, &sl.host_in};
-  if (!(flags & BH_F_KEEP_KEYS) && m <= max_chunk() && keys_first()) u.mark_ev = sl.keys_up;
   const CompactDev db = upload(u, &h, 0, m, f);
   HIPCHK(u.err);
   uint8_t* dsig = const_cast<uint8_t*>(db.b.sig);
   uint8_t* dmsg = const_cast<uint8_t*>(db.b.msg);
   hipError_t ce = hipSuccess;
-  P.pass_b(src, hsig, hmsg, &r, [&](int c) {
-    const uint64_t s0 = r.sig_chunk[c], s1 = r.sig_chunk[c + 1];
-    const uint64_t m0 = r.msg_chunk[c], m1 = r.msg_chunk[c + 1];
-    if (ce == hipSuccess && s1 > s0)
-      ce = hipMemcpyAsync(dsig + s0, hsig + s0, s1 - s0, hipMemcpyHostToDevice, d.copy);
-    if (ce == hipSuccess && m1 > m0)
-      ce = hipMemcpyAsync(dmsg + m0, hmsg + m0, m1 - m0, hipMemcpyHostToDevice, d.copy);
+  auto h2d = [&](const void* dst, const void* srcp, size_t bytes) {
+    if (ce == hipSuccess && bytes)
+      ce = hipMemcpyAsync(const_cast<void*>(dst), srcp, bytes, hipMemcpyHostToDevice, d.copy);
+  };
+  P.fill(src, out, hsig, hmsg, &r, [&](int c) {
+    h2d(dsig + r.sig_chunk[c], hsig + r.sig_chunk[c], r.sig_chunk[c + 1] - r.sig_chunk[c]);
+    h2d(dmsg + r.msg_chunk[c], hmsg + r.msg_chunk[c], r.msg_chunk[c + 1] - r.msg_chunk[c]);
   });
+  h2d(db.keys, out.keys, r.nkeys * 64);
+  if (r.dedup) h2d(db.key_idx, out.key_idx, m * 4);
+  h2d(db.sig_len, out.sig_len, m * 4);
+  if (!r.fixed_msg) h2d(db.msg_len, out.msg_len, m * 4);
   HIPCHK(ce);
   HIPCHK(hipEventRecord(sl.uploaded, d.copy));
-  g_pack_stats.a_ms = r.a_ms;
-  g_pack_stats.b_ms = r.b_ms;
+  g_pack_stats.a_ms = r.plan_ms;
+  g_pack_stats.b_ms = r.fill_ms;
   g_pack_stats.est = r.est_distinct;
   g_pack_stats.shards++;
   g_pack_stats.nkeys = r.nkeys;
@@ -1198,7 +1225,7 @@ int enqueue_staged(bh_job* j, Dev& d, int curve, const Src& src, size_t lo, size
   g_pack_stats.chunks = r.nchunks;
   g_pack_stats.dedup = r.dedup;
   g_pack_stats.rebuilds = r.rebuilds;
-  return launch_part(j, d, k, sl, curve, db, lo, m, flags, u.marked);
+  return launch_part(j, d, k, sl, curve, db, lo, m, flags, false);
 }
 
 // ---- latency path ------------------------------------------------------------
@@ -1388,9 +1415,11 @@ int submit_job(int curve, const B* b, size_t n, uint32_t flags, uint8_t* bitmap,
   // BH_HOST_SHARDS (default 1): shards per device, dealt round-robin -- the
   // multi-device shard path (per-shard staging, compact key gather, bitmap
   // merge at 64-record boundaries) on one device, and a finer upload/compute
-  // pipeline for very large host batches
+  // pipeline for very large host batches. Up to 8: an 8-GPU node's split on
+  // one device (shards beyond the device's kSlots slots reuse a slot once its
+  // earlier shard -- of this or another job -- is collected, take_slot)
   size_t per = 1;
-  if (const char* e = getenv("BH_HOST_SHARDS")) per = (size_t)std::max(1, std::min(atoi(e), kSlots));
+  if (const char* e = getenv("BH_HOST_SHARDS")) per = (size_t)std::max(1, std::min(atoi(e), 8));
   const size_t nd = bh::shard_devices(n, devs.size() * per);
   for (size_t k = 0; k < nd; k++) {
     const bh::Shard sh = bh::shard_of(n, nd, k);
@@ -1437,7 +1466,7 @@ int submit_staged(int curve, const Src& src, size_t n, uint32_t flags, uint8_t* 
   const bool small = curve == BH_CURVE_P256 && n && n <= kSmallMax &&
                      !(flags & BH_F_KEEP_KEYS) && !getenv("BH_NO_SMALL");
   size_t per = 1;
-  if (const char* e = getenv("BH_HOST_SHARDS")) per = (size_t)std::max(1, std::min(atoi(e), kSlots));
+  if (const char* e = getenv("BH_HOST_SHARDS")) per = (size_t)std::max(1, std::min(atoi(e), 8));
   const size_t nd = small ? 1 : bh::shard_devices(n, devs.size() * per);
   static std::atomic<uint32_t> rr{0};
   const size_t first = small ? rr++ % devs.size() : 0;

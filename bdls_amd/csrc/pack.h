@@ -6,15 +6,15 @@
 // measured end to end by bench.py host_path_e2e.
 //
 // Two passes over the records, both on a pool of worker threads:
-//   A: lengths, per-block byte sums, and the key of every record: with
-//      de-duplication, a lock-free open-addressing table over the 64 key
-//      bytes hands out key ids (first claimant copies the key; ids come in
-//      per-thread blocks, so the key array has a few zero-filled holes); without
-//      it (a batch of mostly distinct keys: config 5), each record's key is
-//      copied in record order.
-//   B: the signature and message bytes, chunk by chunk; a chunk's bytes are
-//      contiguous in the output, so the caller can start its H2D copy while
-//      the workers fill the next one (on_chunk).
+//   plan: the lengths only -- byte offsets of every (chunk, thread) block;
+//   fill: per record its lengths, its key and its signature / message bytes.
+//      With de-duplication a lock-free open-addressing table over the keys
+//      hands out key ids (first claimant copies the key; ids come in
+//      per-thread blocks, so the key array has a few zero-filled holes);
+//      without it (a batch of mostly distinct keys: config 5) each record's
+//      key is copied in record order. The bytes stream chunk by chunk; a
+//      chunk's bytes are contiguous in the output, so the caller starts its
+//      H2D copy while the workers fill the next one (on_chunk).
 // Whether to de-duplicate is decided from a strided sample of the keys (the
 // distinct count a uniform draw from D keys would show); a table that fills
 // anyway is rebuilt at its largest size, so the result never depends on the
@@ -118,15 +118,15 @@ inline uint64_t load64(const uint8_t* p) {
   return v;
 }
 
-// 64-bit mix of the 64 key bytes (every byte counts: crafted keys that share
-// a prefix still spread over the table)
+// 64-bit mix of the key: X's first 8 bytes and Y's first 8 (a valid key's
+// coordinates are uniformly spread, and Y separates the two points of one X).
+// Equal keys always collide; keys crafted to share these bytes only lengthen
+// probe runs -- past the probe limit the table is rebuilt and then dedup is
+// dropped, so the packed batch stays exact whatever the keys (every match is
+// confirmed on all 64 bytes).
 inline uint64_t key_hash(const uint8_t* k) {
-  uint64_t h = 0x9E3779B97F4A7C15ull;
-  for (int w = 0; w < 8; w++) {
-    h = (h ^ load64(k + 8 * w)) * 0xff51afd7ed558ccdull;
-    h ^= h >> 29;
-  }
-  h *= 0xc4ceb9fe1a85ec53ull;
+  uint64_t h = (load64(k) ^ 0x9E3779B97F4A7C15ull) * 0xff51afd7ed558ccdull;
+  h = (h ^ (h >> 29) ^ load64(k + 32)) * 0xc4ceb9fe1a85ec53ull;
   return h ^ (h >> 32);
 }
 
@@ -252,14 +252,15 @@ class StreamWriter {
 // ---- the packer ---------------------------------------------------------------
 struct Out {
   uint8_t* keys = nullptr;      // >= m * 64 bytes
-  uint32_t* key_idx = nullptr;  // m (written when dedup)
+  uint32_t* key_idx = nullptr;  // m (written when Result::dedup)
   uint32_t* sig_len = nullptr;  // m
-  uint32_t* msg_len = nullptr;  // m (written unless every message has one length)
+  uint32_t* msg_len = nullptr;  // m
 };
 
 struct Result {
   size_t nkeys = 0;
-  bool dedup = false;          // key_idx written; else keys hold one key per record
+  bool dedup = false;          // key_idx written (keys[key_idx[i]] is record i's key);
+                               // else keys hold one key per record
   bool fixed_msg = false;      // every message msg_stride bytes: msg_len not needed
   uint32_t msg_stride = 0;
   uint64_t sig_bytes = 0, msg_bytes = 0;
@@ -267,31 +268,35 @@ struct Result {
   std::vector<uint64_t> sig_chunk, msg_chunk;  // nchunks + 1 byte offsets
   double est_distinct = 0;     // sample estimate (0: no repeat seen)
   int rebuilds = 0;            // table rebuilt at full size (estimate too low)
-  double a_ms = 0, b_ms = 0;   // pass A / pass B wall time
+  bool dedup_dropped = false;  // rebuilt table overflowed too: identity indices
+  double plan_ms = 0, fill_ms = 0;
 };
 
-// Src: size_t n() const; const uint8_t* key(i); const uint8_t* sig(i);
-// uint32_t sig_len(i); const uint8_t* msg(i); uint32_t msg_len(i).
+// plan(): the dedup decision from a strided sample, then one pass over the
+// lengths -- per (chunk, thread) block byte sums, their prefix offsets, the
+// totals and the chunk bounds (the caller sizes its staging from these).
+// fill(): ONE pass per record -- lengths, key (dedup probe or copy), and the
+// signature / message bytes streamed to their final offsets -- so the dedup's
+// table misses overlap the bandwidth-bound copy instead of adding to it;
+// after chunk c is complete on every thread, on_chunk(c) runs on the calling
+// thread (the H2D of its bytes) while the workers fill chunk c + 1.
+// Src: key(i), sig(i), sig_len(i), msg(i), msg_len(i) for i in [lo, lo + m).
 class Packer {
  public:
   explicit Packer(int threads) : pool_(threads) {}
   int threads() const { return pool_.threads(); }
 
-  // Pass A. m records of src starting at lo.
   template <class Src>
-  int pass_a(const Src& src, size_t lo, size_t m, const Out& out, Result* r, int force = -1) {
+  void plan(const Src& src, size_t lo, size_t m, Result* r, int force = -1) {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
-    const int T = pool_.threads();
     *r = Result{};
-    // chunks for pass B's streaming: ~16 MB of bytes each, 1..16
-    r->nchunks = 1;
-    out_ = out;
-    // dedup decision from a strided sample
+    lo_ = lo;
+    m_ = m;
     bool dedup = false;
     double est = 0;
     if (force >= 0) {
-      dedup = force == 1;
+      dedup = force == 1 && m > 0;
     } else if (m >= 64) {
       const size_t s = std::min<size_t>(m, 8192);
       std::vector<uint64_t> hs(s);
@@ -304,231 +309,244 @@ class Packer {
       dedup = m > 1;
     }
     r->est_distinct = est;
-    // sums per (thread) block for pass A; chunking decided after the sums
-    sig_sum_.assign(T, 0);
-    msg_sum_.assign(T, 0);
-    len_min_.assign(T, UINT32_MAX);
-    len_max_.assign(T, 0);
-    overflow_.store(false);
-    uint64_t cap = 0;
-    uint32_t max_ids = 0;
-    bool full_table = false;  // ids may reach m: one id per claim, no holes
-    auto size_table = [&](bool full) {
-      full_table = full;
-      if (full) {
-        cap = 1024;
-        while (cap < 2 * (uint64_t)m) cap <<= 1;
-      } else {
-        const double want = std::max(4.0 * est, 4096.0);
-        cap = 1024;
-        while ((double)cap < want && cap < 2 * (uint64_t)m) cap <<= 1;
-        while (cap < 2 * (uint64_t)std::min<size_t>(m, 512)) cap <<= 1;
-      }
-      max_ids = (uint32_t)std::min<uint64_t>(cap / 2, m);
-      if (table_.size() < cap) table_ = std::vector<std::atomic<uint64_t>>(cap);
-      if (kcache_.size() < (size_t)max_ids * 64) kcache_.resize((size_t)max_ids * 64);
-      for (uint64_t k = 0; k < cap; k++) table_[k].store(0, std::memory_order_relaxed);
-      next_id_.store(0);
-      overflow_.store(false);
-    };
-    if (dedup) size_table(est == 0);
-    auto range = [&](int t, size_t* a, size_t* b) {
-      *a = lo + (m * (size_t)t) / T;
-      *b = lo + (m * (size_t)(t + 1)) / T;
-    };
-    auto body = [&](int t, bool keys_only) {
-      size_t a, b;
-      range(t, &a, &b);
-      uint64_t ss = 0, ms = 0;
-      uint32_t mn = UINT32_MAX, mx = 0;
-      if (!keys_only) {
-        for (size_t i = a; i < b; i++) {
-          const uint32_t sl = src.sig_len(i), ml = src.msg_len(i);
-          out.sig_len[i - lo] = sl;
-          out.msg_len[i - lo] = ml;
-          ss += sl;
-          ms += ml;
-          mn = std::min(mn, ml);
-          mx = std::max(mx, ml);
-        }
-      }
-      if (!dedup) {
-        for (size_t i = a; i < b; i++) std::memcpy(out.keys + (i - lo) * 64, src.key(i), 64);
-      } else {
-        // groups of kG records: hashes and table slots first, then the
-        // candidate keys, then the compares -- the random table and key
-        // reads of a group overlap instead of costing a miss each in turn
-        constexpr int kG = 16;
-        std::atomic<uint64_t>* tab = table_.data();
-        uint8_t* kc = kcache_.data();
-        const uint64_t mask = cap - 1;
-        IdBlock blk;  // small tables: small blocks, so holes never fill the id range
-        blk.size = full_table ? 1u
-                              : (uint32_t)std::max<uint64_t>(
-                                    1, std::min<uint64_t>(kIdBlock, max_ids / (8 * T)));
-        for (size_t g0 = a; g0 < b && !overflow_.load(std::memory_order_relaxed); g0 += kG) {
-          const int cnt = (int)std::min<size_t>(kG, b - g0);
-          const uint8_t* kp[kG];
-          uint64_t hh[kG];
-          uint32_t cand[kG];
-          for (int j = 0; j < cnt; j++) {
-            kp[j] = src.key(g0 + j);
-            hh[j] = key_hash(kp[j]);
-            __builtin_prefetch(&tab[hh[j] & mask]);
-          }
-          for (int j = 0; j < cnt; j++) {
-            const uint64_t v = tab[hh[j] & mask].load(std::memory_order_acquire);
-            const uint32_t id = (uint32_t)v;
-            cand[j] = kBusy;
-            if ((v >> 32) == ((hh[j] >> 32) | 1u) && id < max_ids) {
-              cand[j] = id;
-              __builtin_prefetch(kc + (size_t)id * 64);
-            }
-          }
-          for (int j = 0; j < cnt; j++) {
-            uint32_t id = cand[j];
-            if (id == kBusy || std::memcmp(kc + (size_t)id * 64, kp[j], 64) != 0)
-              id = insert_key(tab, cap, &next_id_, max_ids, kc, out.keys, kp[j], hh[j], &blk);
-            if (id == kBusy) {
-              overflow_.store(true, std::memory_order_relaxed);
-              break;
-            }
-            out.key_idx[g0 + j - lo] = id;
-          }
-        }
-        for (uint32_t id = blk.next; id < blk.end && id < max_ids; id++)  // the block's holes
-          std::memset(out.keys + (size_t)id * 64, 0, 64);
-      }
-      if (!keys_only) {
-        sig_sum_[t] = ss;
-        msg_sum_[t] = ms;
-        len_min_[t] = mn;
-        len_max_[t] = mx;
-      }
-    };
-    pool_.run([&](int t) { body(t, false); });
-    if (dedup && overflow_.load()) {  // the estimate was low: once more at full size
-      r->rebuilds++;
-      size_table(true);
-      pool_.run([&](int t) { body(t, true); });
-      if (overflow_.load()) {  // cannot happen (cap >= 2 m), but never verify a wrong key
-        dedup = false;
-        pool_.run([&](int t) { body(t, true); });
-      }
-    }
     r->dedup = dedup;
-    // (with id blocks the key array may end in holes: ids up to the last block)
-    r->nkeys = dedup ? std::min<size_t>(next_id_.load(), max_ids) : m;
-    uint32_t mn = UINT32_MAX, mx = 0;
-    for (int t = 0; t < T; t++) {
-      r->sig_bytes += sig_sum_[t];
-      r->msg_bytes += msg_sum_[t];
-      mn = std::min(mn, len_min_[t]);
-      mx = std::max(mx, len_max_[t]);
+    // chunks: ~16 MB of bytes each (from a sample of lengths), 1..16
+    const int T = pool_.threads();
+    uint64_t sample = 0;
+    const size_t ns = std::min<size_t>(m, 1024);
+    for (size_t k = 0; k < ns; k++) {
+      const size_t i = lo + (k * m) / std::max<size_t>(ns, 1);
+      sample += src.sig_len(i) + src.msg_len(i);
     }
-    r->fixed_msg = m > 0 && mn == mx;
-    r->msg_stride = r->fixed_msg ? mn : 0;
-    const uint64_t total = r->sig_bytes + r->msg_bytes;
-    r->nchunks = (int)std::max<uint64_t>(1, std::min<uint64_t>(16, total / (16u << 20)));
-    if (const char* e = getenv("BH_PACK_CHUNKS")) r->nchunks = std::max(1, std::min(64, atoi(e)));
-    r->a_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-    lo_ = lo;
-    m_ = m;
-    return 0;
-  }
-
-  // Pass B: signature / message bytes into sig / msg (r->sig_bytes,
-  // r->msg_bytes). Chunk c = records [lo + m c / K, lo + m (c + 1) / K); after
-  // chunk c is complete, on_chunk(c) runs on the calling thread while the
-  // workers go on with chunk c + 1. r->sig_chunk / msg_chunk get the chunk
-  // boundaries.
-  template <class Src>
-  void pass_b(const Src& src, uint8_t* sig, uint8_t* msg, Result* r,
-              const std::function<void(int)>& on_chunk) {
-    using clk = std::chrono::steady_clock;
-    const auto t0 = clk::now();
-    // pass B streams memory: past ~8 threads the copy is bandwidth-bound and
-    // more threads only contend (BH_PACK_B_THREADS, default all)
-    static const int tb_env = [] {
-      const char* e = getenv("BH_PACK_B_THREADS");
-      return e ? std::max(1, atoi(e)) : 0;
-    }();
-    const int T = tb_env ? std::min(tb_env, pool_.threads()) : pool_.threads();
-    const int K = r->nchunks;
-    const size_t lo = lo_, m = m_;
-    // per (chunk, thread) block byte sums -> offsets (chunk-major order)
+    const double est_bytes = ns ? (double)sample * m / ns : 0.0;
+    int K = (int)std::max(1.0, std::min(16.0, est_bytes / (16u << 20)));
+    if (const char* e = getenv("BH_PACK_CHUNKS")) K = std::max(1, std::min(64, atoi(e)));
+    r->nchunks = K;
+    T_ = T;
     const size_t B = (size_t)K * T;
     boff_s_.assign(B + 1, 0);
     boff_m_.assign(B + 1, 0);
-    auto brange = [&](size_t blk, size_t* a, size_t* b) {
-      const size_t c = blk / T, t = blk % T;
-      const size_t ca = (m * c) / K, cb = (m * (c + 1)) / K;
-      *a = lo + ca + ((cb - ca) * t) / T;
-      *b = lo + ca + ((cb - ca) * (t + 1)) / T;
-    };
-    // block sums (from the source: the page-locked output reads back uncached)
+    len_min_.assign(T, UINT32_MAX);
+    len_max_.assign(T, 0);
     pool_.run([&](int t) {
-      if (t >= T) return;
+      uint32_t mn = UINT32_MAX, mx = 0;
       for (int c = 0; c < K; c++) {
         const size_t blk = (size_t)c * T + t;
         size_t a, b;
         brange(blk, &a, &b);
         uint64_t ss = 0, ms = 0;
         for (size_t i = a; i < b; i++) {
+          const uint32_t ml = src.msg_len(i);
           ss += src.sig_len(i);
-          ms += src.msg_len(i);
+          ms += ml;
+          mn = std::min(mn, ml);
+          mx = std::max(mx, ml);
         }
         boff_s_[blk + 1] = ss;
         boff_m_[blk + 1] = ms;
       }
+      len_min_[t] = mn;
+      len_max_[t] = mx;
     });
     for (size_t k = 0; k < B; k++) {
       boff_s_[k + 1] += boff_s_[k];
       boff_m_[k + 1] += boff_m_[k];
     }
+    r->sig_bytes = boff_s_[B];
+    r->msg_bytes = boff_m_[B];
     r->sig_chunk.assign(K + 1, 0);
     r->msg_chunk.assign(K + 1, 0);
     for (int c = 0; c <= K; c++) {
       r->sig_chunk[c] = boff_s_[(size_t)c * T];
       r->msg_chunk[c] = boff_m_[(size_t)c * T];
     }
+    uint32_t mn = UINT32_MAX, mx = 0;
+    for (int t = 0; t < T; t++) {
+      mn = std::min(mn, len_min_[t]);
+      mx = std::max(mx, len_max_[t]);
+    }
+    r->fixed_msg = m > 0 && mn == mx;
+    r->msg_stride = r->fixed_msg ? mn : 0;
+    r->plan_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  }
+
+  template <class Src>
+  void fill(const Src& src, const Out& out, uint8_t* sig, uint8_t* msg, Result* r,
+            const std::function<void(int)>& on_chunk) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    const int T = T_, K = r->nchunks;
+    const size_t lo = lo_, m = m_;
+    bool dedup = r->dedup;
+    if (dedup) size_table(r->est_distinct == 0, r->est_distinct);
     std::vector<std::atomic<int>> done(K);
     for (auto& x : done) x.store(0);
     pool_.start([&](int t) {
-      if (t >= T) return;
+      IdBlock blk;  // small tables: small blocks, so holes never fill the id range
+      blk.size = full_table_ ? 1u
+                             : (uint32_t)std::max<uint64_t>(
+                                   1, std::min<uint64_t>(kIdBlock, max_ids_ / (8 * T)));
       for (int c = 0; c < K; c++) {
-        const size_t blk = (size_t)c * T + t;
+        const size_t b0 = (size_t)c * T + t;
         size_t a, b;
-        brange(blk, &a, &b);
-        StreamWriter ws(sig + boff_s_[blk]), wm(msg + boff_m_[blk]);
-        for (size_t i = a; i < b; i++) {
-          const uint32_t sl = src.sig_len(i), ml = src.msg_len(i);
-          if (sl) ws.put(src.sig(i), sl);
-          if (ml) wm.put(src.msg(i), ml);
+        brange(b0, &a, &b);
+        StreamWriter ws(sig + boff_s_[b0]), wm(msg + boff_m_[b0]);
+        for (size_t g0 = a; g0 < b; g0 += kGroup) {
+          const int cnt = (int)std::min<size_t>(kGroup, b - g0);
+          if (dedup) keys_group(src, out, g0, cnt, &blk);
+          for (int j = 0; j < cnt; j++) {
+            const size_t i = g0 + j;
+            const uint32_t sl = src.sig_len(i), ml = src.msg_len(i);
+            out.sig_len[i - lo] = sl;
+            out.msg_len[i - lo] = ml;
+            if (!dedup) std::memcpy(out.keys + (i - lo) * 64, src.key(i), 64);
+            if (sl) ws.put(src.sig(i), sl);
+            if (ml) wm.put(src.msg(i), ml);
+          }
         }
         ws.finish();
         wm.finish();
         StreamWriter::fence();  // the chunk's streamed bytes are globally visible
-        done[c].fetch_add(1, std::memory_order_acq_rel);
+        if (done[c].fetch_add(1, std::memory_order_acq_rel) + 1 == T) {
+          std::lock_guard<std::mutex> g(chunk_mu_);
+          chunk_cv_.notify_all();
+        }
       }
+      if (dedup) zero_holes(out, blk);
     });
+    // the calling thread SLEEPS until each chunk is complete: a spinning
+    // caller on top of the workers overran the 16-CPU cgroup quota and the
+    // CFS throttle stalled whole batches
     for (int c = 0; c < K; c++) {
-      while (done[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
+      {
+        std::unique_lock<std::mutex> g(chunk_mu_);
+        chunk_cv_.wait(g, [&] { return done[c].load(std::memory_order_acquire) >= T; });
+      }
       if (on_chunk) on_chunk(c);
     }
     pool_.wait();
-    r->b_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    if (dedup && overflow_.load()) {  // the estimate was low: the keys once more, full size
+      r->rebuilds++;
+      size_table(true, 0);
+      keys_only(src, out);
+      if (overflow_.load()) {  // (cannot happen: cap >= 2 m) identity indices, never a wrong key
+        r->dedup_dropped = true;
+        pool_.run([&](int t) {
+          const size_t a = lo + (m * (size_t)t) / T, b = lo + (m * (size_t)(t + 1)) / T;
+          for (size_t i = a; i < b; i++) {
+            std::memcpy(out.keys + (i - lo) * 64, src.key(i), 64);
+            out.key_idx[i - lo] = (uint32_t)(i - lo);
+          }
+        });
+      }
+    }
+    r->nkeys = !dedup ? m : r->dedup_dropped ? m : std::min<size_t>(next_id_.load(), max_ids_);
+    r->fill_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
   }
 
  private:
+  static constexpr int kGroup = 16;
+
+  void brange(size_t blk, size_t* a, size_t* b) const {
+    const size_t T = (size_t)T_, K = blk_k();
+    const size_t c = blk / T, t = blk % T;
+    const size_t ca = (m_ * c) / K, cb = (m_ * (c + 1)) / K;
+    *a = lo_ + ca + ((cb - ca) * t) / T;
+    *b = lo_ + ca + ((cb - ca) * (t + 1)) / T;
+  }
+  size_t blk_k() const { return (boff_s_.size() - 1) / (size_t)T_; }
+
+  void size_table(bool full, double est) {
+    full_table_ = full;
+    const size_t m = m_;
+    if (full) {
+      cap_ = 1024;
+      while (cap_ < 2 * (uint64_t)m) cap_ <<= 1;
+    } else {
+      const double want = std::max(4.0 * est, 4096.0);
+      cap_ = 1024;
+      while ((double)cap_ < want && cap_ < 2 * (uint64_t)m) cap_ <<= 1;
+      while (cap_ < 2 * (uint64_t)std::min<size_t>(m, 512)) cap_ <<= 1;
+    }
+    max_ids_ = (uint32_t)std::min<uint64_t>(cap_ / 2, m);
+    if (table_.size() < cap_) table_ = std::vector<std::atomic<uint64_t>>(cap_);
+    if (kcache_.size() < (size_t)max_ids_ * 64) kcache_.resize((size_t)max_ids_ * 64);
+    pool_.run([&](int t) {  // clear in parallel (the table can be 2 m words)
+      const uint64_t a = cap_ * t / pool_.threads(), b = cap_ * (t + 1) / pool_.threads();
+      for (uint64_t k = a; k < b; k++) table_[k].store(0, std::memory_order_relaxed);
+    });
+    next_id_.store(0);
+    overflow_.store(false);
+  }
+
+  // the keys of records [g0, g0 + cnt): hashes and table slots first, then
+  // the candidate keys, then the compares -- a group's random table and key
+  // reads overlap instead of costing a miss each in turn
+  template <class Src>
+  void keys_group(const Src& src, const Out& out, size_t g0, int cnt, IdBlock* blk) {
+    if (overflow_.load(std::memory_order_relaxed)) return;
+    std::atomic<uint64_t>* tab = table_.data();
+    uint8_t* kc = kcache_.data();
+    const uint64_t mask = cap_ - 1;
+    const uint8_t* kp[kGroup];
+    uint64_t hh[kGroup];
+    uint32_t cand[kGroup];
+    for (int j = 0; j < cnt; j++) {
+      kp[j] = src.key(g0 + j);
+      hh[j] = key_hash(kp[j]);
+      __builtin_prefetch(&tab[hh[j] & mask]);
+    }
+    for (int j = 0; j < cnt; j++) {
+      const uint64_t v = tab[hh[j] & mask].load(std::memory_order_acquire);
+      const uint32_t id = (uint32_t)v;
+      cand[j] = kBusy;
+      if ((v >> 32) == ((hh[j] >> 32) | 1u) && id < max_ids_) {
+        cand[j] = id;
+        __builtin_prefetch(kc + (size_t)id * 64);
+      }
+    }
+    for (int j = 0; j < cnt; j++) {
+      uint32_t id = cand[j];
+      if (id == kBusy || std::memcmp(kc + (size_t)id * 64, kp[j], 64) != 0)
+        id = insert_key(tab, cap_, &next_id_, max_ids_, kc, out.keys, kp[j], hh[j], blk);
+      if (id == kBusy) {
+        overflow_.store(true, std::memory_order_relaxed);
+        return;
+      }
+      out.key_idx[g0 + j - lo_] = id;
+    }
+  }
+
+  void zero_holes(const Out& out, const IdBlock& blk) {
+    for (uint32_t id = blk.next; id < blk.end && id < max_ids_; id++)
+      std::memset(out.keys + (size_t)id * 64, 0, 64);
+  }
+
+  // the dedup alone over every record (after a table overflow)
+  template <class Src>
+  void keys_only(const Src& src, const Out& out) {
+    const int T = pool_.threads();
+    pool_.run([&](int t) {
+      IdBlock blk;
+      blk.size = 1;
+      const size_t a = lo_ + (m_ * (size_t)t) / T, b = lo_ + (m_ * (size_t)(t + 1)) / T;
+      for (size_t g0 = a; g0 < b && !overflow_.load(std::memory_order_relaxed); g0 += kGroup)
+        keys_group(src, out, g0, (int)std::min<size_t>(kGroup, b - g0), &blk);
+    });
+  }
+
   Pool pool_;
-  Out out_;
+  std::mutex chunk_mu_;
+  std::condition_variable chunk_cv_;
+  int T_ = 1;
   size_t lo_ = 0, m_ = 0;
-  std::vector<uint64_t> sig_sum_, msg_sum_;
   std::vector<uint32_t> len_min_, len_max_;
   std::vector<uint64_t> boff_s_, boff_m_;
   std::vector<std::atomic<uint64_t>> table_;
   std::vector<uint8_t> kcache_;  // the dedup's key copies (cached memory)
+  uint64_t cap_ = 0;
+  uint32_t max_ids_ = 0;
+  bool full_table_ = false;
   std::atomic<uint32_t> next_id_{0};
   std::atomic<bool> overflow_{false};
 };

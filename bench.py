@@ -126,6 +126,9 @@ def lane_count() -> int:
 CONFIG5_TOTAL = 1 << 26
 
 
+NOMINAL_MAC_PEAK = 256 * 4 * 16 * 2.4e9  # u32 MAC/s at the nominal VOP3 issue rate
+
+
 def kernel_fp_ops(stage: str, routes: dict) -> float:
     """Algorithmic F_p ops of one launch of the stage's kernel."""
     if stage == "build_ladder_ms":
@@ -594,6 +597,16 @@ def cpu_baseline(a, w, n):
     }
 
 
+def cgroup_throttle():
+    """(nr_throttled, throttled_usec) of this process's cgroup (v2), or zeros."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            d = dict(l.split() for l in f)
+        return int(d.get("nr_throttled", 0)), int(d.get("throttled_usec", 0))
+    except (OSError, ValueError):
+        return 0, 0
+
+
 def measure_e2e(a, L, w, n, flags, local, world, depth, h2d_gbps):
     """host_path_e2e: K BatchVerify calls through bh_batch_verify_submit /
     bh_verify_wait from PAGEABLE arrays (the generator's, copied into ordinary
@@ -643,9 +656,11 @@ def measure_e2e(a, L, w, n, flags, local, world, depth, h2d_gbps):
     shards0 = st1["shards"]
     phase(f"host_path_e2e: {a.steps} timed batches")
     acc.update(submit_s=0.0, wait_s=0.0)
+    thr0 = cgroup_throttle()
     t0 = time.perf_counter()
     run(a.steps)
     t1 = time.perf_counter()
+    thr1 = cgroup_throttle()
     st = _lib.pack_stats()
     dist.barrier(world)
     elapsed = dist.max_over_ranks(t1 - t0, world)
@@ -669,6 +684,8 @@ def measure_e2e(a, L, w, n, flags, local, world, depth, h2d_gbps):
                      "packing into the library's reused page-locked staging (pack.h worker "
                      "pool), chunked H2D, the pass, results -- no untimed per-batch step" % depth),
             "single_batch_ms": round(single_ms, 3),
+            "cgroup_throttled_ms": round((thr1[1] - thr0[1]) / 1e3, 1),
+            "cgroup_nr_throttled": thr1[0] - thr0[0],
             "submit_ms_per_batch": round(acc["submit_s"] * 1e3 / a.steps, 3),
             "wait_ms_per_batch": round(acc["wait_s"] * 1e3 / a.steps, 3),
             "upload_bytes_per_batch": up_bytes,
@@ -1002,6 +1019,12 @@ def bench_throughput(a, rank, world, local):
             "peak": peak / 1e12,
             "unit": "TMAC/s (u32 x u32 -> u64)",
             "frac": achieved / peak if peak else None,
+            # the same work against the nominal VOP3 issue rate: 256 CUs x 4 SIMDs
+            # x 16 lane-ops/cycle (a wave64 v_mad_u64_u32 every 4 cycles) x 2.4 GHz
+            "peak_nominal": NOMINAL_MAC_PEAK / 1e12,
+            "frac_nominal": achieved / NOMINAL_MAC_PEAK,
+            "peak_nominal_source": "256 CU x 4 SIMD x 16 lane-ops/cycle (4-cycle VOP3) x 2.4 GHz "
+                                   "(MI355X_MICROARCH.md peak clock)",
             "work_per_launch": (f"{routes['ladder']} ladder verifies x {FP_LADDER} + "
                                 f"{routes['key_tables']} key tables x {FP_KTAB}"
                                 + ("" if LL_TABLES else
@@ -1049,6 +1072,10 @@ def bench_throughput(a, rank, world, local):
                 "formula": "SQ_INSTS_VALU x cyc / (GRBM_GUI_ACTIVE/8 XCDs x 256 CUs x 4 SIMDs)",
                 "util_2cyc": c["valu_util_2cyc"],
                 "util_4cyc": c["valu_util_4cyc"],
+                "sq_active_inst_valu_per_launch": c.get("sq_active_inst_valu"),
+                "valu_busy": c.get("valu_busy"),
+                "valu_busy_formula": "rocprof VALUBusy: SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x "
+                                     "GRBM_GUI_ACTIVE/8 XCDs)",
                 "cost_model": ("2cyc: a wave64 VALU instruction occupies a SIMD-32 for 2 cycles "
                                "(MI355X_MICROARCH.md:54); 4cyc: one wave's issue rate and the "
                                "measured v_mad_u64_u32 / u32-add rate (profiles/ubench.json: "

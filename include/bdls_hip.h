@@ -215,9 +215,9 @@ int bh_verify_compact_submit(int curve, const bh_cbatch *b, size_t n, uint32_t f
  * the library packs each shard into page-locked staging it owns and reuses
  * (pipeline slot buffers), on a pool of worker threads -- key de-duplication
  * by a lock-free hash table (each distinct key uploaded once + a u32 index per
- * record, the compact layout), lengths, and the signature and message bytes,
- * the latter in chunks whose H2D copies start while the next chunk is packed;
- * the device pass plans and builds its key tables while the bytes upload.
+ * record, the compact layout), lengths, and the signature and message bytes
+ * in one pass per record, in chunks whose H2D copies start while the next
+ * chunk is packed (include/../bdls_amd/csrc/pack.h).
  * Replaces the per-call packing a Go BatchVerify did on one goroutine into a
  * fresh bh_host_alloc (INTEGRATION.md 2 packBatch) -- the batch points
  * common/policies/policy.go:363-395 and core/committer/txvalidator/v20/
@@ -250,8 +250,9 @@ int bh_batch_verify_ptrs(int curve, const bh_pbatch *b, size_t n, uint32_t flags
                          uint8_t *bitmap, uint8_t *reason);
 int bh_batch_verify_ptrs_submit(int curve, const bh_pbatch *b, size_t n, uint32_t flags,
                                 uint8_t *bitmap, uint8_t *reason, bh_job **job);
-/* The last staged shard's packing: out[0] pass A ms (keys, indices, lengths),
- * [1] pass B ms (bytes, H2D copies queued per chunk), [2] worker threads,
+/* The last staged shard's packing: out[0] plan ms (lengths -> byte offsets),
+ * [1] fill ms (lengths, keys + indices, bytes; the chunks' H2D copies queued
+ * as they complete), [2] worker threads,
  * [3] chunks, [4] keys de-duplicated (1/0), [5] keys uploaded, [6] records,
  * [7] the sample's distinct-key estimate (0: no repeat seen), [8] table
  * rebuilds, [9] staged shards since start. Not in the reference

@@ -336,10 +336,10 @@ extern "C" int hs_shard_check(size_t n, size_t ndev, const uint8_t* valid, size_
 
 // ---- staged BatchVerify packing (bdls_amd/csrc/pack.h) ------------------------
 // Packs records [lo, lo + m) of a SoA batch exactly as bdls_hip.cpp
-// enqueue_staged does (pass A then pass B with the per-chunk callback).
+// enqueue_staged does (plan, then fill with the per-chunk callback).
 // force: -1 the sample decides, 0 / 1 de-duplication off / on. info[0..7] =
 // nkeys, dedup, fixed_msg, msg_stride, sig_bytes, msg_bytes, nchunks, rebuilds,
-// [8..9] pass A / pass B microseconds;
+// [8..9] plan / fill microseconds;
 // bounds: the chunk byte bounds (sig then msg, nchunks + 1 each) in the order
 // the callback saw them complete. Returns -1 when a chunk was reported before
 // its bytes were all written or out of order.
@@ -370,10 +370,10 @@ extern "C" int hs_pack(const uint8_t* pub, const uint8_t* sig, const uint64_t* s
   HsSrcA a{&src};
   bh::pack::Out out{keys, key_idx, slen, mlen};
   bh::pack::Result r;
-  P[threads]->pass_a(a, lo, m, out, &r, force);
+  P[threads]->plan(a, lo, m, &r, force);
   int next = 0, bad = 0;
   static const bool nocheck = getenv("HS_PACK_NOCHECK") != nullptr;  // tools/pack_bench.py
-  P[threads]->pass_b(a, sig_out, msg_out, &r, [&](int c) {
+  P[threads]->fill(a, out, sig_out, msg_out, &r, [&](int c) {
     if (c != next++) bad = 1;
     if (nocheck) return;
     // every record of chunk c is in place when its callback runs
@@ -389,7 +389,7 @@ extern "C" int hs_pack(const uint8_t* pub, const uint8_t* sig, const uint64_t* s
   });
   const uint64_t v[10] = {r.nkeys, (uint64_t)r.dedup, (uint64_t)r.fixed_msg, r.msg_stride,
                           r.sig_bytes, r.msg_bytes, (uint64_t)r.nchunks, (uint64_t)r.rebuilds,
-                          (uint64_t)(r.a_ms * 1e3), (uint64_t)(r.b_ms * 1e3)};
+                          (uint64_t)(r.plan_ms * 1e3), (uint64_t)(r.fill_ms * 1e3)};
   memcpy(info, v, sizeof(v));
   for (int c = 0; c <= r.nchunks; c++) {
     bounds[c] = r.sig_chunk[c];

@@ -491,3 +491,27 @@ def test_config2_exact_shape(L):
     ok_prep = int((w.reason == 0).sum() + (w.reason == 9).sum())  # math-checked records
     assert tm.n_keycomb + tm.n_ladder == ok_prep
     assert tm.n_keytables >= 65_000 and tm.n_keycomb >= 0.99 * ok_prep
+
+
+@pytest.mark.parametrize("shards", ["2", "8"])
+def test_config2_exact_shape_host_shards(L, shards, monkeypatch):
+    """config 2's exact batch split the way a 2- and an
+    8-device node splits it (bdls_amd/csrc/shard.h: contiguous 64-aligned
+    shards, each with its own pipeline slot, staging, key tables and bitmap
+    words, merged into the caller's bitmap) -- here as BH_HOST_SHARDS shards on
+    the one device -- through the plain host ABI and the staged BatchVerify:
+    bitmap and reasons equal the construction, so the in-process multi-device
+    path is exercised on hardware."""
+    n, nkeys = 1 << 20, 1 << 16
+    w = workload.generate(n, nkeys, 256, 16, seed=2)
+    monkeypatch.setenv("BH_HOST_SHARDS", shards)
+    bits, rs = host_verify(L, w)
+    assert (rs == w.reason).all() and (bits == w.expected_valid).all()
+    bm = np.zeros(n // 8, np.uint8)
+    rs2 = np.zeros(n, np.uint8)
+    b = _lib.BhBatch(*[x.ctypes.data for x in w.arrays()])
+    _lib.check(L.bh_batch_verify(0, ctypes.byref(b), n, _lib.BH_F_HASH_SHA256, bm.ctypes.data,
+                                 rs2.ctypes.data))
+    assert (rs2 == w.reason).all()
+    assert (np.unpackbits(bm, bitorder="little").astype(bool) == w.expected_valid).all()
+    assert _lib.pack_stats()["records"] == n // int(shards)

@@ -67,7 +67,8 @@ def main():
         if bi.get("kernel_src_sha") not in (None, kernel_src_sha()):
             raise SystemExit("BUILD_INFO.json describes other kernel sources: rebuild first")
         tr = {"source": f"{src} (rocprofv3 --pmc: FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU + "
-                        f"GRBM_GUI_ACTIVE, separate passes)",
+                        f"GRBM_GUI_ACTIVE / SQ_ACTIVE_INST_VALU + GRBM_GUI_ACTIVE, separate "
+                        f"passes)",
               "workload": tag,
               # the kernel build these counters describe (bench.py refuses them
               # for any other): hash of the kernel sources + the library's rev
@@ -96,6 +97,14 @@ def main():
                 e["grbm_gui_active"] = c["GRBM_GUI_ACTIVE"]
                 e["valu_util_2cyc"] = c["SQ_INSTS_VALU"] * 2 / (cyc * 1024) if cyc else None
                 e["valu_util_4cyc"] = c["SQ_INSTS_VALU"] * 4 / (cyc * 1024) if cyc else None
+            if "SQ_ACTIVE_INST_VALU" in c:
+                # rocprof's VALUBusy: SQ_ACTIVE_INST_VALU (quad-cycles, summed
+                # over waves) x 4 / (SIMDs x GRBM_GUI_ACTIVE per XCD); the
+                # GRBM_GUI_ACTIVE of the same pass when collected there
+                e = tr["kernels"].setdefault(k, {})
+                g = c.get("GRBM_GUI_ACTIVE")
+                e["sq_active_inst_valu"] = c["SQ_ACTIVE_INST_VALU"]
+                e["valu_busy"] = (c["SQ_ACTIVE_INST_VALU"] * 4 / (g / 8.0 * 1024)) if g else None
         path = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--traffic-out=")),
                     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                  "profiles", "traffic.json"))

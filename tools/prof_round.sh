@@ -19,7 +19,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 rc=$?; [ $rc -eq 0 ] || [ $rc -eq 3 ] || stop prof $rc
 python3 tools/prof_check.py gpurun_out/prof/run_kernel_trace.csv gpurun_out/prof_bench.json \
   gpurun_out/prof_check.json; cat gpurun_out/prof_check.json | head -30
-for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU GRBM_GUI_ACTIVE"; do
+for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU GRBM_GUI_ACTIVE" "SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
   tag=$(echo $grp | tr ' ' '_' | cut -c1-40)
   BH_LANES=1 BH_KEYS_FIRST=0 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv \
     -d gpurun_out/pmc_$tag -o pmc -- python3 bench.py --steps 1 --warmup 0 --cpu-baseline 0 \
@@ -27,7 +27,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU GRBM_GUI_ACTIVE"; do
   rc=$?; [ $rc -eq 0 ] || [ $rc -eq 3 ] || stop "pmc $grp" $rc
 done
 python3 tools/pmc_summary.py gpurun_out gpurun_out/pmc_summary.json --traffic \
-  --workload=config2:n1048576 --source=profiles/${PROF_TAG:-r05} \
+  --workload=config2:n1048576 --source=profiles/${PROF_TAG:-r06} \
   --traffic-out=gpurun_out/traffic.json > gpurun_out/pmc_summary.txt 2>&1 || echo "pmc_summary failed"
 timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.json \
   2> gpurun_out/bench.err; rc=$?; [ $rc -eq 0 ] || [ $rc -eq 3 ] || stop bench $rc
