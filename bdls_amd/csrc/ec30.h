@@ -162,8 +162,7 @@ BH_HD void j_zaddu(J30& r, J30& p, const J30& q) {
   f_sqr<F>(d, t2);                        // [b2]   D = (Y1 - Y2)^2
   f_sub<F, 32>(t3, w1, w2);               // [b34]
   f_mul<F>(p.Y, p.Y, t3);                 // [b2]   A1 = Y1 (W1 - W2)
-  f_add(t3, w1, w2);                      // [b4]
-  f_sub<F, 32>(r.X, d, t3);               // [b34]  X3 = D - W1 - W2
+  f_sub2<F, 32>(r.X, d, w1, w2);          // [b34]  X3 = D - W1 - W2 (one pass)
   f_sub<F, 64>(t3, w1, r.X);              // [b66]
   f_mul<F>(t3, t2, t3);                   // [b2]   128*66
   f_sub<F, 32>(r.Y, t3, p.Y);             // [b34]  Y3 = (Y1 - Y2)(W1 - X3) - A1
@@ -172,175 +171,117 @@ BH_HD void j_zaddu(J30& r, J30& p, const J30& q) {
   f_copy(p.Z, r.Z);
 }
 
-// r = p + q (Jacobian, neither at infinity). Requires beta <= 63 on X1, Y1,
-// X2, Y2 and beta <= 34 on Z1, Z2... (products below stay <= 16000).
-// Output beta (34, 34, 2). Returns true iff x(p) == x(q) (degenerate); then r
-// is garbage and *same_y says p == q (double) vs p == -q (infinity).
+// Degenerate-case resolution shared by the additions: called only when Z3 is
+// 0 mod p (x1 == x2); same_y from the canonical r = S2 - S1.
+template <class F>
+BH_HD bool j_degenerate(const uint32_t z3[9], const uint32_t rr[9], bool* same_y) {
+  const bool degenerate = f_is_zero2<F>(z3);
+  if (degenerate) {  // rare: decide double vs infinity on the canonical r
+    uint32_t t[9];
+    f_reduce<F>(t, rr);
+    uint32_t z = 0;
+    for (int i = 0; i < 9; i++) z |= t[i];
+    *same_y = (z == 0);
+  } else {
+    *same_y = false;
+  }
+  return degenerate;
+}
+
+// r = p + (+-q) (Jacobian, neither at infinity; neg adds -q: q's sign folded
+// into r = S2 - S1, f_csub). With CO, pz = p rescaled to r's Z, (U1 H^2,
+// S1 H^3, Z3) -- both intermediates of the addition, the co-Z partner j_zaddu
+// needs for 2 p + q = (p + q) + p. Requires beta <= 63 on X1, Y1, X2, Y2 and
+// beta <= 34 on Z1, Z2 (products below stay <= 16000). Output beta (34, 34,
+// 2), pz (2, 2, 2). Returns true iff x(p) == x(q) (degenerate); then r is
+// garbage and *same_y says p == +-q (double) vs p == -(+-q) (infinity). r may
+// alias p. Round 6: H^3 + 2V once (f_add2x), X3 and V - X3 from it in one
+// pass each (was five passes), the sign in the r pass (was a negation + select).
+template <class F, bool CO>
+BH_HD bool j_add_impl(J30& r, J30* pz, const J30& p, const J30& q, bool neg, bool* same_y) {
+  uint32_t z1z1[9], z2z2[9], u1[9], u2[9], s1[9], s2[9], h[9], rr[9], t[9], hh[9], hhh[9], w[9];
+  f_sqr<F>(z1z1, p.Z);                    // [b2]
+  f_sqr<F>(z2z2, q.Z);                    // [b2]
+  f_mul<F>(u1, p.X, z2z2);                // [b2]
+  f_mul<F>(u2, q.X, z1z1);                // [b2]
+  f_mul<F>(t, q.Z, z2z2);                 // [b2]
+  f_mul<F>(s1, p.Y, t);                   // [b2]
+  f_mul<F>(t, p.Z, z1z1);                 // [b2]
+  f_mul<F>(s2, q.Y, t);                   // [b2]
+  f_sub<F, 32>(h, u2, u1);                // [b34]
+  f_csub<F, 32>(rr, neg, s2, s1);         // [b34]  +-S2 - S1
+  f_sqr<F>(hh, h);                        // [b2]
+  f_mul<F>(hhh, hh, h);                   // [b2]
+  f_mul<F>(u1, u1, hh);                   // [b2]  V = U1 H^2
+  f_sqr<F>(t, rr);                        // [b2]  r^2
+  f_add2x(w, hhh, u1);                    // [b6]  H^3 + 2V
+  f_sub<F, 32>(r.X, t, w);                // [b34] X3 = r^2 - H^3 - 2V
+  f_addsub<F, 32>(u2, w, u1, t);          // [b40] V - X3 = 3V + H^3 - r^2
+  f_mul<F>(u2, rr, u2);                   // [b2]  34*40
+  f_mul<F>(s1, s1, hhh);                  // [b2]  S1 H^3
+  f_sub<F, 32>(r.Y, u2, s1);              // [b34] Y3 = r (V - X3) - S1 H^3
+  f_mul<F>(t, p.Z, q.Z);                  // [b2]
+  f_mul<F>(r.Z, t, h);                    // [b2]  Z3 = Z1 Z2 H
+  if constexpr (CO) {
+    f_copy(pz->X, u1);
+    f_copy(pz->Y, s1);
+    f_copy(pz->Z, r.Z);
+  }
+  return j_degenerate<F>(r.Z, rr, same_y);
+}
+
 template <class F>
 BH_HD bool j_add(J30& r, const J30& p, const J30& q, bool* same_y) {
-  uint32_t z1z1[9], z2z2[9], u1[9], u2[9], s1[9], s2[9], h[9], rr[9], t[9], hh[9], hhh[9];
-  f_sqr<F>(z1z1, p.Z);                    // [b2]
-  f_sqr<F>(z2z2, q.Z);                    // [b2]
-  f_mul<F>(u1, p.X, z2z2);                // [b2]
-  f_mul<F>(u2, q.X, z1z1);                // [b2]
-  f_mul<F>(t, q.Z, z2z2);                 // [b2]
-  f_mul<F>(s1, p.Y, t);                   // [b2]
-  f_mul<F>(t, p.Z, z1z1);                 // [b2]
-  f_mul<F>(s2, q.Y, t);                   // [b2]
-  f_sub<F, 32>(h, u2, u1);                // [b34]
-  f_sub<F, 32>(rr, s2, s1);               // [b34]
-  f_sqr<F>(hh, h);                        // [b2]
-  f_mul<F>(hhh, hh, h);                   // [b2]
-  f_mul<F>(u1, u1, hh);                   // [b2]  v = U1 H^2
-  f_sqr<F>(t, rr);                        // [b2]  r^2
-  // X3 = r^2 - H^3 - 2V
-  f_mulc<2>(u2, u1);                      // [b4]
-  f_add(u2, u2, hhh);                     // [b6]
-  f_sub<F, 32>(r.X, t, u2);               // [b34]
-  // Y3 = r (V - X3) - S1 H^3 = r (3V + H^3 - r^2) - S1 H^3
-  f_mulc<3>(u2, u1);                      // [b6]
-  f_add(u2, u2, hhh);                     // [b8]
-  f_sub<F, 32>(u2, u2, t);                // [b40]
-  f_mul<F>(u2, rr, u2);                   // [b2]  34*40
-  f_mul<F>(s1, s1, hhh);                  // [b2]
-  f_sub<F, 32>(r.Y, u2, s1);              // [b34]
-  // Z3 = Z1 Z2 H
-  f_mul<F>(t, p.Z, q.Z);                  // [b2]
-  f_mul<F>(r.Z, t, h);                    // [b2]
-  const bool degenerate = f_is_zero2<F>(r.Z);
-  if (degenerate) {  // rare: decide double vs infinity on the canonical r
-    f_reduce<F>(t, rr);
-    uint32_t z = 0;
-    for (int i = 0; i < 9; i++) z |= t[i];
-    *same_y = (z == 0);
-  } else {
-    *same_y = false;
-  }
-  return degenerate;
+  return j_add_impl<F, false>(r, nullptr, p, q, false, same_y);
+}
+template <class F>
+BH_HD bool j_add_co(J30& r, J30& pz, const J30& p, const J30& q, bool* same_y, bool neg = false) {
+  return j_add_impl<F, true>(r, &pz, p, q, neg, same_y);
 }
 
-// r = p + (x2, y2, 1). Requires beta <= 63 on X1, Y1; beta(Z1) <= 34;
-// beta(x2), beta(y2) <= 64. Output beta (34, 34, 2). Degenerate contract as j_add.
-template <class F>
-BH_HD bool j_madd(J30& r, const J30& p, const uint32_t x2[9], const uint32_t y2[9],
-                  bool* same_y) {
-  uint32_t z1z1[9], u2[9], s2[9], h[9], rr[9], t[9], hh[9], hhh[9];
+// r = p + (x2, +-y2, 1) (mixed; neg adds (x2, -y2)). Requires beta <= 63 on X1
+// (and on Y1 when !neg, <= 62 when neg: the sign pass needs S2 + Y1 <= 64 p),
+// beta(Z1) <= 34, beta(x2), beta(y2) <= 64. Output beta (34, 34, 2); with CO, pz = (X1 H^2, Y1 H^3, Z3) beta
+// (2, 2, 2) (j_madd_co: the composite 2 p + q = (p + q) + p). Degenerate
+// contract as j_add_impl; r may alias p.
+template <class F, bool CO>
+BH_HD bool j_madd_impl(J30& r, J30* pz, const J30& p, const uint32_t x2[9], const uint32_t y2[9],
+                       bool neg, bool* same_y) {
+  uint32_t z1z1[9], u2[9], s2[9], h[9], rr[9], t[9], hh[9], hhh[9], v[9], w[9];
   f_sqr<F>(z1z1, p.Z);                    // [b2]
   f_mul<F>(u2, x2, z1z1);                 // [b2]
   f_mul<F>(t, p.Z, z1z1);                 // [b2]
   f_mul<F>(s2, y2, t);                    // [b2]
   f_sub<F, 64>(h, u2, p.X);               // [b66]
-  f_sub<F, 64>(rr, s2, p.Y);              // [b66]
+  f_csub<F, 64>(rr, neg, s2, p.Y);        // [b66]  +-S2 - Y1
   f_sqr<F>(hh, h);                        // [b2]  4356
   f_mul<F>(hhh, hh, h);                   // [b2]
-  f_mul<F>(u2, p.X, hh);                  // [b2]  V = X1 H^2
+  f_mul<F>(v, p.X, hh);                   // [b2]  V = X1 H^2
   f_sqr<F>(t, rr);                        // [b2]
-  f_mulc<2>(s2, u2);                      // [b4]
-  f_add(s2, s2, hhh);                     // [b6]
-  f_sub<F, 32>(r.X, t, s2);               // [b34]  X3 = r^2 - H^3 - 2V
-  f_mulc<3>(s2, u2);                      // [b6]
-  f_add(s2, s2, hhh);                     // [b8]
-  f_sub<F, 32>(s2, s2, t);                // [b40]  V - X3
-  f_mul<F>(s2, rr, s2);                   // [b2]   66*40
-  f_mul<F>(t, p.Y, hhh);                  // [b2]
+  f_add2x(w, hhh, v);                     // [b6]  H^3 + 2V
+  f_sub<F, 32>(r.X, t, w);                // [b34] X3 = r^2 - H^3 - 2V
+  f_addsub<F, 32>(s2, w, v, t);           // [b40] V - X3
+  f_mul<F>(s2, rr, s2);                   // [b2]  66*40
+  f_mul<F>(t, p.Y, hhh);                  // [b2]  Y1 H^3
   f_sub<F, 32>(r.Y, s2, t);               // [b34]
-  f_mul<F>(r.Z, p.Z, h);                  // [b2]   34*66
-  const bool degenerate = f_is_zero2<F>(r.Z);
-  if (degenerate) {
-    f_reduce<F>(t, rr);
-    uint32_t z = 0;
-    for (int i = 0; i < 9; i++) z |= t[i];
-    *same_y = (z == 0);
-  } else {
-    *same_y = false;
+  f_mul<F>(r.Z, p.Z, h);                  // [b2]  34*66
+  if constexpr (CO) {
+    f_copy(pz->X, v);
+    f_copy(pz->Y, t);
+    f_copy(pz->Z, r.Z);
   }
-  return degenerate;
+  return j_degenerate<F>(r.Z, rr, same_y);
 }
 
-// j_madd that also returns pz = p rescaled to r's Z: (X1 H^2, Y1 H^3, Z3) --
-// both are intermediates of the addition, so pz is free; it is the co-Z
-// partner j_zaddu needs for the composite 2 p + q = (p + q) + p. Requirements
-// and degenerate contract as j_madd (r may alias p). pz beta (2, 2, 2).
+template <class F>
+BH_HD bool j_madd(J30& r, const J30& p, const uint32_t x2[9], const uint32_t y2[9], bool* same_y,
+                  bool neg = false) {
+  return j_madd_impl<F, false>(r, nullptr, p, x2, y2, neg, same_y);
+}
 template <class F>
 BH_HD bool j_madd_co(J30& r, J30& pz, const J30& p, const uint32_t x2[9], const uint32_t y2[9],
-                     bool* same_y) {
-  uint32_t z1z1[9], u2[9], s2[9], h[9], rr[9], t[9], hh[9], hhh[9];
-  f_sqr<F>(z1z1, p.Z);                    // [b2]
-  f_mul<F>(u2, x2, z1z1);                 // [b2]
-  f_mul<F>(t, p.Z, z1z1);                 // [b2]
-  f_mul<F>(s2, y2, t);                    // [b2]
-  f_sub<F, 64>(h, u2, p.X);               // [b66]
-  f_sub<F, 64>(rr, s2, p.Y);              // [b66]
-  f_sqr<F>(hh, h);                        // [b2]
-  f_mul<F>(hhh, hh, h);                   // [b2]
-  f_mul<F>(pz.X, p.X, hh);                // [b2]   V = X1 H^2
-  f_sqr<F>(t, rr);                        // [b2]
-  f_mulc<2>(s2, pz.X);                    // [b4]
-  f_add(s2, s2, hhh);                     // [b6]
-  f_sub<F, 32>(r.X, t, s2);               // [b34]  X3 = r^2 - H^3 - 2V
-  f_mulc<3>(s2, pz.X);                    // [b6]
-  f_add(s2, s2, hhh);                     // [b8]
-  f_sub<F, 32>(s2, s2, t);                // [b40]  V - X3
-  f_mul<F>(s2, rr, s2);                   // [b2]   66*40
-  f_mul<F>(pz.Y, p.Y, hhh);               // [b2]   Y1 H^3
-  f_sub<F, 32>(r.Y, s2, pz.Y);            // [b34]
-  f_mul<F>(r.Z, p.Z, h);                  // [b2]   34*66
-  f_copy(pz.Z, r.Z);
-  const bool degenerate = f_is_zero2<F>(r.Z);
-  if (degenerate) {
-    f_reduce<F>(t, rr);
-    uint32_t z = 0;
-    for (int i = 0; i < 9; i++) z |= t[i];
-    *same_y = (z == 0);
-  } else {
-    *same_y = false;
-  }
-  return degenerate;
-}
-
-// j_add that also returns pz = p rescaled to r's Z: (U1 H^2, S1 H^3, Z3) with
-// U1 = X1 Z2^2, S1 = Y1 Z2^3 (Z3 = Z1 Z2 H) -- intermediates of the addition,
-// the co-Z partner j_zaddu needs for 2 p + q = (p + q) + p. Requirements and
-// degenerate contract as j_add (r may alias p). pz beta (2, 2, 2).
-template <class F>
-BH_HD bool j_add_co(J30& r, J30& pz, const J30& p, const J30& q, bool* same_y) {
-  uint32_t z1z1[9], z2z2[9], u1[9], u2[9], s1[9], s2[9], h[9], rr[9], t[9], hh[9], hhh[9];
-  f_sqr<F>(z1z1, p.Z);                    // [b2]
-  f_sqr<F>(z2z2, q.Z);                    // [b2]
-  f_mul<F>(u1, p.X, z2z2);                // [b2]
-  f_mul<F>(u2, q.X, z1z1);                // [b2]
-  f_mul<F>(t, q.Z, z2z2);                 // [b2]
-  f_mul<F>(s1, p.Y, t);                   // [b2]
-  f_mul<F>(t, p.Z, z1z1);                 // [b2]
-  f_mul<F>(s2, q.Y, t);                   // [b2]
-  f_sub<F, 32>(h, u2, u1);                // [b34]
-  f_sub<F, 32>(rr, s2, s1);               // [b34]
-  f_sqr<F>(hh, h);                        // [b2]
-  f_mul<F>(hhh, hh, h);                   // [b2]
-  f_mul<F>(pz.X, u1, hh);                 // [b2]  V = U1 H^2
-  f_sqr<F>(t, rr);                        // [b2]  r^2
-  f_mulc<2>(u2, pz.X);                    // [b4]
-  f_add(u2, u2, hhh);                     // [b6]
-  f_sub<F, 32>(r.X, t, u2);               // [b34]  X3 = r^2 - H^3 - 2V
-  f_mulc<3>(u2, pz.X);                    // [b6]
-  f_add(u2, u2, hhh);                     // [b8]
-  f_sub<F, 32>(u2, u2, t);                // [b40]
-  f_mul<F>(u2, rr, u2);                   // [b2]  34*40
-  f_mul<F>(pz.Y, s1, hhh);                // [b2]  S1 H^3
-  f_sub<F, 32>(r.Y, u2, pz.Y);            // [b34]
-  f_mul<F>(t, p.Z, q.Z);                  // [b2]
-  f_mul<F>(r.Z, t, h);                    // [b2]
-  f_copy(pz.Z, r.Z);
-  const bool degenerate = f_is_zero2<F>(r.Z);
-  if (degenerate) {
-    f_reduce<F>(t, rr);
-    uint32_t z = 0;
-    for (int i = 0; i < 9; i++) z |= t[i];
-    *same_y = (z == 0);
-  } else {
-    *same_y = false;
-  }
-  return degenerate;
+                     bool* same_y, bool neg = false) {
+  return j_madd_impl<F, true>(r, &pz, p, x2, y2, neg, same_y);
 }
 
 // y^2 == x^3 + a x + b for Montgomery-domain x, y with beta <= 2.

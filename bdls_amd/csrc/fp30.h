@@ -192,6 +192,102 @@ BH_HD void f_sub(uint32_t r[9], const uint32_t a[9], const uint32_t b[9]) {
   r[8] = a[8] + k8 - b[8] + c;
 }
 
+// K p in a borrowed form that lends B 2^30 to every limb below the top:
+// limb 0 = n_0 + B 2^30, limbs 1..7 = n_i + B 2^30 - B, limb 8 = n_8 - B
+// (n = K p's normalised limbs). B = 1 is the k32 / k64 form; B = 2 leaves
+// every limb >= 2^31 - 2, so TWO normalised limbs can be subtracted from it in
+// one pass (round 6: the fused passes below, one carry chain where the
+// formulas had two or three).
+struct Limbs9 {
+  uint32_t v[9];
+};
+template <class F, int K, int B>
+constexpr Limbs9 kp_borrowed() {
+  Limbs9 r{};
+  uint64_t c = 0;
+  for (int i = 0; i < 9; i++) {
+    const uint64_t t = (uint64_t)F::p[i] * (uint64_t)K + c;
+    const uint64_t n = i < 8 ? (t & kM30) : t;
+    c = i < 8 ? (t >> 30) : 0;
+    r.v[i] = (uint32_t)(n + (i < 8 ? ((uint64_t)B << 30) : 0) - (i > 0 ? (uint64_t)B : 0));
+  }
+  return r;
+}
+template <class F, int K, int B>
+struct KpB {
+  static constexpr Limbs9 k = kp_borrowed<F, K, B>();
+  static_assert(k.v[8] < (1u << 26), "K p's top limb covers the borrow");
+};
+
+// r = a + 2 b, limbs re-normalised (beta_a + 2 beta_b): H^3 + 2V of the
+// additions in one pass (t < 3 * 2^30 + 3).
+BH_HD void f_add2x(uint32_t r[9], const uint32_t a[9], const uint32_t b[9]) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t t = a[i] + (b[i] << 1) + c;
+    r[i] = t & kM30;
+    c = t >> 30;
+  }
+  r[8] = a[8] + (b[8] << 1) + c;
+}
+
+// r = a + b - c + K p (K = 32 or 64) in one pass instead of f_add then f_sub.
+// Requires value(c) <= K p; returns beta_a + beta_b + K. A limb never leaves
+// u32: a_i + b_i + kk_i + carry <= 2 (2^30 - 1) + (2^31 - 2) + 3 < 2^32 (the
+// B = 1 borrowed limbs are <= n_i + 2^30 - 1), and kk_i >= c_i.
+template <class F, int K>
+BH_HD void f_addsub(uint32_t r[9], const uint32_t a[9], const uint32_t b[9], const uint32_t c[9]) {
+  static_assert(K == 32 || K == 64, "K");
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t kk = (K == 32) ? F::k32[i] : F::k64[i];
+    const uint32_t t = a[i] + b[i] + kk + cy - c[i];
+    r[i] = t & kM30;
+    cy = t >> 30;
+  }
+  const uint32_t k8 = (K == 32) ? F::k32[8] : F::k64[8];
+  r[8] = a[8] + b[8] + k8 + cy - c[8];
+}
+
+// r = a - b - c + K p in one pass (the B = 2 borrowed K p: kk_i >= b_i + c_i,
+// and a_i + kk_i + carry <= (2^30 - 1) + (2^31 + 2^30 - 3) + 3 < 2^32).
+// Requires value(b) + value(c) <= K p; returns beta_a + K.
+template <class F, int K>
+BH_HD void f_sub2(uint32_t r[9], const uint32_t a[9], const uint32_t b[9], const uint32_t c[9]) {
+  constexpr Limbs9 kk = KpB<F, K, 2>::k;
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t t = a[i] + kk.v[i] + cy - b[i] - c[i];
+    r[i] = t & kM30;
+    cy = t >> 30;
+  }
+  r[8] = a[8] + kk.v[8] + cy - b[8] - c[8];
+}
+
+// r = (neg ? -s : s) - y + K p in one pass: a table point's sign folded into
+// the subtraction that consumes its y (the additions' r = S2 - Y1), instead of
+// negating y and selecting first. Per limb the true value kk_i +- s_i - y_i +
+// carry lies in [0, 2^32) (B = 2 borrowed K p), so the u32 wrap of -s_i is
+// exact. Requires value(s) + value(y) <= K p when neg, value(y) <= K p else;
+// returns K (neg) or beta_s + K.
+template <class F, int K>
+BH_HD void f_csub(uint32_t r[9], bool neg, const uint32_t s[9], const uint32_t y[9]) {
+  constexpr Limbs9 kk = KpB<F, K, 2>::k;
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t x = neg ? 0u - s[i] : s[i];
+    const uint32_t t = kk.v[i] + x + cy - y[i];
+    r[i] = t & kM30;
+    cy = t >> 30;
+  }
+  const uint32_t x8 = neg ? 0u - s[8] : s[8];
+  r[8] = kk.v[8] + x8 + cy - y[8];
+}
+
 // r = K p - a
 template <class F, int K>
 BH_HD void f_neg(uint32_t r[9], const uint32_t a[9]) {
@@ -246,8 +342,12 @@ BH_HD bool f_eq(const uint32_t a[9], const uint32_t b[9]) {
 }
 
 // beta <= 2 and normalised: value == 0 mod p  <=>  a in {0, p}
+// (round 6: limb 0 filters first -- a value in {0, p} has limb 0 in {0, p_0} --
+// so the hot formulas' degenerate checks cost a compare, and the full test
+// runs only in the branch the lanes almost never take)
 template <class F>
 BH_HD bool f_is_zero2(const uint32_t a[9]) {
+  if (a[0] != 0u && a[0] != F::p[0]) return false;
   uint32_t z = 0, q = 0;
 #pragma unroll
   for (int i = 0; i < 9; i++) {

@@ -1825,12 +1825,10 @@ BH_HD void g2_column(const uint64_t gl[kLLTeeth], int j, uint32_t& idx, bool& ne
 template <class P>
 BH_HD void ll_madd(J30& A, bool& a_inf, const uint32_t tx[9], uint32_t ty[9], bool neg,
                    const uint32_t one[9]) {
-  uint32_t nty[9];
-  f_neg<P, 64>(nty, ty);
-  f_sel(ty, neg, nty, ty);
   bool same;
-  const bool deg = j_madd<P>(A, A, tx, ty, &same);
+  const bool deg = j_madd<P>(A, A, tx, ty, &same, neg);  // the sign in its r pass
   if (a_inf || deg) {  // rare (crafted scalars)
+    if (neg) f_neg<P, 64>(ty, ty);
     if (a_inf || same) {
       J30 T;
       f_copy(T.X, tx);
@@ -1851,13 +1849,13 @@ BH_HD void ll_madd(J30& A, bool& a_inf, const uint32_t tx[9], uint32_t ty[9], bo
 // (round 5). Degenerate cases, as branches the lanes skip together: A at
 // infinity -> T; A == T -> 3 T = 2 T + T; A == -T -> A; A + T == -A (the
 // co-Z sum's x difference is 0; A + T == A would need T = 0) -> infinity.
+// Round 6: the sign of T is folded into the mixed addition's r pass (f_csub);
+// ty is negated in place only on the rare branches that use T itself.
 template <class P>
 BH_HD void ll_dbladd(J30& A, bool& a_inf, const uint32_t tx[9], uint32_t ty[9], bool neg,
                      const uint32_t one[9]) {
-  uint32_t nty[9];
-  f_neg<P, 64>(nty, ty);
-  f_sel(ty, neg, nty, ty);
   if (a_inf) {  // rare: 2 inf + T
+    if (neg) f_neg<P, 64>(ty, ty);
     f_copy(A.X, tx);
     f_copy(A.Y, ty);
     f_copy(A.Z, one);
@@ -1866,7 +1864,8 @@ BH_HD void ll_dbladd(J30& A, bool& a_inf, const uint32_t tx[9], uint32_t ty[9], 
   }
   J30 R, Az;
   bool same;
-  if (j_madd_co<P>(R, Az, A, tx, ty, &same)) {  // rare: A == +-T
+  if (j_madd_co<P>(R, Az, A, tx, ty, &same, neg)) {  // rare: A == +-T
+    if (neg) f_neg<P, 64>(ty, ty);
     J30 T;
     f_copy(T.X, tx);
     f_copy(T.Y, ty);
@@ -1949,19 +1948,22 @@ BH_HD bool stage_keycomb_fold(const Work& w, uint32_t i, const uint32_t* tab, ui
 // 13 of them against the 13-bit G comb's 20 plus the final A + B. Per verify
 // ~3,070 F_p ops against ~3,280 (3,200).
 //
-// A = 2 A + T for a Jacobian T (already signed), degenerate cases as
-// ll_dbladd: A at infinity -> T; A == T -> 3 T; A == -T -> A (unchanged);
+// A = 2 A + (+-T) for a Jacobian T (neg: -T, the sign folded into the
+// addition's r pass; T.Y is negated in place only on the rare branches that
+// use T itself), degenerate cases as ll_dbladd: A at infinity -> T; A == T -> 3 T; A == -T -> A (unchanged);
 // A + T == -A -> infinity.
 template <class P>
-BH_HD void j_dbladd(J30& A, bool& a_inf, const J30& T) {
+BH_HD void j_dbladd(J30& A, bool& a_inf, J30& T, bool neg) {
   if (a_inf) {  // rare: 2 inf + T
+    if (neg) f_neg<P, 64>(T.Y, T.Y);
     j_copy(A, T);
     a_inf = false;
     return;
   }
   J30 R, Az;
   bool same;
-  if (j_add_co<P>(R, Az, A, T, &same)) {  // rare: A == +-T
+  if (j_add_co<P>(R, Az, A, T, &same, neg)) {  // rare: A == +-T (the sign in its r pass)
+    if (neg) f_neg<P, 64>(T.Y, T.Y);
     if (same) {
       J30 D;
       j_dbl<P>(D, T);
@@ -2053,8 +2055,7 @@ BH_HD void q_ladder_odd_g(J30& A, bool& a_inf, const Work& w, uint32_t i, uint32
       j_dbl<P>(A, A);  // (while a_inf, A is a placeholder the next point replaces)
       if (g_fold_pos(5 * win + 5 - d)) g_add();
     }
-    if (neg) f_neg<P, 64>(T.Y, T.Y);
-    j_dbladd<P>(A, a_inf, T);
+    j_dbladd<P>(A, a_inf, T, neg);
     if (g_fold_pos(5 * win)) g_add();
   }
 }

@@ -261,6 +261,22 @@ extern "C" void hs_f_sub64(const uint32_t* a, const uint32_t* b, uint32_t* r) {
 extern "C" void hs_f_add(const uint32_t* a, const uint32_t* b, uint32_t* r) { f_add(r, a, b); }
 extern "C" void hs_f_reduce(const uint32_t* a, uint32_t* r) { f_reduce<F30_p256>(r, a); }
 extern "C" void hs_f_sqr(const uint32_t* a, uint32_t* r) { f_sqr<F30_p256>(r, a); }
+// round 6's fused passes, both curves (curve 0 = P-256, 1 = secp256k1), K = 32 / 64
+template <class F, int K>
+static void fused(int op, const uint32_t* a, const uint32_t* b, const uint32_t* c, uint32_t* r) {
+  switch (op) {
+    case 0: f_add2x(r, a, b); break;
+    case 1: f_addsub<F, K>(r, a, b, c); break;
+    case 2: f_sub2<F, K>(r, a, b, c); break;
+    case 3: f_csub<F, K>(r, false, a, b); break;
+    case 4: f_csub<F, K>(r, true, a, b); break;
+  }
+}
+extern "C" void hs_f_fused(int curve, int K, int op, const uint32_t* a, const uint32_t* b,
+                           const uint32_t* c, uint32_t* r) {
+  if (curve == 0) (K == 32 ? fused<F30_p256, 32> : fused<F30_p256, 64>)(op, a, b, c, r);
+  else (K == 32 ? fused<F30_k1, 32> : fused<F30_k1, 64>)(op, a, b, c, r);
+}
 extern "C" void hs_bdls_hash(uint32_t version, const uint8_t* x32, const uint8_t* y32,
                              const uint8_t* msg, uint32_t mlen, uint8_t* out) {
   bdls_signed_proto_hash(out, version, x32, y32, msg, mlen);

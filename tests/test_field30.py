@@ -1,7 +1,11 @@
 """CPU: the radix-2^30 lazy field (bdls_amd/csrc/fp30.h, compiled for the host by
 the test-only harness) at the edges of its value contract:
   f_mul needs beta_a * beta_b <= 16000 (tested to 16000; the formulas stay <= 9604) and returns t < 2p, t == a b 2^-270 (mod p);
-  f_sub<K> needs beta_b <= K - 1 and returns a - b + K p with normalised limbs.
+  f_sub<K> needs beta_b <= K - 1 and returns a - b + K p with normalised limbs;
+  round 6's fused one-pass forms (f_add2x a + 2b, f_addsub a + b - c + K p,
+  f_sub2 a - b - c + K p, f_csub +-s - y + K p) on both curves, with values and
+  limb patterns (every limb 0 or 2^30 - 1) at their contracts' edges: a limb
+  sum leaving u32 would show as a wrong value.
 Values are drawn at the bounds (beta p - 1, all-ones limbs, 0, p) to catch
 64-bit column overflow."""
 import ctypes
@@ -101,3 +105,59 @@ def test_f_sqr_bounds(L, ba):
         t = from9(out)
         assert normalised(out) and t < 2 * P
         assert t % P == a * a * Rinv % P
+
+
+P_K1 = 2**256 - 2**32 - 977
+
+
+def limb_patterns(beta, p, rng, k=30):
+    """Values <= beta p - 1 whose low limbs are each 0 or 2^30 - 1 (the per-limb
+    extremes of the fused passes' u32 sums), top limb as large as allowed."""
+    hi = beta * p - 1
+    out = []
+    for _ in range(k):
+        low = sum((M if rng.random() < 0.5 else 0) << (30 * i) for i in range(8))
+        top = (hi - low) >> 240
+        if top >= 0:
+            out.append(low + (top << 240))
+    return out
+
+
+def edge_all(beta, p, rng, k=12):
+    return [v for v in edge_values(beta, rng, k) if v <= beta * p - 1] + limb_patterns(beta, p, rng)
+
+
+@pytest.mark.parametrize("curve", [0, 1])
+@pytest.mark.parametrize("K", [32, 64])
+def test_fused_passes(L, curve, K):
+    p = P if curve == 0 else P_K1
+    rng = random.Random(curve * 100 + K)
+    out = (ctypes.c_uint32 * 9)()
+    call = L.hs_f_fused
+    z = to9(0)
+    # f_add2x: a + 2 b (the formulas: H^3 + 2V, beta 2 + 2 * 2)
+    for a in edge_all(34, p, rng):
+        for b in edge_all(34, p, rng, 4):
+            call(curve, K, 0, to9(a), to9(b), z, out)
+            assert normalised(out) and from9(out) == a + 2 * b
+    # f_addsub: a + b - c + K p, value(c) <= K p (V - X3 = w + V - r^2, beta 6 + 2 + 32)
+    for a in edge_all(34, p, rng):
+        for b in edge_all(34, p, rng, 3):
+            for c in edge_all(K, p, rng, 3):
+                call(curve, K, 1, to9(a), to9(b), to9(c), out)
+                assert normalised(out) and from9(out) == a + b - c + K * p
+    # f_sub2: a - b - c + K p, value(b) + value(c) <= K p (X3 = D - W1 - W2)
+    for a in edge_all(66, p, rng):
+        for bb, bc in ((K // 2, K // 2), (2, K - 2), (K - 2, 2)):
+            for b in edge_all(bb, p, rng, 3):
+                for c in edge_all(bc, p, rng, 3):
+                    call(curve, K, 2, to9(a), to9(b), to9(c), out)
+                    assert normalised(out) and from9(out) == a - b - c + K * p
+    # f_csub: (+-s) - y + K p (the additions' r with the table point's sign)
+    for s_ in edge_all(2, p, rng):
+        for y in edge_all(K, p, rng, 6):
+            call(curve, K, 3, to9(s_), to9(y), z, out)
+            assert normalised(out) and from9(out) == s_ - y + K * p
+        for y in edge_all(K - 2, p, rng, 6):
+            call(curve, K, 4, to9(s_), to9(y), z, out)
+            assert normalised(out) and from9(out) == K * p - s_ - y

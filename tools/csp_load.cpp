@@ -10,6 +10,7 @@
 //
 // register = 1: the records' keys are registered before timing.
 #include <pthread.h>
+#include <sys/resource.h>
 
 #include <algorithm>
 #include <atomic>
@@ -124,6 +125,8 @@ int main(int argc, char** argv) {
   }
   unsigned long long thr0, us0, thr1, us1;
   cpu_stat(&thr0, &us0);
+  struct rusage ru0, ru1;
+  getrusage(RUSAGE_SELF, &ru0);
   const auto t0 = std::chrono::steady_clock::now();
   {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -132,6 +135,12 @@ int main(int argc, char** argv) {
   g_cv.notify_all();
   for (int t = 0; t < T; t++) pthread_join(th[t], nullptr);
   cpu_stat(&thr1, &us1);
+  getrusage(RUSAGE_SELF, &ru1);
+  auto tv_ms = [](const timeval& a, const timeval& b) {
+    return (b.tv_sec - a.tv_sec) * 1e3 + (b.tv_usec - a.tv_usec) / 1e3;
+  };
+  const double user_ms = tv_ms(ru0.ru_utime, ru1.ru_utime), sys_ms = tv_ms(ru0.ru_stime, ru1.ru_stime);
+  const long nvcsw = ru1.ru_nvcsw - ru0.ru_nvcsw, nivcsw = ru1.ru_nivcsw - ru0.ru_nivcsw;
   const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   bh_csp_stats(st1);
   std::vector<double> all;
@@ -142,10 +151,11 @@ int main(int argc, char** argv) {
          "\"p999_us\": %.1f, \"max_us\": %.1f, "
          "\"verifies_per_s\": %.1f, \"device_batches\": %llu, \"max_batch\": %llu, "
          "\"registered_before\": %s, \"bad\": %d, \"cgroup_nr_throttled\": %llu, "
-         "\"cgroup_throttled_us\": %llu}\n",
+         "\"cgroup_throttled_us\": %llu, \"wall_ms\": %.1f, \"cpu_user_ms\": %.1f, "
+         "\"cpu_sys_ms\": %.1f, \"vol_csw\": %ld, \"invol_csw\": %ld}\n",
          T, all.size(), pct(0.5), pct(0.99), pct(0.999), all.back(), all.size() / el,
          (unsigned long long)(st1[1] - st0[1]), (unsigned long long)st1[2], reg ? "true" : "false",
-         g_bad.load(), thr1 - thr0, us1 - us0);
+         g_bad.load(), thr1 - thr0, us1 - us0, el * 1e3, user_ms, sys_ms, nvcsw, nivcsw);
   bh_shutdown();
   return g_bad.load() ? 1 : 0;
 }
