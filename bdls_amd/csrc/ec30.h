@@ -48,8 +48,7 @@ BH_HD void j_dbl(J30& r, const J30& p) {
     // Z3 = (Y + Z)^2 - gamma - delta
     f_add(t0, p.Y, p.Z);                  // [bY+bZ]
     f_sqr<F>(t0, t0);                     // [b2]
-    f_add(t1, gamma, delta);              // [b4]
-    f_sub<F, 32>(r.Z, t0, t1);            // [b34]
+    f_sub2<F, 32>(r.Z, t0, gamma, delta); // [b34] (one pass)
     // X3 = alpha^2 - 8 beta
     f_sqr<F>(u, alpha);                   // [b2]  36
     f_mulc<8>(t0, bt);                    // [b16]
@@ -106,8 +105,7 @@ BH_HD void j_dblu(J30& r, J30& pp, const J30& p) {
     f_mulc<3>(alpha, u);                  // [b6]
     f_add(t0, p.Y, p.Z);                  // [bY+bZ]
     f_sqr<F>(t0, t0);                     // [b2]
-    f_add(t1, gamma, delta);              // [b4]
-    f_sub<F, 32>(r.Z, t0, t1);            // [b34]  2YZ
+    f_sub2<F, 32>(r.Z, t0, gamma, delta); // [b34]  2YZ (one pass)
     f_sqr<F>(u, alpha);                   // [b2]
     f_mulc<8>(t0, bt);                    // [b16]
     f_sub<F, 32>(r.X, u, t0);             // [b34]
@@ -240,8 +238,9 @@ BH_HD bool j_add_co(J30& r, J30& pz, const J30& p, const J30& q, bool* same_y, b
 }
 
 // r = p + (x2, +-y2, 1) (mixed; neg adds (x2, -y2)). Requires beta <= 63 on X1
-// (and on Y1 when !neg, <= 62 when neg: the sign pass needs S2 + Y1 <= 64 p),
-// beta(Z1) <= 34, beta(x2), beta(y2) <= 64. Output beta (34, 34, 2); with CO, pz = (X1 H^2, Y1 H^3, Z3) beta
+// and beta <= 94 on Y1 (the sign pass needs S2 + Y1 <= 96 p; a point whose y
+// was negated by f_neg<64> has beta 64), beta(Z1) <= 34, beta(x2),
+// beta(y2) <= 64. Output beta (34, 34, 2); with CO, pz = (X1 H^2, Y1 H^3, Z3) beta
 // (2, 2, 2) (j_madd_co: the composite 2 p + q = (p + q) + p). Degenerate
 // contract as j_add_impl; r may alias p.
 template <class F, bool CO>
@@ -253,15 +252,16 @@ BH_HD bool j_madd_impl(J30& r, J30* pz, const J30& p, const uint32_t x2[9], cons
   f_mul<F>(t, p.Z, z1z1);                 // [b2]
   f_mul<F>(s2, y2, t);                    // [b2]
   f_sub<F, 64>(h, u2, p.X);               // [b66]
-  f_csub<F, 64>(rr, neg, s2, p.Y);        // [b66]  +-S2 - Y1
+  f_csub<F, 96>(rr, neg, s2, p.Y);        // [b98]  +-S2 - Y1 (96 p: Y1 may be a negated
+                                          // table y, < 64 p, and S2 < 2 p)
   f_sqr<F>(hh, h);                        // [b2]  4356
   f_mul<F>(hhh, hh, h);                   // [b2]
   f_mul<F>(v, p.X, hh);                   // [b2]  V = X1 H^2
-  f_sqr<F>(t, rr);                        // [b2]
+  f_sqr<F>(t, rr);                        // [b2]  9604
   f_add2x(w, hhh, v);                     // [b6]  H^3 + 2V
   f_sub<F, 32>(r.X, t, w);                // [b34] X3 = r^2 - H^3 - 2V
   f_addsub<F, 32>(s2, w, v, t);           // [b40] V - X3
-  f_mul<F>(s2, rr, s2);                   // [b2]  66*40
+  f_mul<F>(s2, rr, s2);                   // [b2]  98*40
   f_mul<F>(t, p.Y, hhh);                  // [b2]  Y1 H^3
   f_sub<F, 32>(r.Y, s2, t);               // [b34]
   f_mul<F>(r.Z, p.Z, h);                  // [b2]  34*66

@@ -274,6 +274,13 @@ static void fused(int op, const uint32_t* a, const uint32_t* b, const uint32_t* 
 }
 extern "C" void hs_f_fused(int curve, int K, int op, const uint32_t* a, const uint32_t* b,
                            const uint32_t* c, uint32_t* r) {
+  if (K == 96) {  // the mixed addition's sign pass (f_csub only)
+    if (op == 3 || op == 4) {
+      if (curve == 0) f_csub<F30_p256, 96>(r, op == 4, a, b);
+      else f_csub<F30_k1, 96>(r, op == 4, a, b);
+    }
+    return;
+  }
   if (curve == 0) (K == 32 ? fused<F30_p256, 32> : fused<F30_p256, 64>)(op, a, b, c, r);
   else (K == 32 ? fused<F30_k1, 32> : fused<F30_k1, 64>)(op, a, b, c, r);
 }

@@ -161,3 +161,20 @@ def test_fused_passes(L, curve, K):
         for y in edge_all(K - 2, p, rng, 6):
             call(curve, K, 4, to9(s_), to9(y), z, out)
             assert normalised(out) and from9(out) == K * p - s_ - y
+
+
+@pytest.mark.parametrize("curve", [0, 1])
+def test_csub_96(L, curve):
+    """f_csub<96>: the mixed addition's r = +-S2 - Y1 + 96 p with Y1 up to a
+    negated table y (64 p) -- the case a GPU edge batch caught at K = 64."""
+    p = P if curve == 0 else P_K1
+    rng = random.Random(96 + curve)
+    out = (ctypes.c_uint32 * 9)()
+    z = to9(0)
+    for s_ in edge_all(2, p, rng):
+        for y in edge_all(94, p, rng, 8):
+            L.hs_f_fused(curve, 96, 4, to9(s_), to9(y), z, out)
+            assert normalised(out) and from9(out) == 96 * p - s_ - y
+        for y in edge_all(96, p, rng, 8):
+            L.hs_f_fused(curve, 96, 3, to9(s_), to9(y), z, out)
+            assert normalised(out) and from9(out) == s_ - y + 96 * p

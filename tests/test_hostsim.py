@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from tests.conftest import ROOT, pack
+from tests.test_gpu_comb import p256_edge_batch  # noqa: F401 (fixture, shared with the GPU test)
 
 LIB = os.environ.get("HOSTSIM_LIB") or os.path.join(ROOT, "tests", "native", "build", "libhostsim.so")
 
@@ -457,3 +458,20 @@ def test_hostsim_crafted_through_registry_slots(hs, wide):
         hs.hs_set_reg(0)
     assert ncomb.value == len(recs)
     assert [int(o) for o in out] == [r[4] for r in recs]
+
+
+def test_hostsim_p256_edge_batch_llcomb(hs, p256_edge_batch):
+    """The GPU comb-route edge batch (tests/test_gpu_comb.py p256_edge_batch:
+    golden + crafted comb / window / folded-G records + filler, 40,960
+    records) through the host build of the comb path. Round 6: a GPU run of
+    this batch caught the fused sign pass (ec30.h j_madd_impl) wrapping when a
+    degenerate branch had left A.Y as a negated table y (64 p); the host
+    harness now runs the same batch on every CPU pass."""
+    arrs, want = p256_edge_batch
+    hs.hs_set_ll(1)
+    try:
+        got = run(hs, arrs, False)
+    finally:
+        hs.hs_set_ll(0)
+    bad = np.nonzero(got != want)[0]
+    assert not len(bad), [(int(i), int(got[i]), int(want[i])) for i in bad[:10]]
