@@ -26,6 +26,16 @@
 #include "bh_common.h"
 #include "curve_consts.h"
 
+// BH_ZFILTER (default 0): test limb 0 first in f_is_zero2. It saves ~50
+// VALU instructions per comb step, but the early return is divergent control
+// flow inside the hot formulas and the register allocator pays for it:
+// k_ktab_ladder 116 -> 132 VGPRs (3 waves per SIMD instead of 4; config 5's
+// ladder -6 %, the build kernel +24 % cycles), k_keycomb 88 -> 112 (round 6,
+// hipcc -S variants in DESIGN 4.8). Off.
+#ifndef BH_ZFILTER
+#define BH_ZFILTER 0
+#endif
+
 namespace bh {
 
 constexpr uint32_t kM30 = 0x3fffffffu;
@@ -342,12 +352,13 @@ BH_HD bool f_eq(const uint32_t a[9], const uint32_t b[9]) {
 }
 
 // beta <= 2 and normalised: value == 0 mod p  <=>  a in {0, p}
-// (round 6: limb 0 filters first -- a value in {0, p} has limb 0 in {0, p_0} --
-// so the hot formulas' degenerate checks cost a compare, and the full test
-// runs only in the branch the lanes almost never take)
+// (BH_ZFILTER: limb 0 filters first -- a value in {0, p} has limb 0 in
+// {0, p_0} -- measured and left off, see its definition)
 template <class F>
 BH_HD bool f_is_zero2(const uint32_t a[9]) {
+#if BH_ZFILTER
   if (a[0] != 0u && a[0] != F::p[0]) return false;
+#endif
   uint32_t z = 0, q = 0;
 #pragma unroll
   for (int i = 0; i < 9; i++) {

@@ -1952,6 +1952,9 @@ BH_HD bool stage_keycomb_fold(const Work& w, uint32_t i, const uint32_t* tab, ui
 // addition's r pass; T.Y is negated in place only on the rare branches that
 // use T itself), degenerate cases as ll_dbladd: A at infinity -> T; A == T -> 3 T; A == -T -> A (unchanged);
 // A + T == -A -> infinity.
+#ifndef BH_LADDER_CSUB
+#define BH_LADDER_CSUB 1
+#endif
 template <class P>
 BH_HD void j_dbladd(J30& A, bool& a_inf, J30& T, bool neg) {
   if (a_inf) {  // rare: 2 inf + T
@@ -2055,7 +2058,12 @@ BH_HD void q_ladder_odd_g(J30& A, bool& a_inf, const Work& w, uint32_t i, uint32
       j_dbl<P>(A, A);  // (while a_inf, A is a placeholder the next point replaces)
       if (g_fold_pos(5 * win + 5 - d)) g_add();
     }
+#if BH_LADDER_CSUB
     j_dbladd<P>(A, a_inf, T, neg);
+#else
+    if (neg) f_neg<P, 64>(T.Y, T.Y);
+    j_dbladd<P>(A, a_inf, T, false);
+#endif
     if (g_fold_pos(5 * win)) g_add();
   }
 }

@@ -512,8 +512,22 @@ constexpr uint32_t kWaveTimes = 65536;
 __device__ unsigned long long g_wave_t[kWaveTimes * 4];
 #endif
 
+// BH_KTAB_WAVES (default 0 = the compiler's choice): occupancy floor for
+// k_ktab_ladder, waves per SIMD. Round 6 found the kernel at 132 VGPRs (3
+// waves per SIMD; config 5's ladder -6 %) and the cause in BH_ZFILTER; with
+// the filter off it is back at 116 (4 waves). A floor of 4 on the 132-VGPR
+// code spilled 344 VGPRs to scratch, so it stays a switch, not a default.
+#ifndef BH_KTAB_WAVES
+#define BH_KTAB_WAVES 0
+#endif
+#if BH_KTAB_WAVES > 0
+#define BH_KTAB_ATTR __attribute__((amdgpu_waves_per_eu(BH_KTAB_WAVES)))
+#else
+#define BH_KTAB_ATTR
+#endif
 template <class P>
-__global__ __launch_bounds__(256) void k_ktab_ladder(Work w, Plan pl, KeyReg g,
+__global__ __launch_bounds__(256) BH_KTAB_ATTR
+void k_ktab_ladder(Work w, Plan pl, KeyReg g,
                                                      const uint32_t* __restrict__ gtab,
                                                      uint8_t* __restrict__ reason,
                                                      uint32_t tab_blocks,
