@@ -181,6 +181,7 @@ struct Slot {
   // library-owned page-locked memory, reused batch after batch -- keys, key
   // indices and lengths; signature and message bytes
   HostBuf pk_small, pk_bytes;
+  HostBuf co_in;  // Uploader's gathered small arrays (batches up to kCoalesceMax bytes)
   bh_job* owner = nullptr;  // job whose results are in flight / sit in host_out
   size_t owner_part = 0;
 };
@@ -732,19 +733,44 @@ struct Uploader {
   bool marked = false;
   size_t used = 0;
   hipError_t err = hipSuccess;
+  // Round 6: small arrays (<= co_max bytes) are gathered on the host into
+  // page-locked staging `co` (same layout as `base`) and go up as ONE copy
+  // per contiguous run; larger arrays are copied directly. A latency batch's
+  // upload was one hipMemcpyAsync per array -- 7 to 11 of them from pageable
+  // memory, ~6 us of API time each, on the critical path ahead of the first
+  // kernel (config 4: 80 us of a 0.49 ms call; rocprofv3 --hip-trace,
+  // profiles/r06/lat). flush() must end the upload (mark() flushes too).
+  char* co = nullptr;
+  size_t co_max = 0;
+  size_t run_lo = 0, run_hi = 0;  // pending gathered run [run_lo, run_hi) (empty: equal)
+  void flush() {
+    if (run_hi > run_lo && err == hipSuccess)
+      err = hipMemcpyAsync(base + run_lo, co + run_lo, run_hi - run_lo, hipMemcpyHostToDevice, s);
+    run_lo = run_hi = 0;
+  }
   // the arrays queued so far are the pass's key half (keys and lengths)
   void mark() {
+    flush();
     if (!mark_ev || err != hipSuccess) return;
     err = hipEventRecord(mark_ev, s);
     marked = err == hipSuccess;
   }
   template <class T>
   const T* put(const T* src, size_t count) {
-    char* dst = base + used;
+    const size_t off = used;
+    char* dst = base + off;
     const size_t bytes = count * sizeof(T);
     used += round256(bytes + 1);
-    if (bytes && src && err == hipSuccess)
-      err = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+    if (bytes && src && err == hipSuccess) {
+      if (co && bytes <= co_max) {
+        std::memcpy(co + off, src, bytes);
+        if (run_hi == run_lo) run_lo = off;  // a run spans the padding between its arrays
+        run_hi = off + bytes;
+      } else {
+        flush();
+        err = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+      }
+    }
     return (const T*)dst;
   }
   // staged bytes of v, as a pointer the caller's offsets index directly
@@ -1098,6 +1124,18 @@ int launch_part(bh_job* j, Dev& d, int k, Slot& sl, int curve, const D& db, size
   return BH_OK;
 }
 
+// Upload coalescing (Uploader::co): batches whose staging is at most
+// kCoalesceMax bytes gather their arrays of up to BH_COALESCE_BYTES (default
+// 32 KB; 0 turns it off) on the host and send each contiguous run as one copy.
+constexpr size_t kCoalesceMax = size_t(8) << 20;
+size_t coalesce_max() {
+  static const size_t v = [] {
+    const char* e = getenv("BH_COALESCE_BYTES");
+    return e ? (size_t)std::max(0L, atol(e)) : size_t(32) << 10;
+  }();
+  return v;
+}
+
 // Enqueue shard [lo, lo + m) on device d (caller holds d.mu).
 template <class B>
 int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, uint32_t flags) {
@@ -1116,7 +1154,13 @@ int enqueue_part(bh_job* j, Dev& d, int curve, const B* b, size_t lo, size_t m, 
   // signatures and messages upload (BH_KEYS_FIRST=0: wait for the whole shard)
   if (keys_first_ok(b) && !(flags & BH_F_KEEP_KEYS) && m <= max_chunk() && keys_first())
     u.mark_ev = sl.keys_up;
+  if (f.bytes <= kCoalesceMax && coalesce_max() > 0) {  // latency-sized batches
+    if ((rc = sl.co_in.ensure(f.bytes + 4096))) return rc;
+    u.co = (char*)sl.co_in.p;
+    u.co_max = coalesce_max();
+  }
   const auto db = upload(u, b, lo, m, f);
+  u.flush();
   HIPCHK(u.err);
   HIPCHK(hipEventRecord(sl.uploaded, d.copy));
   return launch_part(j, d, k, sl, curve, db, lo, m, flags, u.marked);
@@ -1197,6 +1241,7 @@ int enqueue_staged(bh_job* j, Dev& d, int curve, const Src& src, size_t lo, size
   if ((rc = sl.host_out.ensure(out_bytes))) return rc;
   Uploader u{(char*)sl.stage.p, d.copy, &sl.host_in};
   const CompactDev db = upload(u, &h, 0, m, f);
+  u.flush();
   HIPCHK(u.err);
   uint8_t* dsig = const_cast<uint8_t*>(db.b.sig);
   uint8_t* dmsg = const_cast<uint8_t*>(db.b.msg);

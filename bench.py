@@ -1218,6 +1218,20 @@ def single_verify_measure(L, threads_list=(1, 8, 64, 256)) -> dict:
                 res = json.loads(r.stdout.strip().splitlines()[-1])
                 ok = ok and res["bad"] == 0
                 out[f"{mode}_{nth}thr"] = res
+        # the same 256 registered callers confined to the CPUs the cgroup
+        # quota grants (csp_load's cpus argument: the cpuset of a peer pinned
+        # to its CPU limit). Unconfined, their wake-ups cost ~48 us of system
+        # time each on a 256-CPU box and can trip the quota.
+        cpus = host_cpus()
+        usable = int(min(cpus.get("affinity", cpus["nproc"]),
+                         cpus.get("cgroup_quota_cpus", cpus["nproc"]))) or 1
+        if 256 in threads_list and usable < cpus.get("affinity", cpus["nproc"]):
+            r = subprocess.run([tool, path, "256", str(max(16, min(400, 8192 // 256))), "1",
+                                str(usable)], capture_output=True, text=True, timeout=120)
+            if r.returncode in (0, 1) and r.stdout.strip():
+                res = json.loads(r.stdout.strip().splitlines()[-1])
+                ok = ok and res["bad"] == 0
+                out["registered_256thr_cpuset"] = res
     finally:
         os.unlink(path)
     m = 512

@@ -14,7 +14,8 @@ threads = tuple(int(x) for x in sys.argv[1:]) or (1, 8, 64, 256)
 out = bench.single_verify_measure(None, threads)
 keep = {k: {f: v.get(f) for f in ("p50_us", "p99_us", "p999_us", "max_us", "verifies_per_s",
                                    "cgroup_nr_throttled", "cgroup_throttled_us", "bad", "wall_ms",
-                                   "cpu_user_ms", "cpu_sys_ms", "vol_csw", "invol_csw")}
+                                   "cpu_user_ms", "cpu_sys_ms", "vol_csw", "invol_csw",
+                                   "cpus_pinned")}
         for k, v in out.items() if isinstance(v, dict) and "p50_us" in v}
 keep["env"] = {k: v for k, v in os.environ.items() if k.startswith("BH_")}
 print(json.dumps(keep))
