@@ -31,6 +31,7 @@
 // public key; an identity this code cannot resolve is reported as such and
 // left to the Go path (the verified set never claims what it did not check).
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
@@ -1043,7 +1044,7 @@ void resolve_tx(TxRec* t, SdEntry* ends, IdentMemo& memo) {
 
 // Small persistent worker pool for the block decode (parallel_for over chunk
 // indices; the calling thread takes chunks too). Size: BH_DECODE_THREADS, else
-// min(4, hardware threads) -- the peer's validator shares the host.
+// 1 (measured below) -- the peer's validator shares the host.
 class Pool {
  public:
   static Pool& get() {
@@ -1057,24 +1058,29 @@ class Pool {
       return;
     }
     std::unique_lock<std::mutex> call(call_mu_);  // one parallel_for at a time
+    uint64_t g;
     {
-      std::lock_guard<std::mutex> g(mu_);
-      fn_ = &fn;
-      next_ = 0;
-      tasks_ = tasks;
-      left_ = tasks;
-      gen_++;
+      std::lock_guard<std::mutex> l(mu_);
+      fn_.store(&fn, std::memory_order_relaxed);
+      tasks_.store(tasks, std::memory_order_relaxed);
+      left_.store(tasks, std::memory_order_relaxed);
+      g = ++gen_;
+      claim_.store(g << 32, std::memory_order_release);
     }
     cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> g(mu_);
-    done_cv_.wait(g, [&] { return left_ == 0; });
-    fn_ = nullptr;
+    work(g);
+    std::unique_lock<std::mutex> l(mu_);
+    done_cv_.wait(l, [&] { return left_.load(std::memory_order_acquire) == 0; });
+    fn_.store(nullptr, std::memory_order_relaxed);
   }
 
  private:
   Pool() {
-    size_t n = std::min<size_t>(4, std::max(1u, std::thread::hardware_concurrency()));
+    // default 1 (round 6, tools/r6_dec.sh on the box, decode-only p50 of the
+    // config-3 block: 1 thread 0.25 ms, 2 / 4 / 8 threads 0.31-0.40 /
+    // 0.17-0.37 / 0.37-0.53 ms -- waking workers across the box's 256 CPUs
+    // costs more than the ~13 us chunks they would take)
+    size_t n = 1;
     if (const char* e = getenv("BH_DECODE_THREADS")) n = std::max(1L, std::min(64L, atol(e)));
     for (size_t k = 1; k < n; k++) th_.emplace_back([this] { loop(); });
     for (auto& t : th_) t.detach();
@@ -1083,33 +1089,43 @@ class Pool {
     uint64_t seen = 0;
     for (;;) {
       {
-        std::unique_lock<std::mutex> g(mu_);
-        cv_.wait(g, [&] { return gen_ != seen; });
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return gen_ != seen; });
         seen = gen_;
       }
-      work();
+      work(seen);
     }
   }
-  void work() {
+  // Round 6: a chunk is claimed with one compare-exchange on a word that
+  // carries the run's generation (high half) and the next chunk (low half);
+  // the mutex per claim before made the workers queue on futexes, and on the
+  // box's 256 CPUs a futex hand-off costs tens of microseconds of a ~200 us
+  // decode. A worker that wakes late sees another generation (or no chunk
+  // left) and claims nothing -- it never consumes a later run's chunk nor
+  // runs a finished run's function.
+  void work(uint64_t g) {
     for (;;) {
+      uint64_t c = claim_.load(std::memory_order_acquire);
       size_t k;
-      const std::function<void(size_t)>* fn;
-      {
-        std::lock_guard<std::mutex> g(mu_);
-        if (!fn_ || next_ >= tasks_) return;
-        k = next_++;
-        fn = fn_;
+      do {
+        if ((c >> 32) != g) return;
+        k = (size_t)(c & 0xffffffffu);
+        if (k >= tasks_.load(std::memory_order_relaxed)) return;
+      } while (!claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel,
+                                             std::memory_order_acquire));
+      (*fn_.load(std::memory_order_relaxed))(k);  // run g is still open: its fn
+      if (left_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        std::lock_guard<std::mutex> l(mu_);
+        done_cv_.notify_all();
       }
-      (*fn)(k);
-      std::lock_guard<std::mutex> g(mu_);
-      if (--left_ == 0) done_cv_.notify_all();
     }
   }
   std::vector<std::thread> th_;
   std::mutex mu_, call_mu_;
   std::condition_variable cv_, done_cv_;
-  const std::function<void(size_t)>* fn_ = nullptr;
-  size_t next_ = 0, tasks_ = 0, left_ = 0;
+  std::atomic<const std::function<void(size_t)>*> fn_{nullptr};
+  std::atomic<size_t> tasks_{0}, left_{0};
+  std::atomic<uint64_t> claim_{0};
   uint64_t gen_ = 0;
 };
 
