@@ -780,7 +780,12 @@ __global__ __launch_bounds__(256) void k_reg_publish(Work w, Plan pl, KeyReg g) 
 #ifndef BH_KEYCOMB_LDS
 #define BH_KEYCOMB_LDS 1
 #endif
-constexpr uint32_t kLdsTabs = (17u * 64u) / kLLEnt;  // 78 KB of slots: 17 at 7 teeth, 8 at 8
+// BH_LDS_TABS: slots per workgroup (default 17 at 7 teeth: 78 KB, two
+// workgroups per CU)
+#ifndef BH_LDS_TABS
+#define BH_LDS_TABS ((17u * 64u) / kLLEnt)
+#endif
+constexpr uint32_t kLdsTabs = BH_LDS_TABS;  // 78 KB of slots: 17 at 7 teeth, 8 at 8
 constexpr uint32_t kLdsTabWords = kLLEnt * kLLLds;
 template <class P>
 __global__ __launch_bounds__(256) BH_KEYCOMB_ATTR void k_keycomb(Work w, Plan pl, KeyReg g,

@@ -589,3 +589,42 @@ def test_gpu_two_phase_implicit_meta_one_device_batch(classes_block, which):
                         lambda sd: fabric.preverify_sets(empty, [sd], min_batch=1),
                         [o.status for o in got])
         assert _lib.device_stats()[0] - b3 == n_eval
+
+
+_DECODE_SCRIPT = r"""
+import json, sys
+sys.path.insert(0, sys.argv[1])
+from bdls_amd import fabric
+from bdls_amd.workload import fabric as F
+from tests.test_fabric import _got
+out = []
+for seed, kw in ((7, dict(ntx=2 * len(F.CORRUPTIONS), corrupt_den=0, classes=F.CORRUPTIONS)),
+                 (3, {})):
+    fb = F.generate_fabric_block(seed=seed, **kw)
+    for _ in range(3):  # the pool reused call after call
+        out.append([list(map(str, _got(o))) for o in fabric.block_preverify(fb.block,
+                                                                            decode_only=True)])
+print(json.dumps(out))
+"""
+
+
+def test_parallel_decode_matches_serial():
+    """The block decode's worker pool (fabric.cpp Pool: generation-tagged
+    chunk claims, per-chunk identity memos; one thread by default since round
+    6) gives the same per-transaction outcome at 1, 2, 4 and 8 threads, on the
+    every-class block and on a config-3 block, three calls each in one
+    process. Subprocesses: the pool size is read once per process."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    outs = {}
+    for t in (1, 2, 4, 8):
+        env = dict(os.environ, BH_DECODE_THREADS=str(t))
+        r = subprocess.run([sys.executable, "-c", _DECODE_SCRIPT, ROOT], env=env, cwd=ROOT,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[t] = json.loads(r.stdout.strip().splitlines()[-1])
+    for t in (2, 4, 8):
+        assert outs[t] == outs[1]
