@@ -163,11 +163,14 @@ constexpr int kQRot1 = 0x39;  // quad_perm [1,2,3,0]: lane c reads lane c+1
 constexpr int kQRot2 = 0x4E;  // [2,3,0,1]
 constexpr int kQRot3 = 0x93;  // [3,0,1,2]
 
+// (mov_dpp: no `old` operand -- a quad permutation reads a valid lane for
+// every lane, and update_dpp's old = 0 cost a v_mov of 0 into every DPP
+// destination first, 12 per round; round 6, hipcc -S of k_bdls_hash)
 template <int CTRL>
 __device__ __forceinline__ uint64_t qperm(uint64_t x) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xf, 0xf, false);
-  const uint32_t hi =
-      (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, 0xf, 0xf, false);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xf, 0xf, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xf, 0xf,
+                                                         true);
   return ((uint64_t)hi << 32) | lo;
 }
 
