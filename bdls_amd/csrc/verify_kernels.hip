@@ -1345,10 +1345,11 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
       return hipGetLastError();
     }
   }
-  if ((e = plan_reset(pl, s))) return e;
-  REC(0);
   // digests: on the second stream when there is one (forked here, joined
-  // before the first kernel that needs u1), else first on this stream
+  // before the first kernel that needs u1), else first on this stream. The
+  // fork and the digest launch come before the plan reset (round 6): on a
+  // latency call the digest chain is the critical path, and every host
+  // launch ahead of it delays it by the launch's API time.
   bool joined = true;
   hipStream_t hs = s;
   if ((kBdls || split) && o.aux) {
@@ -1360,24 +1361,27 @@ static hipError_t seq(const IN& in, const Work& w, const Plan& pl, const KeyReg&
   if constexpr (kBdls) {
     hipLaunchKernelGGL((k_bdls_hash<C>), dim3((n * 4 + 255) / 256), blk, 0, hs, in, w, n);
     if (!joined && (e = hipEventRecord((hipEvent_t)o.ev_join, hs))) return e;
-    hipLaunchKernelGGL((k_prep<P, N, C, BdlsIn, 0>), grd, blk, 0, s, in, w, n);
   } else if (split) {
     if (in.flags & BHF_HASH_SHA3_256) {
       hipLaunchKernelGGL((k_digest<C, HK_SHA3_256>), grd, blk, 0, hs, in, w, n);
-      if (!joined && (e = hipEventRecord((hipEvent_t)o.ev_join, hs))) return e;
-      hipLaunchKernelGGL((k_prep<P, N, C, BatchIn, HK_SHA3_256, true>), grd, blk, 0, s, in, w, n);
     } else if ((in.flags & BHF_HASH_SHA256) && digest_grp()) {
       hipLaunchKernelGGL((k_digest_grp<C>), dim3((n * kDigG + kDigBlock - 1) / kDigBlock),
                          dim3(kDigBlock), 0, hs, in, w, n);
-      if (!joined && (e = hipEventRecord((hipEvent_t)o.ev_join, hs))) return e;
-      hipLaunchKernelGGL((k_prep<P, N, C, BatchIn, HK_GIVEN_OR_SHA256, true>), grd, blk, 0, s, in,
-                         w, n);
     } else {
       hipLaunchKernelGGL((k_digest<C, HK_GIVEN_OR_SHA256>), grd, blk, 0, hs, in, w, n);
-      if (!joined && (e = hipEventRecord((hipEvent_t)o.ev_join, hs))) return e;
+    }
+    if (!joined && (e = hipEventRecord((hipEvent_t)o.ev_join, hs))) return e;
+  }
+  if ((e = plan_reset(pl, s))) return e;
+  REC(0);
+  if constexpr (kBdls) {
+    hipLaunchKernelGGL((k_prep<P, N, C, BdlsIn, 0>), grd, blk, 0, s, in, w, n);
+  } else if (split) {
+    if (in.flags & BHF_HASH_SHA3_256)
+      hipLaunchKernelGGL((k_prep<P, N, C, BatchIn, HK_SHA3_256, true>), grd, blk, 0, s, in, w, n);
+    else
       hipLaunchKernelGGL((k_prep<P, N, C, BatchIn, HK_GIVEN_OR_SHA256, true>), grd, blk, 0, s, in,
                          w, n);
-    }
   } else {
     launch_prep<P, N, C>(in, w, n, grd, blk, s);
   }
