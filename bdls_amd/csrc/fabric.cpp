@@ -1331,6 +1331,22 @@ extern "C" int bh_verify_x509(const uint8_t* certs, const uint64_t* cert_off,
   return BH_OK;
 }
 
+// The block's H2D queued while it is decoded (bdls_hip.cpp, "pre-staged block
+// spans"): library-internal, hidden.
+extern "C" int bhi_prestage_begin(const uint8_t* p, size_t len);
+extern "C" void bhi_prestage_wait();
+extern "C" void bhi_prestage_end();
+struct Prestage {
+  int on;
+  Prestage(const uint8_t* p, size_t n, bool want) : on(want ? bhi_prestage_begin(p, n) : 0) {}
+  void wait() const {
+    if (on) bhi_prestage_wait();
+  }
+  ~Prestage() {
+    if (on) bhi_prestage_end();
+  }
+};
+
 static int block_preverify(const uint8_t* block, size_t len, uint32_t flags, bh_fab_tx* txs,
                            size_t tx_cap, size_t* n_tx, uint8_t* endorse, size_t endorse_cap,
                            size_t* n_endorse, bh_fab_sigref* refs, size_t ref_cap,
@@ -1343,6 +1359,8 @@ static int block_preverify(const uint8_t* block, size_t len, uint32_t flags, bh_
   // tools/r6_dec.sh; off by default)
   static const bool timing = getenv("BH_FAB_TIMING") != nullptr;
   const auto T0 = std::chrono::steady_clock::now();
+  // the block goes up while it is decoded (round 6; not for decode-only calls)
+  const Prestage pre(block, len, !(flags & BH_FAB_F_DECODE_ONLY));
   std::vector<Span> data;
   if (!dec_block(Span{block, len, true}, &data))
     return bh::host_fail(BH_E_INVALID, "block does not unmarshal (common.Block)");
@@ -1379,6 +1397,7 @@ static int block_preverify(const uint8_t* block, size_t len, uint32_t flags, bh_
     sets.push_back(SetRange{x.end_first, x.end_count});
   }
   std::vector<uint32_t> valid;
+  pre.wait();  // its H2D is queued: the batch's upload indexes the device copy
   const auto T3 = std::chrono::steady_clock::now();
   if (int rc = verify_sets(ends, sets, verify_flags(flags), decode_only, &valid, &creators))
     return rc;
