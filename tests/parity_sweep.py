@@ -11,7 +11,8 @@ of the routing rules: the small-batch kernels, the 32,768-record wide/comb
 boundary, key-table thresholds), distinct keys, message length, corruption
 rate, SHA-256 or SHA3-256 family -- generates it with workload/gen.c (which
 knows every record's expected reason) and runs it through the host ABI
-(bh_verify, bh_verify_compact) and the device ABI (bh_verify_dev). Every
+(bh_verify, bh_verify_compact), the staged BatchVerify (bh_batch_verify, round
+6) and the device ABI (bh_verify_dev). Every
 bitmap bit and reason byte must equal the construction's; a 50-record sample
 per case is re-checked against oracle/orc.c (OpenSSL's ECDSA core).
 """
@@ -67,6 +68,12 @@ def main():
         _lib.check(L.bh_verify_compact(0, ctypes.byref(cb), n, flag, bm2.ctypes.data,
                                        rs2.ctypes.data))
         res["compact"] = bool((rs2 == w.reason).all() and (bits_of(bm2, n) == w.expected_valid).all())
+        # staged BatchVerify from the same pageable arrays (pack.h: the library
+        # dedups and packs into its own page-locked staging)
+        bm3 = np.zeros((n + 7) // 8, np.uint8)
+        rs3 = np.zeros(n, np.uint8)
+        _lib.check(L.bh_batch_verify(0, ctypes.byref(b), n, flag, bm3.ctypes.data, rs3.ctypes.data))
+        res["staged"] = bool((rs3 == w.reason).all() and (bits_of(bm3, n) == w.expected_valid).all())
         # device ABI
         DA = _lib.DeviceArray
         d = [DA.from_numpy(0, x) for x in w.arrays()]
@@ -91,7 +98,8 @@ def main():
         res["oracle_sample"] = bool(ok)
         res["valid"] = int(w.expected_valid.sum())
         res["s"] = round(time.time() - t0, 2)
-        good = res["host"] and res["compact"] and res["device"] and res["oracle_sample"]
+        good = (res["host"] and res["compact"] and res["staged"] and res["device"]
+                and res["oracle_sample"])
         bad += 0 if good else 1
         print(json.dumps(res), flush=True)
     print(json.dumps({"cases": cases, "failed": bad}), flush=True)
