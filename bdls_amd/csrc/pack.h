@@ -35,7 +35,6 @@
 #include <cstring>
 #include <functional>
 #include <mutex>
-#include <string>
 #include <thread>
 #include <vector>
 #ifdef __linux__
@@ -48,80 +47,13 @@
 namespace bh {
 namespace pack {
 
-// ---- worker placement (BH_PACK_SPREAD) ----------------------------------------
-// The pool's threads are woken by one caller, and the scheduler's wake-affine
-// placement tends to keep them in the caller's last-level-cache domain: on a
-// chiplet CPU one core complex, whose single link to memory then carries the
-// whole pack (round 6 probe: 8 -> 15 threads only 7.35 -> 6.34 ms per config-2
-// batch, ~100 GB/s). BH_PACK_SPREAD=1 gives worker t the CPUs of L3 domain
-// t mod D (the domains of the creating thread's package, among the CPUs this
-// process may use); 2 takes every package's domains. Off (0) by default until
-// measured; the caller's own CPU set is never narrowed.
-inline std::vector<std::vector<int>> l3_domains(int mode) {
-  std::vector<std::vector<int>> out;
-#ifdef __linux__
-  if (mode <= 0) return out;
-  cpu_set_t allowed;
-  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return out;
-  auto read_str = [](int cpu, const char* leaf) {
-    char path[128], buf[256] = {0};
-    std::snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/%s", cpu, leaf);
-    if (FILE* f = std::fopen(path, "r")) {
-      if (!std::fgets(buf, sizeof(buf), f)) buf[0] = 0;
-      std::fclose(f);
-    }
-    return std::string(buf);
-  };
-  const int self = sched_getcpu();
-  const std::string pkg = self >= 0 ? read_str(self, "topology/physical_package_id") : "";
-  std::vector<std::string> keys;
-  for (int c = 0; c < CPU_SETSIZE; c++) {
-    if (!CPU_ISSET(c, &allowed)) continue;
-    if (mode == 1 && !pkg.empty() && read_str(c, "topology/physical_package_id") != pkg) continue;
-    const std::string k = read_str(c, "cache/index3/shared_cpu_list");
-    if (k.empty()) continue;
-    size_t g = 0;
-    while (g < keys.size() && keys[g] != k) g++;
-    if (g == keys.size()) {
-      keys.push_back(k);
-      out.emplace_back();
-    }
-    out[g].push_back(c);
-  }
-  if (out.size() < 2) out.clear();  // one domain: nothing to spread over
-#else
-  (void)mode;
-#endif
-  return out;
-}
-
-inline int spread_mode() {
-  static const int m = [] {
-    const char* e = getenv("BH_PACK_SPREAD");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
-}
-
 // ---- worker pool -------------------------------------------------------------
 // Persistent threads; run(fn) calls fn(t) for t in [0, threads) on the workers
 // and returns when all are done. One job at a time (callers serialise).
 class Pool {
  public:
   explicit Pool(int threads) : n_(std::max(1, threads)) {
-    const std::vector<std::vector<int>> dom = l3_domains(spread_mode());
-    for (int t = 0; t < n_; t++)
-      th_.emplace_back([this, t, d = dom.empty() ? std::vector<int>() : dom[t % dom.size()]] {
-#ifdef __linux__
-        if (!d.empty()) {
-          cpu_set_t s;
-          CPU_ZERO(&s);
-          for (int c : d) CPU_SET(c, &s);
-          (void)sched_setaffinity(0, sizeof(s), &s);  // this worker only
-        }
-#endif
-        loop(t);
-      });
+    for (int t = 0; t < n_; t++) th_.emplace_back([this, t] { loop(t); });
   }
   ~Pool() {
     {

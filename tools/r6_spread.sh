@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 6: packer worker placement A/B (pack.h BH_PACK_SPREAD) on one GPU box.
+# Round 6: packer worker placement A/B (BH_PACK_SPREAD: pack.h as of commit
+# 62712ff; the switch was measured and removed) on one GPU box.
 # (1) tools/pack_bench.py (the packer alone, CPU) at 8 and 15 threads for each
 # mode; (2) the default bench line's host_path_e2e for each mode, two passes.
 # Every step has its own limit; a failure stops the script.
