@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cctype>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -1247,10 +1248,72 @@ struct SrcPtrs {
   uint32_t msg_len(size_t i) const { return b->msg[i] ? b->msg_len[i] : 0u; }
 };
 
+// The CPUs of device dev's NUMA node that this process may run on (the PCI
+// function's numa_node in sysfs); false when unknown or when the node has none
+// of our CPUs.
+bool device_node_cpus(int dev, cpu_set_t* out) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) return false;
+  for (char* c = bus; *c; c++) *c = (char)tolower((unsigned char)*c);
+  auto read_line = [](const std::string& path, char* buf, int n) {
+    FILE* f = std::fopen(path.c_str(), "r");
+    if (!f) return false;
+    const bool ok = std::fgets(buf, n, f) != nullptr;
+    std::fclose(f);
+    return ok;
+  };
+  char line[4096];
+  if (!read_line(std::string("/sys/bus/pci/devices/") + bus + "/numa_node", line, sizeof(line)))
+    return false;
+  const int node = atoi(line);
+  if (node < 0 ||
+      !read_line("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist", line,
+                 sizeof(line)))
+    return false;
+  cpu_set_t allowed;
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return false;
+  CPU_ZERO(out);
+  for (char* p = line; *p && *p != '\n';) {  // "a-b,c,d-e"
+    char* e;
+    const long a = strtol(p, &e, 10);
+    long b = a;
+    if (e == p) break;
+    if (*e == '-') b = strtol(e + 1, &e, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; c++)
+      if (c >= 0 && CPU_ISSET((int)c, &allowed)) CPU_SET((int)c, out);
+    p = *e == ',' ? e + 1 : e;
+  }
+  return CPU_COUNT(out) > 0;
+}
+
+// Round 6 (profiles/r06/numa): the staged BatchVerify's packer writes the
+// page-locked staging the GPU's DMA reads; with its workers spread over both
+// sockets of a 2-socket host the whole process got 100 M verifies/s end to end,
+// confined to the GPU's socket 141 M (the other socket 125 M). The worker
+// threads are therefore created on the CPUs of the first staging device's
+// NUMA node: they inherit the creating thread's affinity, which is narrowed
+// for the constructor only and restored (the caller's own placement is never
+// changed). BH_PACK_NUMA=0 keeps the inherited placement.
+bool pack_numa_on() {
+  static const bool on = [] {
+    const char* e = getenv("BH_PACK_NUMA");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 // one packer (worker pool) per process; one staged shard packs at a time
 std::mutex g_pack_mu;
-bh::pack::Packer& packer() {
-  static bh::pack::Packer* p = new bh::pack::Packer(bh::pack::default_threads());
+bh::pack::Packer& packer(int dev) {
+  static bh::pack::Packer* p = [dev] {
+    cpu_set_t old, node;
+    const bool narrow = pack_numa_on() && sched_getaffinity(0, sizeof(old), &old) == 0 &&
+                        device_node_cpus(dev, &node) &&
+                        sched_setaffinity(0, sizeof(node), &node) == 0;
+    auto* q = new bh::pack::Packer(bh::pack::default_threads());
+    if (narrow) (void)sched_setaffinity(0, sizeof(old), &old);
+    return q;
+  }();
   return *p;
 }
 struct PackStats {
@@ -1278,7 +1341,7 @@ int enqueue_staged(bh_job* j, Dev& d, int curve, const Src& src, size_t lo, size
   bh::pack::Out out{(uint8_t*)hs, (uint32_t*)(hs + o_idx), (uint32_t*)(hs + o_slen),
                     (uint32_t*)(hs + o_mlen)};
   std::lock_guard<std::mutex> pg(g_pack_mu);
-  bh::pack::Packer& P = packer();
+  bh::pack::Packer& P = packer(d.id);
   bh::pack::Result r;
   P.plan(src, lo, m, &r);
   const size_t o_msg = round256(r.sig_bytes + 1);
