@@ -11,8 +11,8 @@ of the routing rules: the small-batch kernels, the 32,768-record wide/comb
 boundary, key-table thresholds), distinct keys, message length, corruption
 rate, SHA-256 or SHA3-256 family -- generates it with workload/gen.c (which
 knows every record's expected reason) and runs it through the host ABI
-(bh_verify, bh_verify_compact), the staged BatchVerify (bh_batch_verify, round
-6) and the device ABI (bh_verify_dev). Every
+(bh_verify, bh_verify_compact), the staged BatchVerify (bh_batch_verify and
+bh_batch_verify_ptrs, round 6) and the device ABI (bh_verify_dev). Every
 bitmap bit and reason byte must equal the construction's; a 50-record sample
 per case is re-checked against oracle/orc.c (OpenSSL's ECDSA core).
 """
@@ -74,6 +74,19 @@ def main():
         rs3 = np.zeros(n, np.uint8)
         _lib.check(L.bh_batch_verify(0, ctypes.byref(b), n, flag, bm3.ctypes.data, rs3.ctypes.data))
         res["staged"] = bool((rs3 == w.reason).all() and (bits_of(bm3, n) == w.expected_valid).all())
+        # ... and its per-record pointer form (the Go binding's bh_pbatch)
+        kp = (w.pub.ctypes.data + 64 * np.arange(n, dtype=np.uint64)).astype(np.uint64)
+        sp = (w.sig.ctypes.data + w.sig_off[:n]).astype(np.uint64)
+        mp = (w.msg.ctypes.data + w.msg_off[:n]).astype(np.uint64)
+        sl = np.ascontiguousarray(w.sig_len[:n])
+        ml = np.ascontiguousarray(w.msg_len[:n])
+        pb = _lib.BhPBatch(*[x.ctypes.data for x in (kp, sp, sl, mp, ml)])
+        bm4 = np.zeros((n + 7) // 8, np.uint8)
+        rs4 = np.zeros(n, np.uint8)
+        _lib.check(L.bh_batch_verify_ptrs(0, ctypes.byref(pb), n, flag, bm4.ctypes.data,
+                                          rs4.ctypes.data))
+        res["staged_ptrs"] = bool((rs4 == w.reason).all()
+                                  and (bits_of(bm4, n) == w.expected_valid).all())
         # device ABI
         DA = _lib.DeviceArray
         d = [DA.from_numpy(0, x) for x in w.arrays()]
@@ -98,7 +111,8 @@ def main():
         res["oracle_sample"] = bool(ok)
         res["valid"] = int(w.expected_valid.sum())
         res["s"] = round(time.time() - t0, 2)
-        good = (res["host"] and res["compact"] and res["staged"] and res["device"]
+        good = (res["host"] and res["compact"] and res["staged"] and res["staged_ptrs"]
+                and res["device"]
                 and res["oracle_sample"])
         bad += 0 if good else 1
         print(json.dumps(res), flush=True)
